@@ -1,0 +1,625 @@
+// vs_api.hip — the C-ABI of libvsearch.so (declared in include/vsearch.h).
+//
+// A vs_index is one device's exact flat index: library-owned row storage in HBM
+// (fp32, stride `ld` floats, zero padding), the squared norms of every row, and
+// ntotal.  It mirrors faiss::IndexFlat (faiss-cpu 1.11.0, not vendored; see
+// /root/reference/poetry.lock:866-867): add copies the caller's rows, search
+// writes caller-allocated D/I, remove_ids compacts stably.
+//
+// Concurrency follows faiss's contract (concurrent searches allowed, add/remove
+// exclusive): a shared_mutex guards the storage; per-call scratch comes from the
+// stream-ordered allocator so concurrent searches on different streams never
+// share workspace.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/vsearch.h"
+#include "vs_internal.h"
+
+using namespace vs;
+
+struct vs_index {
+  int d = 0;
+  int metric = VS_METRIC_L2;
+  int dtype = VS_DTYPE_F32;
+  int device = 0;
+  int64_t ld = 0;        // row stride in floats (multiple of kBK)
+  int64_t ntotal = 0;
+  int64_t capacity = 0;  // rows allocated (multiple of kRowPad, >= ntotal + kBQ)
+  int64_t id_base = 0;
+  float* codes = nullptr;  // [capacity][ld]
+  float* norms = nullptr;  // [capacity] squared L2 norms
+  std::shared_mutex mu;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return e == hipErrorOutOfMemory ? VS_E_OOM : VS_E_HIP;
+}
+
+#define VS_HIP(expr, what)                    \
+  do {                                        \
+    hipError_t e_ = (expr);                   \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+// Selects the index's device for the duration of a call, restoring the caller's.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Stream-ordered scratch allocation, released on scope exit (on the same stream).
+struct Scratch {
+  hipStream_t st;
+  std::vector<void*> ptrs;
+  explicit Scratch(hipStream_t s) : st(s) {}
+  hipError_t alloc(void** p, size_t bytes) {
+    *p = nullptr;
+    if (bytes == 0) return hipSuccess;
+    hipError_t e = hipMallocAsync(p, bytes, st);
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+  ~Scratch() {
+    for (void* p : ptrs) (void)hipFreeAsync(p, st);
+  }
+};
+
+// Kernel timer (measurement hook for bench.py; see vs_timer_* in vsearch.h).
+std::mutex g_timer_mu;
+bool g_timer_on = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_timer_events;
+
+struct KernelTimer {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t st;
+  explicit KernelTimer(hipStream_t s) : st(s) {
+    std::lock_guard<std::mutex> g(g_timer_mu);
+    if (!g_timer_on) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+      a = b = nullptr;
+      return;
+    }
+    (void)hipEventRecord(a, st);
+  }
+  void stop() {
+    if (!a) return;
+    (void)hipEventRecord(b, st);
+    std::lock_guard<std::mutex> g(g_timer_mu);
+    g_timer_events.emplace_back(a, b);
+    a = b = nullptr;
+  }
+};
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
+
+// Grows storage to hold `rows` rows (plus the tile slack), preserving content.
+int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
+  const int64_t need = round_up(rows + kBQ, kRowPad);
+  if (need <= idx->capacity) return VS_OK;
+  int64_t cap = std::max(need, round_up(idx->capacity + idx->capacity / 2, kRowPad));
+  float* codes = nullptr;
+  float* norms = nullptr;
+  hipError_t e = hipMalloc(&codes, (size_t)cap * idx->ld * sizeof(float));
+  if (e != hipSuccess) {
+    // retry without the growth headroom
+    cap = need;
+    e = hipMalloc(&codes, (size_t)cap * idx->ld * sizeof(float));
+    if (e != hipSuccess) return hip_fail(e, "vs: allocating row storage");
+  }
+  e = hipMalloc(&norms, (size_t)cap * sizeof(float));
+  if (e != hipSuccess) {
+    (void)hipFree(codes);
+    return hip_fail(e, "vs: allocating norm storage");
+  }
+  // zero the whole tail (tile reads past ntotal must see zeros, never NaN garbage)
+  const int64_t keep = idx->ntotal;
+  VS_HIP(hipMemsetAsync(codes + keep * idx->ld, 0, (size_t)(cap - keep) * idx->ld * sizeof(float),
+                        st),
+         "vs: zeroing storage");
+  VS_HIP(hipMemsetAsync(norms + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
+         "vs: zeroing norms");
+  if (idx->codes && keep > 0) {
+    VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->ld * sizeof(float),
+                          hipMemcpyDeviceToDevice, st),
+           "vs: copying storage");
+    VS_HIP(hipMemcpyAsync(norms, idx->norms, (size_t)keep * sizeof(float),
+                          hipMemcpyDeviceToDevice, st),
+           "vs: copying norms");
+  }
+  // In-flight searches (any stream) may still read the old storage.
+  VS_HIP(hipDeviceSynchronize(), "vs: storage growth");
+  if (idx->codes) (void)hipFree(idx->codes);
+  if (idx->norms) (void)hipFree(idx->norms);
+  idx->codes = codes;
+  idx->norms = norms;
+  idx->capacity = cap;
+  return VS_OK;
+}
+
+// Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
+// zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
+int run_topk(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq, int nq_pad,
+             int k, int64_t self0, float min_score, float* D, int64_t* I, hipStream_t st,
+             const float* xaux) {
+  // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
+  // lowest 2k-1 (key, label) entries of every partial list to be exact.
+  const int KP = mode == MODE_IP ? kp_for(std::min(2 * k - 1, VS_MAX_K)) : kp_for(k);
+  const int ntotal = (int)idx->ntotal;
+  Scratch scr(st);
+  Partials part;
+  part.KP = KP;
+
+  const bool gemv = (mode == MODE_IP || mode == MODE_L2) && self0 < 0 && nq <= kGemvMaxQ &&
+                    (size_t)kGemvMaxQ * idx->ld * sizeof(float) <= 64 * 1024;
+  if (gemv) {
+    const int gmode = mode == MODE_L2 ? MODE_L2D : MODE_IP;
+    int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
+    part.P = nblocks * 4;
+    const int nql = nq <= 2 ? nq : (nq <= 4 ? 4 : 8);
+    const size_t n = (size_t)nql * part.P * KP;
+    VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
+    KernelTimer tm(st);
+    VS_HIP(launch_gemv_topk(KP, gmode, nq, idx->codes, qbuf, idx->ld, ntotal, nblocks, part, st),
+           "vs: gemv_topk launch");
+    tm.stop();
+    VS_HIP(launch_merge_partials(gmode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+           "vs: merge launch");
+    return VS_OK;
+  }
+
+  const int nqt = nq_pad / kBQ;
+  const int ntiles = (ntotal + kBN - 1) / kBN;
+  // ~2 workgroups per CU on 256 CUs; never more splits than database tiles.
+  int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
+  part.P = 2 * nsplit;
+  const size_t n = (size_t)nq_pad * part.P * KP;
+  VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
+  KernelTimer tm(st);
+  VS_HIP(launch_gemm_topk(KP, mode, idx->codes, xaux, qbuf, qaux, idx->ld, ntotal, nq_pad, nsplit,
+                          self0, part, st),
+         "vs: gemm_topk launch");
+  tm.stop();
+  VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+         "vs: merge launch");
+  return VS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vs_last_error(void) { return g_err.c_str(); }
+
+int vs_version(void) { return 100; }
+
+int vs_device_count(int* n) {
+  if (!n) return fail(VS_E_INVALID, "vs_device_count: null output");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return hip_fail(e, "vs_device_count");
+  }
+  *n = c;
+  return VS_OK;
+}
+
+int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
+  if (!out) return fail(VS_E_INVALID, "vs_create: null output");
+  *out = nullptr;
+  if (d <= 0) return fail(VS_E_INVALID, "vs_create: d must be > 0");
+  if (metric != VS_METRIC_L2 && metric != VS_METRIC_INNER_PRODUCT)
+    return fail(VS_E_INVALID, "vs_create: metric must be METRIC_L2 or METRIC_INNER_PRODUCT");
+  if (dtype != VS_DTYPE_F32)
+    return fail(VS_E_UNSUPPORTED, "vs_create: only float32 storage is built in this version");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return fail(VS_E_HIP, "vs_create: no HIP device available");
+  if (device < 0 || device >= ndev) return fail(VS_E_INVALID, "vs_create: bad device ordinal");
+  DeviceGuard g(device);
+  if (!g.ok) return fail(VS_E_HIP, "vs_create: hipSetDevice failed");
+  // Keep freed stream-ordered scratch cached in the pool instead of returning it
+  // to the driver at every synchronisation.
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t thr = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  vs_index* idx = new vs_index();
+  idx->d = d;
+  idx->metric = metric;
+  idx->dtype = dtype;
+  idx->device = device;
+  idx->ld = round_up(d, kBK);
+  *out = idx;
+  return VS_OK;
+}
+
+int vs_destroy(vs_index* idx) {
+  if (!idx) return VS_OK;
+  {
+    DeviceGuard g(idx->device);
+    (void)hipDeviceSynchronize();
+    if (idx->codes) (void)hipFree(idx->codes);
+    if (idx->norms) (void)hipFree(idx->norms);
+  }
+  delete idx;
+  return VS_OK;
+}
+
+int vs_reserve(vs_index* idx, int64_t n) {
+  if (!idx) return fail(VS_E_INVALID, "vs_reserve: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_reserve: n < 0");
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  return ensure_capacity(idx, std::max(n, idx->ntotal), nullptr);
+}
+
+int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
+  if (!idx) return fail(VS_E_INVALID, "vs_add: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_add: n < 0");
+  if (n == 0) return VS_OK;
+  if (!x) return fail(VS_E_INVALID, "vs_add: null vectors");
+  if (idx->ntotal + n >= (int64_t)INT32_MAX - 2 * kRowPad)
+    return fail(VS_E_UNSUPPORTED, "vs_add: a shard holds fewer than 2^31 rows");
+  hipStream_t st = (hipStream_t)stream;
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  int rc = ensure_capacity(idx, idx->ntotal + n, st);
+  if (rc) return rc;
+  const hipMemcpyKind kind = (flags & VS_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  VS_HIP(hipMemcpy2DAsync(idx->codes + idx->ntotal * idx->ld, idx->ld * sizeof(float), x,
+                          (size_t)idx->d * sizeof(float), (size_t)idx->d * sizeof(float), (size_t)n,
+                          kind, st),
+         "vs_add: copying rows");
+  VS_HIP(launch_row_norms(idx->codes, idx->ld, idx->ntotal, n, idx->norms, st), "vs_add: norms");
+  // Source host buffers may be released by the caller as soon as we return.
+  VS_HIP(hipStreamSynchronize(st), "vs_add: synchronise");
+  idx->ntotal += n;
+  return VS_OK;
+}
+
+int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void* stream) {
+  if (!idx) return fail(VS_E_INVALID, "vs_add_synthetic: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_add_synthetic: n < 0");
+  if (n == 0) return VS_OK;
+  if (idx->ntotal + n >= (int64_t)INT32_MAX - 2 * kRowPad)
+    return fail(VS_E_UNSUPPORTED, "vs_add_synthetic: a shard holds fewer than 2^31 rows");
+  hipStream_t st = (hipStream_t)stream;
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  int rc = ensure_capacity(idx, idx->ntotal + n, st);
+  if (rc) return rc;
+  VS_HIP(launch_fill_synthetic(idx->codes + idx->ntotal * idx->ld, n, idx->d, idx->ld, seed, row0,
+                               st),
+         "vs_add_synthetic: fill");
+  VS_HIP(launch_row_norms(idx->codes, idx->ld, idx->ntotal, n, idx->norms, st),
+         "vs_add_synthetic: norms");
+  VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic: synchronise");
+  idx->ntotal += n;
+  return VS_OK;
+}
+
+int vs_reset(vs_index* idx) {
+  if (!idx) return fail(VS_E_INVALID, "vs_reset: null index");
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  VS_HIP(hipDeviceSynchronize(), "vs_reset");
+  if (idx->codes) (void)hipFree(idx->codes);
+  if (idx->norms) (void)hipFree(idx->norms);
+  idx->codes = nullptr;
+  idx->norms = nullptr;
+  idx->capacity = 0;
+  idx->ntotal = 0;
+  return VS_OK;
+}
+
+int vs_ntotal(const vs_index* idx, int64_t* out) {
+  if (!idx || !out) return fail(VS_E_INVALID, "vs_ntotal: null argument");
+  *out = idx->ntotal;
+  return VS_OK;
+}
+
+int vs_dim(const vs_index* idx, int* out) {
+  if (!idx || !out) return fail(VS_E_INVALID, "vs_dim: null argument");
+  *out = idx->d;
+  return VS_OK;
+}
+
+int vs_metric(const vs_index* idx, int* out) {
+  if (!idx || !out) return fail(VS_E_INVALID, "vs_metric: null argument");
+  *out = idx->metric;
+  return VS_OK;
+}
+
+int vs_dtype(const vs_index* idx, int* out) {
+  if (!idx || !out) return fail(VS_E_INVALID, "vs_dtype: null argument");
+  *out = idx->dtype;
+  return VS_OK;
+}
+
+int vs_set_id_base(vs_index* idx, int64_t id_base) {
+  if (!idx) return fail(VS_E_INVALID, "vs_set_id_base: null index");
+  if (id_base < 0) return fail(VS_E_INVALID, "vs_set_id_base: negative base");
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  idx->id_base = id_base;
+  return VS_OK;
+}
+
+int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int64_t* I,
+              int flags, void* stream) {
+  if (!idx) return fail(VS_E_INVALID, "vs_search: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_search: n < 0");
+  if (k <= 0) return fail(VS_E_INVALID, "vs_search: k must be > 0");  // faiss: FAISS_THROW_IF_NOT(k > 0)
+  if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_search: k > VS_MAX_K (64) not supported yet");
+  if (n == 0) return VS_OK;
+  if (!x || !D || !I) return fail(VS_E_INVALID, "vs_search: null buffer");
+  hipStream_t st = (hipStream_t)stream;
+  std::shared_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  if (!g.ok) return fail(VS_E_HIP, "vs_search: hipSetDevice failed");
+  const bool out_dev = (flags & VS_OUT_DEVICE) != 0;
+  const int mode = idx->metric == VS_METRIC_L2 ? MODE_L2 : MODE_IP;
+  Scratch scr(st);
+
+  float* Dd = D;
+  int64_t* Id = I;
+  if (!out_dev) {
+    VS_HIP(scr.alloc((void**)&Dd, (size_t)n * k * sizeof(float)), "vs_search: scratch");
+    VS_HIP(scr.alloc((void**)&Id, (size_t)n * k * sizeof(int64_t)), "vs_search: scratch");
+  }
+  if (idx->ntotal == 0) {
+    VS_HIP(launch_fill_empty(mode, Dd, Id, n * k, st), "vs_search: fill");
+  } else {
+    // Queries are processed in chunks so that scratch stays bounded for any n.
+    const int64_t chunk = 65536;
+    float* qbuf = nullptr;
+    float* qaux = nullptr;
+    const int64_t cmax = std::min<int64_t>(n, chunk);
+    const int64_t qrows = round_up(std::max<int64_t>(cmax, kGemvMaxQ), kBQ);
+    VS_HIP(scr.alloc((void**)&qbuf, (size_t)qrows * idx->ld * sizeof(float)), "vs_search: scratch");
+    VS_HIP(scr.alloc((void**)&qaux, (size_t)qrows * sizeof(float)), "vs_search: scratch");
+    const hipMemcpyKind kind =
+        (flags & VS_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    for (int64_t c0 = 0; c0 < n; c0 += chunk) {
+      const int64_t nc = std::min(chunk, n - c0);
+      const int64_t nq_pad = round_up(std::max<int64_t>(nc, kGemvMaxQ), kBQ);
+      VS_HIP(hipMemsetAsync(qbuf, 0, (size_t)nq_pad * idx->ld * sizeof(float), st),
+             "vs_search: zero queries");
+      VS_HIP(hipMemcpy2DAsync(qbuf, idx->ld * sizeof(float), x + c0 * idx->d,
+                              (size_t)idx->d * sizeof(float), (size_t)idx->d * sizeof(float),
+                              (size_t)nc, kind, st),
+             "vs_search: staging queries");
+      if (mode == MODE_L2)
+        VS_HIP(launch_row_norms(qbuf, idx->ld, 0, nq_pad, qaux, st), "vs_search: query norms");
+      int rc = run_topk(idx, mode, qbuf, qaux, (int)nc, (int)nq_pad, (int)k, -1, 0.0f,
+                        Dd + c0 * k, Id + c0 * k, st, idx->norms);
+      if (rc) return rc;
+    }
+  }
+  if (!out_dev) {
+    VS_HIP(hipMemcpyAsync(D, Dd, (size_t)n * k * sizeof(float), hipMemcpyDeviceToHost, st),
+           "vs_search: copy D");
+    VS_HIP(hipMemcpyAsync(I, Id, (size_t)n * k * sizeof(int64_t), hipMemcpyDeviceToHost, st),
+           "vs_search: copy I");
+    VS_HIP(hipStreamSynchronize(st), "vs_search: synchronise");
+  } else {
+    VS_HIP(hipGetLastError(), "vs_search");
+  }
+  return VS_OK;
+}
+
+int vs_reconstruct_n(vs_index* idx, int64_t i0, int64_t n, float* out, int flags, void* stream) {
+  if (!idx) return fail(VS_E_INVALID, "vs_reconstruct_n: null index");
+  if (n < 0 || i0 < 0 || i0 + n > idx->ntotal)
+    return fail(VS_E_INVALID, "vs_reconstruct_n: key out of range");  // faiss: FAISS_THROW_IF_NOT
+  if (n == 0) return VS_OK;
+  if (!out) return fail(VS_E_INVALID, "vs_reconstruct_n: null output");
+  hipStream_t st = (hipStream_t)stream;
+  std::shared_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  const hipMemcpyKind kind =
+      (flags & VS_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  VS_HIP(hipMemcpy2DAsync(out, (size_t)idx->d * sizeof(float), idx->codes + i0 * idx->ld,
+                          idx->ld * sizeof(float), (size_t)idx->d * sizeof(float), (size_t)n, kind,
+                          st),
+         "vs_reconstruct_n: copy");
+  if (!(flags & VS_OUT_DEVICE)) VS_HIP(hipStreamSynchronize(st), "vs_reconstruct_n: synchronise");
+  return VS_OK;
+}
+
+int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremoved) {
+  if (!idx) return fail(VS_E_INVALID, "vs_remove_ids: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_remove_ids: n < 0");
+  if (nremoved) *nremoved = 0;
+  if (n == 0) return VS_OK;
+  if (!ids) return fail(VS_E_INVALID, "vs_remove_ids: null ids");
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  // IDSelectorBatch semantics: membership test; duplicates and out-of-range ids
+  // are ignored.  Labels here are global (id_base applied), as faiss sees them.
+  std::vector<int64_t> rm;
+  rm.reserve((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = ids[i] - idx->id_base;
+    if (r >= 0 && r < idx->ntotal) rm.push_back(r);
+  }
+  std::sort(rm.begin(), rm.end());
+  rm.erase(std::unique(rm.begin(), rm.end()), rm.end());
+  const int64_t nrem = (int64_t)rm.size();
+  if (nrem == 0) return VS_OK;
+  DeviceGuard g(idx->device);
+  // Searches already queued on other streams read the rows we are about to move.
+  VS_HIP(hipDeviceSynchronize(), "vs_remove_ids: drain");
+  hipStream_t st = nullptr;
+  Scratch scr(st);
+  int64_t* drm = nullptr;
+  VS_HIP(scr.alloc((void**)&drm, (size_t)nrem * sizeof(int64_t)), "vs_remove_ids: scratch");
+  VS_HIP(hipMemcpyAsync(drm, rm.data(), (size_t)nrem * sizeof(int64_t), hipMemcpyHostToDevice, st),
+         "vs_remove_ids: upload");
+  // Chunked stable compaction from the first removed row on: each chunk's kept
+  // rows are packed into scratch, then copied down to their final position.
+  // Destinations never exceed the chunk's own source range, and earlier chunks
+  // are already consumed, so the in-place move is safe with O(chunk) scratch.
+  const int64_t chunk = std::max<int64_t>(1024, (int64_t)(256ull << 20) / (idx->ld * 4));
+  float* tmp = nullptr;
+  float* tmpn = nullptr;
+  VS_HIP(scr.alloc((void**)&tmp, (size_t)chunk * idx->ld * sizeof(float)), "vs_remove_ids: scratch");
+  VS_HIP(scr.alloc((void**)&tmpn, (size_t)chunk * sizeof(float)), "vs_remove_ids: scratch");
+  const int64_t first = rm[0];
+  for (int64_t s0 = first; s0 < idx->ntotal; s0 += chunk) {
+    const int64_t cn = std::min(chunk, idx->ntotal - s0);
+    const int64_t before = std::lower_bound(rm.begin(), rm.end(), s0) - rm.begin();
+    const int64_t in_chunk = std::lower_bound(rm.begin(), rm.end(), s0 + cn) - rm.begin() - before;
+    const int64_t kept = cn - in_chunk;
+    const int64_t dst = s0 - before;
+    VS_HIP(launch_gather_kept(idx->codes, idx->norms, idx->ld, s0, cn, drm, nrem, tmp, tmpn, st),
+           "vs_remove_ids: gather");
+    if (kept > 0) {
+      VS_HIP(hipMemcpyAsync(idx->codes + dst * idx->ld, tmp, (size_t)kept * idx->ld * sizeof(float),
+                            hipMemcpyDeviceToDevice, st),
+             "vs_remove_ids: move rows");
+      VS_HIP(hipMemcpyAsync(idx->norms + dst, tmpn, (size_t)kept * sizeof(float),
+                            hipMemcpyDeviceToDevice, st),
+             "vs_remove_ids: move norms");
+    }
+  }
+  const int64_t nt = idx->ntotal - nrem;
+  VS_HIP(hipMemsetAsync(idx->codes + nt * idx->ld, 0, (size_t)nrem * idx->ld * sizeof(float), st),
+         "vs_remove_ids: zero tail");
+  VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),
+         "vs_remove_ids: zero tail");
+  VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
+  idx->ntotal = nt;
+  if (nremoved) *nremoved = nrem;
+  return VS_OK;
+}
+
+int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_self,
+                float min_sim, float* D, int64_t* I, int flags, void* stream) {
+  if (!idx) return fail(VS_E_INVALID, "vs_selfjoin: null index");
+  if (k <= 0) return fail(VS_E_INVALID, "vs_selfjoin: k must be > 0");
+  if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_selfjoin: k > VS_MAX_K (64) not supported yet");
+  if (q0 < 0 || nq < 0 || q0 + nq > idx->ntotal)
+    return fail(VS_E_INVALID, "vs_selfjoin: query rows out of range");
+  if (nq == 0) return VS_OK;
+  if (!D || !I) return fail(VS_E_INVALID, "vs_selfjoin: null buffer");
+  hipStream_t st = (hipStream_t)stream;
+  std::shared_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  const bool out_dev = (flags & VS_OUT_DEVICE) != 0;
+  Scratch scr(st);
+  float* Dd = D;
+  int64_t* Id = I;
+  if (!out_dev) {
+    VS_HIP(scr.alloc((void**)&Dd, (size_t)nq * k * sizeof(float)), "vs_selfjoin: scratch");
+    VS_HIP(scr.alloc((void**)&Id, (size_t)nq * k * sizeof(int64_t)), "vs_selfjoin: scratch");
+  }
+  float* rinv = nullptr;
+  VS_HIP(scr.alloc((void**)&rinv, (size_t)idx->capacity * sizeof(float)), "vs_selfjoin: scratch");
+  VS_HIP(launch_rsqrt(idx->norms, idx->capacity, rinv, st), "vs_selfjoin: rsqrt");
+  // Query tiles read stored rows directly (capacity keeps kBQ rows of slack).
+  const int64_t chunk = 65536;
+  for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
+    const int64_t nc = std::min(chunk, nq - c0);
+    const int64_t nq_pad = round_up(nc, kBQ);
+    const int64_t qrow = q0 + c0;
+    int rc = run_topk(idx, MODE_COS, idx->codes + qrow * idx->ld, rinv + qrow, (int)nc,
+                      (int)nq_pad, (int)k, exclude_self ? qrow : -1, min_sim, Dd + c0 * k,
+                      Id + c0 * k, st, rinv);
+    if (rc) return rc;
+  }
+  if (!out_dev) {
+    VS_HIP(hipMemcpyAsync(D, Dd, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, st),
+           "vs_selfjoin: copy D");
+    VS_HIP(hipMemcpyAsync(I, Id, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToHost, st),
+           "vs_selfjoin: copy I");
+    VS_HIP(hipStreamSynchronize(st), "vs_selfjoin: synchronise");
+  }
+  return VS_OK;
+}
+
+int vs_merge_topk(const float* D_parts, const int64_t* I_parts, int64_t nparts, int64_t nq,
+                  int64_t k_in, int64_t k, int metric, float* D, int64_t* I, void* stream) {
+  if (nparts < 1 || nq < 0 || k_in < 1 || k < 1)
+    return fail(VS_E_INVALID, "vs_merge_topk: bad sizes");
+  if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_merge_topk: k > VS_MAX_K");
+  if (metric != VS_METRIC_L2 && metric != VS_METRIC_INNER_PRODUCT)
+    return fail(VS_E_INVALID, "vs_merge_topk: bad metric");
+  if (nq == 0) return VS_OK;
+  if (!D_parts || !I_parts || !D || !I) return fail(VS_E_INVALID, "vs_merge_topk: null buffer");
+  VS_HIP(launch_merge_parts(metric == VS_METRIC_L2 ? MODE_L2 : MODE_IP, D_parts, I_parts,
+                            (int)nparts, (int)nq, (int)k_in, (int)k, D, I, (hipStream_t)stream),
+         "vs_merge_topk: launch");
+  return VS_OK;
+}
+
+int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_t row0,
+                      void* stream) {
+  if (rows < 0 || d <= 0 || row0 < 0) return fail(VS_E_INVALID, "vs_fill_synthetic: bad sizes");
+  if (rows == 0) return VS_OK;
+  if (!out) return fail(VS_E_INVALID, "vs_fill_synthetic: null output");
+  VS_HIP(launch_fill_synthetic(out, rows, d, d, seed, row0, (hipStream_t)stream),
+         "vs_fill_synthetic: launch");
+  return VS_OK;
+}
+
+int vs_timer_enable(int on) {
+  std::lock_guard<std::mutex> g(g_timer_mu);
+  g_timer_on = on != 0;
+  return VS_OK;
+}
+
+int vs_timer_reset(void) {
+  std::lock_guard<std::mutex> g(g_timer_mu);
+  for (auto& p : g_timer_events) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  g_timer_events.clear();
+  return VS_OK;
+}
+
+int vs_timer_read(double* total_ms, int64_t* launches) {
+  if (!total_ms || !launches) return fail(VS_E_INVALID, "vs_timer_read: null output");
+  std::lock_guard<std::mutex> g(g_timer_mu);
+  double tot = 0.0;
+  for (auto& p : g_timer_events) {
+    VS_HIP(hipEventSynchronize(p.second), "vs_timer_read: synchronise");
+    float ms = 0.0f;
+    VS_HIP(hipEventElapsedTime(&ms, p.first, p.second), "vs_timer_read: elapsed");
+    tot += ms;
+  }
+  *total_ms = tot;
+  *launches = (int64_t)g_timer_events.size();
+  return VS_OK;
+}
+
+}  // extern "C"

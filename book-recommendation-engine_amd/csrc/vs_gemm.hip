@@ -1,0 +1,241 @@
+// vs_gemm.hip — fused fp32 MFMA distance + top-k kernel (large query batches).
+// List semantics and key conventions: vs_device.h / vs_internal.h.
+#include "vs_device.h"
+
+namespace vs {
+
+// ---------------------------------------------------------------------------
+// GEMM path.
+//
+// Workgroup = 256 threads (4 waves), tile = 128 database rows x 128 queries.
+// Wave w owns queries [32w, 32w+32) of the tile against all 128 rows: four
+// 32x32 accumulators (database subtiles s = 0..3).  In v_mfma_f32_32x32x2_f32 the
+// A operand is the database row block (row i = lane&31) and the B operand the
+// query block (column j = lane&31), so after the K loop lane l holds, for query
+// column l&31, the scores of rows (r&3) + 8(r>>2) + 4(l>>5) of each subtile: a
+// lane sees one query only, and can keep that query's top-k in its own
+// registers with no cross-lane traffic.  Each query therefore owns two lists per
+// workgroup (lane halves h = 0, 1); the merge kernel combines them.
+//
+// K loop: BK = 32 floats per stage, double-buffered in LDS and filled with
+// global_load_lds_dwordx4 (no VGPR staging).  An LDS row is 128 B = 8 chunks of
+// 16 B; chunk c of row r is stored at c ^ ((r >> 1) & 7), which makes the
+// ds_read_b128 fragment reads conflict-free (each 16-lane read group lands on 16
+// distinct 16-B slots).  glds writes LDS lane-linearly, so the swizzle is applied
+// to the per-lane GLOBAL source address instead.
+//
+// Fragment k-order: for MFMA step t (0..3) lane half h supplies k = 4h + t of the
+// current 8-wide k chunk, on both operands, so each lane reads one 16-B chunk per
+// operand per 4 MFMAs.  The summation order differs from faiss's sgemm, which is
+// inside the documented fp32 tolerance.
+//
+// Workgroup -> (query tile, split) mapping is XCD-aware: consecutive logical ids
+// (which share a database split and differ in query tile) are packed onto one XCD
+// so the 4 MiB L2 there serves each database tile to all query tiles in flight.
+template <int KP, int MODE>
+__global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
+    const float* __restrict__ X, const float* __restrict__ xaux, const float* __restrict__ Q,
+    const float* __restrict__ qaux, int64_t ld, int nstage, int ntotal, int ntiles, int nsplit,
+    int nqt, int64_t self0, float* __restrict__ pkey, int* __restrict__ pid) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * kBN * kBK];  // [buf][X|Q][128][32]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int h = lane >> 5;
+  const int c32 = lane & 31;
+
+  // Bijective XCD remap (blocks b and b+8 are dispatched to the same XCD).
+  const int nblk = gridDim.x;
+  const int b = blockIdx.x;
+  int lb;
+  {
+    const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
+    lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+  }
+  const int qt = lb % nqt;
+  const int sp = lb / nqt;
+  const int t0 = (int)((int64_t)sp * ntiles / nsplit);
+  const int t1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
+
+  const int qloc = 32 * w + c32;
+  const int gq = qt * kBQ + qloc;
+  float qa = 0.0f;
+  if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa = qaux[gq];
+  const int64_t selfrow = self0 >= 0 ? self0 + gq : -1;
+
+  float lk[KP];
+  int li[KP];
+  list_init<KP, int>(lk, li);
+
+  const float* Qblk = Q + (int64_t)qt * kBQ * ld;
+  // glds geometry: a wave instruction moves 8 rows x 128 B; wave w stages row
+  // groups 4w..4w+3 of both operands.
+  const int srow = lane >> 3;
+  const int sphys = lane & 7;
+  // fragment-read geometry: (row >> 1) & 7 is the same for every subtile.
+  const int fsw = (c32 >> 1) & 7;
+
+  for (int t = t0; t < t1; ++t) {
+    const float* Xblk = X + (int64_t)t * kBN * ld;
+    f32x16 acc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[s][r] = 0.0f;
+    }
+
+    auto stage = [&](int buf, int kb) {
+      float* dX = smem + buf * (2 * kBN * kBK);
+      float* dQ = dX + kBN * kBK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int g = w * 4 + i;
+        const int row = g * 8 + srow;
+        const int c = sphys ^ ((row >> 1) & 7);
+        __builtin_amdgcn_global_load_lds(Xblk + (int64_t)row * ld + kb + c * 4,
+                                         VS_LDS(dX + g * 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(Qblk + (int64_t)row * ld + kb + c * 4,
+                                         VS_LDS(dQ + g * 256), 16, 0, 0);
+      }
+    };
+
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (int st = 0; st < nstage; ++st) {
+      if (st + 1 < nstage) stage((st + 1) & 1, (st + 1) * kBK);
+      const float* cX = smem + (st & 1) * (2 * kBN * kBK);
+      const float* cQ = cX + kBN * kBK;
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        const int coff = ((kc * 2 + h) ^ fsw) * 4;
+        const f32x4 bq = *(const f32x4*)(cQ + qloc * kBK + coff);
+        f32x4 ax[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ax[s] = *(const f32x4*)(cX + (32 * s + c32) * kBK + coff);
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(ax[s][tt], bq[tt], acc[s], 0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+
+    // Epilogue.  Phase A (unrolled, branch-free): scores -> keys in place, and a
+    // 64-bit mask of the values that beat the lane's current worst entry.  The
+    // threshold only tightens while inserting, so testing against the value it
+    // had at the start admits a superset.  Phase B (rare after the first tiles):
+    // the lane parks its 64 keys in a private column of the (now idle) staging
+    // LDS and inserts the flagged ones, so the insertion code exists once.
+    const int r0 = t * kBN;
+    const float tk = lk[KP - 1];
+    const int ti = li[KP - 1];
+    uint64_t m = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rb = r0 + 32 * s + 8 * j + 4 * h;
+        f32x4 xa = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == MODE_L2 || MODE == MODE_COS) xa = *(const f32x4*)(xaux + rb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rb + i;
+          const float v = acc[s][j * 4 + i];
+          float key;
+          if constexpr (MODE == MODE_IP) {
+            key = -v;
+          } else if constexpr (MODE == MODE_L2) {
+            key = l2_from_ip(qa, xa[i], v);
+          } else {
+            key = -(v * (qa * xa[i]));
+          }
+          acc[s][j * 4 + i] = key;
+          const bool cand = row < ntotal && (int64_t)row != selfrow && lex_less(key, row, tk, ti);
+          m |= (uint64_t)cand << (s * 16 + j * 4 + i);
+        }
+      }
+    }
+    if (m) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) smem[(s * 16 + r) * 256 + tid] = acc[s][r];
+      }
+      do {
+        const int bi = __builtin_ctzll(m);
+        m &= m - 1;
+        const int row = r0 + 32 * (bi >> 4) + (bi & 3) + 8 * ((bi >> 2) & 3) + 4 * h;
+        list_insert<KP, int>(lk, li, smem[bi * 256 + tid], row);
+      } while (m);
+    }
+    // The next tile's first stage overwrites the LDS the epilogue may have used.
+    __syncthreads();
+  }
+
+  const int P = nsplit * 2;
+  float* ok = pkey + ((int64_t)gq * P + sp * 2 + h) * KP;
+  int* oi = pid + ((int64_t)gq * P + sp * 2 + h) * KP;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    ok[j] = lk[j];
+    oi[j] = li[j];
+  }
+}
+
+template <int KP, int MODE>
+static hipError_t gemm_dispatch_mode(const float* X, const float* xaux, const float* Q,
+                                     const float* qaux, int64_t ld, int ntotal, int nq_pad,
+                                     int nsplit, int64_t self0, Partials part, hipStream_t st) {
+  const int ntiles = (ntotal + kBN - 1) / kBN;
+  const int nqt = nq_pad / kBQ;
+  const int nblk = nqt * nsplit;
+  hipLaunchKernelGGL((gemm_topk_f32<KP, MODE>), dim3(nblk), dim3(256), 0, st, X, xaux, Q, qaux,
+                     ld, (int)(ld / kBK), ntotal, ntiles, nsplit, nqt, self0, part.key, part.id);
+  return hipGetLastError();
+}
+
+template <int KP>
+static hipError_t gemm_dispatch(int mode, const float* X, const float* xaux, const float* Q,
+                                const float* qaux, int64_t ld, int ntotal, int nq_pad,
+                                int nsplit, int64_t self0, Partials part, hipStream_t st) {
+  switch (mode) {
+    case MODE_IP:
+      return gemm_dispatch_mode<KP, MODE_IP>(X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0,
+                                             part, st);
+    case MODE_L2:
+      return gemm_dispatch_mode<KP, MODE_L2>(X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0,
+                                             part, st);
+    case MODE_COS:
+      return gemm_dispatch_mode<KP, MODE_COS>(X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit,
+                                              self0, part, st);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_gemm_topk(int KP, int mode, const float* X, const float* xaux, const float* Q,
+                            const float* qaux, int64_t ld, int ntotal, int nq_pad, int nsplit,
+                            int64_t self0, Partials part, hipStream_t st) {
+  if (nq_pad % kBQ != 0 || ld % kBK != 0 || part.KP != KP || part.P != 2 * nsplit)
+    return hipErrorInvalidValue;
+  switch (KP) {
+    case 8:
+      return gemm_dispatch<8>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+    case 16:
+      return gemm_dispatch<16>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+    case 32:
+      return gemm_dispatch<32>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+    case 64:
+      return gemm_dispatch<64>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace vs

@@ -1,0 +1,141 @@
+// vs_gemv.hip — streaming distance + top-k kernel for small query batches (nq <= 8).
+#include "vs_device.h"
+
+namespace vs {
+
+// ---------------------------------------------------------------------------
+// GEMV path (nq <= 8): each wave streams 4 rows at a time; lane l reads float4
+// chunks l, l+64, ... of every row (1 KiB per wave instruction, fully
+// coalesced), the queries sit in LDS, partial sums are reduced across the wave,
+// and lane q keeps query q's list.  MODE_L2D computes sum (x-q)^2 directly, as
+// faiss does for nq < 20 (fvec_L2sqr); MODE_IP the plain dot product.
+template <int NQ, int KP, int MODE>
+__global__ __launch_bounds__(256) void gemv_topk_f32(const float* __restrict__ X,
+                                                      const float* __restrict__ Q, int64_t ld,
+                                                      int ntotal, int rows_per_block,
+                                                      float* __restrict__ pkey,
+                                                      int* __restrict__ pid) {
+  extern __shared__ __attribute__((aligned(16))) float sq[];  // [NQ][ld]
+  const int tid = threadIdx.x;
+  for (int64_t i = (int64_t)tid * 4; i < (int64_t)NQ * ld; i += 1024)
+    *(f32x4*)(sq + i) = *(const f32x4*)(Q + i);
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int ld4 = (int)(ld >> 2);
+  const int rb0 = blockIdx.x * rows_per_block;
+  const int ntot16 = (ntotal + 15) & ~15;
+  const int rb1 = min(rb0 + rows_per_block, ntot16);
+
+  float lk[KP];
+  int li[KP];
+  list_init<KP, int>(lk, li);
+
+  for (int r = rb0 + 4 * w; r < rb1; r += 16) {
+    float acc[4][NQ];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[a][q] = 0.0f;
+
+    const float* xr = X + (int64_t)r * ld;
+    for (int c = lane; c < ld4; c += 64) {
+      f32x4 xv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) xv[a] = __builtin_nontemporal_load((const f32x4*)(xr + a * ld) + c);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const f32x4 qv = *(const f32x4*)(sq + q * ld + c * 4);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          if constexpr (MODE == MODE_L2D) {
+            const f32x4 dv = xv[a] - qv;
+            acc[a][q] += dv.x * dv.x + dv.y * dv.y + dv.z * dv.z + dv.w * dv.w;
+          } else {
+            acc[a][q] += xv[a].x * qv.x + xv[a].y * qv.y + xv[a].z * qv.z + xv[a].w * qv.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float mine = 0.0f;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const float s = wave_sum(acc[a][q]);
+        if (q == lane) mine = s;
+      }
+      const int row = r + a;
+      if (lane < NQ && row < ntotal) {
+        const float key = (MODE == MODE_L2D) ? mine : -mine;
+        list_insert<KP, int>(lk, li, key, row);
+      }
+    }
+  }
+
+  if (lane < NQ) {
+    const int P = gridDim.x * 4;
+    float* ok = pkey + ((int64_t)lane * P + blockIdx.x * 4 + w) * KP;
+    int* oi = pid + ((int64_t)lane * P + blockIdx.x * 4 + w) * KP;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      ok[j] = lk[j];
+      oi[j] = li[j];
+    }
+  }
+}
+
+template <int NQ, int KP>
+static hipError_t gemv_dispatch_q(int mode, const float* X, const float* Q, int64_t ld,
+                                  int ntotal, int nblocks, Partials part, hipStream_t st) {
+  const int ntot16 = (ntotal + 15) & ~15;
+  int rpb = (ntot16 + nblocks - 1) / nblocks;
+  rpb = (rpb + 15) & ~15;
+  const size_t lds = (size_t)NQ * ld * sizeof(float);
+  if (mode == MODE_L2D)
+    hipLaunchKernelGGL((gemv_topk_f32<NQ, KP, MODE_L2D>), dim3(nblocks), dim3(256), lds, st, X, Q,
+                       ld, ntotal, rpb, part.key, part.id);
+  else if (mode == MODE_IP)
+    hipLaunchKernelGGL((gemv_topk_f32<NQ, KP, MODE_IP>), dim3(nblocks), dim3(256), lds, st, X, Q,
+                       ld, ntotal, rpb, part.key, part.id);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+template <int KP>
+static hipError_t gemv_dispatch(int mode, int nq, const float* X, const float* Q, int64_t ld,
+                                int ntotal, int nblocks, Partials part, hipStream_t st) {
+  switch (nq) {
+    case 1:
+      return gemv_dispatch_q<1, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+    case 2:
+      return gemv_dispatch_q<2, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+    case 3:
+    case 4:
+      return gemv_dispatch_q<4, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+    default:
+      return gemv_dispatch_q<8, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+  }
+}
+
+hipError_t launch_gemv_topk(int KP, int mode, int nq, const float* X, const float* Q, int64_t ld,
+                            int ntotal, int nblocks, Partials part, hipStream_t st) {
+  if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks * 4 || ld % 4 != 0)
+    return hipErrorInvalidValue;
+  switch (KP) {
+    case 8:
+      return gemv_dispatch<8>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+    case 16:
+      return gemv_dispatch<16>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+    case 32:
+      return gemv_dispatch<32>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+    case 64:
+      return gemv_dispatch<64>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace vs

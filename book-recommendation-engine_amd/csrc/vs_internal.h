@@ -1,0 +1,73 @@
+// Internal declarations shared by vs_kernels.hip (device code + launchers) and
+// vs_api.hip (the C-ABI).  Nothing here is part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+namespace vs {
+
+// Score modes of the fused kernels.  Every mode is reduced to a "key" where
+// smaller is better, so one list discipline serves all of them:
+//   IP : key = -<q,x>                        (faiss knn_inner_product, CMin heap)
+//   L2 : key = (|q|^2 + |x|^2) - 2<q,x>, <0 -> 0 (faiss knn_L2sqr BLAS branch)
+//   L2D: key = sum (x-q)^2                   (faiss knn_L2sqr sequential branch, nq < 20)
+//   COS: key = -(<q,x> * rq * rx)             (pgvector 1 - (a <=> b))
+enum Mode : int { MODE_IP = 0, MODE_L2 = 1, MODE_COS = 2, MODE_L2D = 3 };
+
+// GEMM tile geometry (fp32 MFMA path): 128 database rows x 128 queries per
+// workgroup, K staged 32 floats at a time through LDS.
+constexpr int kBN = 128;
+constexpr int kBQ = 128;
+constexpr int kBK = 32;
+// Row storage stride (floats) is a multiple of kBK; capacity keeps >= kBQ rows of
+// zeroed slack past ntotal and is a multiple of kRowPad, so every tile load of
+// the GEMM (database tiles and self-join query tiles) stays inside the buffer.
+constexpr int kRowPad = 256;
+// The GEMV (small batch) path handles up to this many queries per launch.
+constexpr int kGemvMaxQ = 8;
+
+// Merge-buffer record: key + local row id (int32; a shard never holds 2^31 rows).
+struct Partials {
+  float* key = nullptr;
+  int* id = nullptr;
+  int P = 0;   // lists per query
+  int KP = 0;  // entries per list
+};
+
+// ---- launchers (return the launch status; all asynchronous on `st`) -------
+// Fused MFMA distance + top-k over database tiles, writing 2*nsplit lists/query.
+hipError_t launch_gemm_topk(int KP, int mode, const float* X, const float* xaux,
+                            const float* Q, const float* qaux, int64_t ld, int ntotal,
+                            int nq_pad, int nsplit, int64_t self0, Partials part,
+                            hipStream_t st);
+// Streaming (HBM-bound) distance + top-k for nq <= kGemvMaxQ.
+hipError_t launch_gemv_topk(int KP, int mode, int nq, const float* X, const float* Q,
+                            int64_t ld, int ntotal, int nblocks, Partials part,
+                            hipStream_t st);
+// Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
+hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
+                                 float min_score, float* D, int64_t* I, int64_t ldo,
+                                 hipStream_t st);
+// Shard lists [nparts][nq][k_in] (scores, int64 labels) -> [nq][k].
+hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts,
+                              int nq, int k_in, int k, float* D, int64_t* I, hipStream_t st);
+// out[r] = sum_j X[r][j]^2 for rows [r0, r0+n).
+hipError_t launch_row_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
+                            hipStream_t st);
+// out[r] = 1/sqrt(norm[r]) (double-precision rsqrt rounded to float).
+hipError_t launch_rsqrt(const float* norm, int64_t n, float* out, hipStream_t st);
+// Counter-based synthetic rows into a pitched buffer (zero padding d..ldo).
+hipError_t launch_fill_synthetic(float* out, int64_t rows, int64_t d, int64_t ldo,
+                                 uint64_t seed, int64_t row0, hipStream_t st);
+// Fill n (D, I) pairs with the empty-result sentinel of `mode`.
+hipError_t launch_fill_empty(int mode, float* D, int64_t* I, int64_t n, hipStream_t st);
+// Stable compaction helper: copy the kept rows of [src0, src0+n) into tmp,
+// given the sorted removed-row list (device).  Also moves the norms.
+hipError_t launch_gather_kept(const float* X, const float* norms, int64_t ld, int64_t src0,
+                              int64_t n, const int64_t* removed, int64_t nrem, float* tmp,
+                              float* tmp_norms, hipStream_t st);
+
+}  // namespace vs

@@ -1,0 +1,367 @@
+// vs_kernels.hip — gfx950 (MI355X / CDNA4) kernels of the exact flat index.
+//
+// Semantics follow faiss-cpu 1.11.0 IndexFlat::search (not vendored; pinned at
+// /root/reference/poetry.lock:866-867): exact top-k, squared L2 or inner
+// product, ties broken by the lower label, k > ntotal padded with (neutral, -1).
+// Every score is mapped to a key where smaller is better (vs_internal.h), and
+// lists are ordered by (key, row) lexicographically — the order faiss's heaps
+// produce with CMax/CMin::cmp2.
+//
+// Kernels
+//   gemm_topk_f32   fp32 MFMA (v_mfma_f32_32x32x2_f32) Q.X^T tile with the top-k
+//                   selection fused into the epilogue; large query batches,
+//                   bounded by the fp32 matrix-core peak.
+//   gemv_topk_f32   one streaming pass of the corpus for nq <= 8, bounded by HBM.
+//   merge_*         per-query merge of partial lists (also the shard merge that
+//                   follows the RCCL all-gather).
+//   row_norms, rsqrt, fill_synthetic, fill_empty, gather_kept: support.
+#include "vs_device.h"
+
+namespace vs {
+
+// ---------------------------------------------------------------------------
+// Merge: one wave per query.  Each lane filters a strided slice of the
+// candidates into its own register list, then the 64 lists are combined by a
+// 6-round pairwise merge through LDS.  Output keys are mapped back to scores.
+template <int KP, typename IdT>
+__device__ __forceinline__ void wave_tree_merge(float (&lk)[KP], IdT (&li)[KP], float* sk,
+                                                IdT* si, int lane) {
+  // sk/si: LDS [64][KP]
+  for (int step = 1; step < 64; step <<= 1) {
+    if ((lane & (step - 1)) == 0) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        sk[lane * KP + j] = lk[j];
+        si[lane * KP + j] = li[j];
+      }
+    }
+    __syncthreads();
+    if ((lane & (2 * step - 1)) == 0) {
+      const float* ak = sk + lane * KP;
+      const IdT* ai = si + lane * KP;
+      const float* bk = sk + (lane + step) * KP;
+      const IdT* bi = si + (lane + step) * KP;
+      int ia = 0, ib = 0;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        const float ka = ak[ia], kb = bk[ib];
+        const IdT xa = ai[ia], xb = bi[ib];
+        const bool ta = !lex_less(kb, xb, ka, xa);
+        lk[j] = ta ? ka : kb;
+        li[j] = ta ? xa : xb;
+        ia += ta ? 1 : 0;
+        ib += ta ? 0 : 1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// faiss's inner-product tie rule on a lexicographic (key, label) list held in
+// LDS (lane 0 only).  faiss's CMin heap keeps, at equal scores, the SMALLER label
+// on top, so later better rows evict the smallest admitted labels; and
+// heap_reorder emits equal scores in DESCENDING label order.  With v the k-th key,
+// c the count strictly better, a_i the labels with key v (ascending) and g_i the
+// number of better labels below a_i, faiss keeps a_{A-r} .. a_{A-1} where
+// A = #{i : i + g_i < k} and r = k - c.  (L2's CMax heap needs no adjustment: it
+// is exactly the lexicographic order.)  The candidate pool is the merged list;
+// if its v-run was truncated at KP entries the result stays a valid tie order.
+template <typename IdT>
+__device__ void faiss_ip_tie_order(float* sk, IdT* si, int KP, int k) {
+  int nv = 0;
+  while (nv < KP && si[nv] >= 0) ++nv;
+  const int m = nv < k ? nv : k;
+  if (nv > k) {
+    const float v = sk[k - 1];
+    int c = 0;
+    while (sk[c] < v) ++c;
+    int t = 0;
+    while (c + t < nv && sk[c + t] == v) ++t;
+    int A = 0;
+    for (int i = 0; i < t; ++i) {
+      int g = 0;
+      for (int j = 0; j < c; ++j) g += si[j] < si[c + i] ? 1 : 0;
+      if (i + g < k) A = i + 1;
+      else break;
+    }
+    const int r = k - c;
+    for (int i = 0; i < r; ++i) {  // source index >= destination: forward copy is safe
+      sk[c + i] = sk[c + A - r + i];
+      si[c + i] = si[c + A - r + i];
+    }
+  }
+  for (int s0 = 0; s0 < m;) {  // descending label inside equal keys
+    int e = s0;
+    while (e + 1 < m && sk[e + 1] == sk[s0]) ++e;
+    for (int a = s0, b = e; a < b; ++a, --b) {
+      const IdT tmp = si[a];
+      si[a] = si[b];
+      si[b] = tmp;
+    }
+    s0 = e + 1;
+  }
+}
+
+__device__ __forceinline__ void emit_result(int mode, float key, int64_t id, int64_t id_base,
+                                            float min_score, float* D, int64_t* I) {
+  if (id < 0) {
+    *D = (mode == MODE_L2 || mode == MODE_L2D) ? FLT_MAX : -FLT_MAX;
+    *I = -1;
+    return;
+  }
+  const float score = (mode == MODE_L2 || mode == MODE_L2D) ? key : -key;
+  if (mode == MODE_COS && !(score >= min_score)) {
+    *D = -FLT_MAX;
+    *I = -1;
+    return;
+  }
+  *D = score;
+  *I = id + id_base;
+}
+
+template <int KP>
+__global__ __launch_bounds__(64) void merge_partials_kernel(const float* __restrict__ pkey,
+                                                            const int* __restrict__ pid, int P,
+                                                            int k, int mode, int64_t id_base,
+                                                            float min_score, float* __restrict__ D,
+                                                            int64_t* __restrict__ I, int64_t ldo) {
+  __shared__ float sk[64 * KP];
+  __shared__ int si[64 * KP];
+  const int lane = threadIdx.x;
+  const int q = blockIdx.x;
+  float lk[KP];
+  int li[KP];
+  list_init<KP, int>(lk, li);
+  const int64_t n = (int64_t)P * KP;
+  const float* ck = pkey + (int64_t)q * n;
+  const int* ci = pid + (int64_t)q * n;
+  for (int64_t c = lane; c < n; c += 64) {
+    const int id = ci[c];
+    if (id >= 0) list_insert<KP, int>(lk, li, ck[c], id);
+  }
+  wave_tree_merge<KP, int>(lk, li, sk, si, lane);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      sk[j] = lk[j];
+      si[j] = li[j];
+    }
+    if (mode == MODE_IP) faiss_ip_tie_order<int>(sk, si, KP, k);
+  }
+  __syncthreads();
+  if (lane < k) emit_result(mode, sk[lane], si[lane], id_base, min_score, D + q * ldo + lane,
+                            I + q * ldo + lane);
+}
+
+hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
+                                 float min_score, float* D, int64_t* I, int64_t ldo,
+                                 hipStream_t st) {
+  if (k < 1 || k > part.KP || nq < 0) return hipErrorInvalidValue;
+  if (nq == 0) return hipSuccess;
+  switch (part.KP) {
+#define VS_MERGE_CASE(KPV)                                                                     \
+  case KPV:                                                                                   \
+    hipLaunchKernelGGL((merge_partials_kernel<KPV>), dim3(nq), dim3(64), 0, st, part.key,     \
+                       part.id, part.P, k, mode, id_base, min_score, D, I, ldo);              \
+    break;
+    VS_MERGE_CASE(8)
+    VS_MERGE_CASE(16)
+    VS_MERGE_CASE(32)
+    VS_MERGE_CASE(64)
+#undef VS_MERGE_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int KP>
+__global__ __launch_bounds__(64) void merge_parts_kernel(const float* __restrict__ Dp,
+                                                         const int64_t* __restrict__ Ip,
+                                                         int nparts, int nq, int k_in, int k,
+                                                         int mode, float* __restrict__ D,
+                                                         int64_t* __restrict__ I) {
+  __shared__ float sk[64 * KP];
+  __shared__ int64_t si[64 * KP];
+  const int lane = threadIdx.x;
+  const int q = blockIdx.x;
+  const bool asc = (mode == MODE_L2 || mode == MODE_L2D);
+  float lk[KP];
+  int64_t li[KP];
+  list_init<KP, int64_t>(lk, li);
+  const int64_t n = (int64_t)nparts * k_in;
+  for (int64_t c = lane; c < n; c += 64) {
+    const int p = (int)(c / k_in), j = (int)(c % k_in);
+    const int64_t off = ((int64_t)p * nq + q) * k_in + j;
+    const int64_t id = Ip[off];
+    if (id >= 0) {
+      const float s = Dp[off];
+      list_insert<KP, int64_t>(lk, li, asc ? s : -s, id);
+    }
+  }
+  wave_tree_merge<KP, int64_t>(lk, li, sk, si, lane);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      sk[j] = lk[j];
+      si[j] = li[j];
+    }
+    if (!asc) faiss_ip_tie_order<int64_t>(sk, si, KP, k);
+  }
+  __syncthreads();
+  if (lane < k) emit_result(asc ? MODE_L2 : MODE_IP, sk[lane], si[lane], 0, 0.0f,
+                            D + (int64_t)q * k + lane, I + (int64_t)q * k + lane);
+}
+
+hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts, int nq,
+                              int k_in, int k, float* D, int64_t* I, hipStream_t st) {
+  if (k < 1 || k > 64 || nq < 0 || nparts < 1 || k_in < 1) return hipErrorInvalidValue;
+  if (nq == 0) return hipSuccess;
+  const int KP = k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64;
+  switch (KP) {
+#define VS_MERGEP_CASE(KPV)                                                                   \
+  case KPV:                                                                                  \
+    hipLaunchKernelGGL((merge_parts_kernel<KPV>), dim3(nq), dim3(64), 0, st, Dp, Ip, nparts, \
+                       nq, k_in, k, mode, D, I);                                             \
+    break;
+    VS_MERGEP_CASE(8)
+    VS_MERGEP_CASE(16)
+    VS_MERGEP_CASE(32)
+    VS_MERGEP_CASE(64)
+#undef VS_MERGEP_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Support kernels.
+__global__ __launch_bounds__(256) void row_norms_kernel(const float* __restrict__ X, int64_t ld,
+                                                        int64_t r0, int64_t n,
+                                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* xr = X + (r0 + row) * ld;
+  float s = 0.0f;
+  for (int64_t c = lane; c < (ld >> 2); c += 64) {
+    const f32x4 v = *(const f32x4*)(xr + c * 4);
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[r0 + row] = s;
+}
+
+hipError_t launch_row_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nb = (n + 3) / 4;
+  hipLaunchKernelGGL(row_norms_kernel, dim3((unsigned)nb), dim3(256), 0, st, X, ld, r0, n, out);
+  return hipGetLastError();
+}
+
+__global__ void rsqrt_kernel(const float* __restrict__ nrm, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (float)(1.0 / sqrt((double)nrm[i]));
+}
+
+hipError_t launch_rsqrt(const float* norm, int64_t n, float* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rsqrt_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, norm, n,
+                     out);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_synthetic_kernel(float* __restrict__ out, int64_t rows,
+                                                             int64_t d, int64_t ldo, uint64_t seed,
+                                                             int64_t row0) {
+  const int64_t row = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (row >= rows) return;
+  const uint64_t base = (uint64_t)(row0 + row) * (uint64_t)d;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < ldo; j += (int64_t)gridDim.x * 256) {
+    float v = 0.0f;
+    if (j < d) {
+      const uint64_t z = splitmix64(seed ^ (base + (uint64_t)j));
+      v = (float)(z >> 40) * (1.0f / 8388608.0f) - 1.0f;
+    }
+    out[row * ldo + j] = v;
+  }
+}
+
+hipError_t launch_fill_synthetic(float* out, int64_t rows, int64_t d, int64_t ldo, uint64_t seed,
+                                 int64_t row0, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  const int64_t gy = rows < 65535 ? rows : 65535;
+  const int64_t gz = (rows + 65534) / 65535;
+  const int gx = (int)((ldo + 255) / 256 < 8 ? (ldo + 255) / 256 : 8);
+  hipLaunchKernelGGL(fill_synthetic_kernel, dim3(gx, (unsigned)gy, (unsigned)gz), dim3(256), 0, st,
+                     out, rows, d, ldo, seed, row0);
+  return hipGetLastError();
+}
+
+__global__ void fill_empty_kernel(int asc, float* __restrict__ D, int64_t* __restrict__ I,
+                                  int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    D[i] = asc ? FLT_MAX : -FLT_MAX;
+    I[i] = -1;
+  }
+}
+
+hipError_t launch_fill_empty(int mode, float* D, int64_t* I, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_empty_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (mode == MODE_L2 || mode == MODE_L2D) ? 1 : 0, D, I, n);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ int64_t count_less(const int64_t* a, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One wave per source row: kept rows of [src0, src0+n) are packed, in order,
+// into tmp (and their norms into tmp_norms).
+__global__ __launch_bounds__(256) void gather_kept_kernel(const float* __restrict__ X,
+                                                          const float* __restrict__ norms,
+                                                          int64_t ld, int64_t src0, int64_t n,
+                                                          const int64_t* __restrict__ removed,
+                                                          int64_t nrem, float* __restrict__ tmp,
+                                                          float* __restrict__ tmp_norms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t row = src0 + i;
+  const int64_t before_row = count_less(removed, nrem, row);
+  if (before_row < nrem && removed[before_row] == row) return;  // removed
+  const int64_t before_src0 = count_less(removed, nrem, src0);
+  const int64_t dst = i - (before_row - before_src0);
+  const f32x4* s = (const f32x4*)(X + row * ld);
+  f32x4* dd = (f32x4*)(tmp + dst * ld);
+  for (int64_t c = lane; c < (ld >> 2); c += 64) dd[c] = s[c];
+  if (lane == 0) tmp_norms[dst] = norms[row];
+}
+
+hipError_t launch_gather_kept(const float* X, const float* norms, int64_t ld, int64_t src0,
+                              int64_t n, const int64_t* removed, int64_t nrem, float* tmp,
+                              float* tmp_norms, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X,
+                     norms, ld, src0, n, removed, nrem, tmp, tmp_norms);
+  return hipGetLastError();
+}
+
+}  // namespace vs

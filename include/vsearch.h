@@ -1,0 +1,158 @@
+/*
+ * vsearch.h — C-ABI of libvsearch.so, the MI355X-native exact flat-index engine.
+ *
+ * This is the drop-in boundary for the reference's one data-parallel hot path:
+ * brute-force top-k over 1536-d book / student embeddings.  In the reference the
+ * path is reached through LangChain's `FAISS` vector store
+ * (langchain-community 0.3.26, /root/reference/poetry.lock:1577-1578) whose
+ * `.index` is a faiss-cpu 1.11.0 `IndexFlatL2` / `IndexFlatIP`
+ * (/root/reference/poetry.lock:866-867), plus the pgvector cosine top-15
+ * self-join in /root/reference/src/graph_refresher/main.py:339-354.
+ *
+ * Every entry point below names the reference interface it replaces.  faiss and
+ * langchain are not vendored in /root/reference; their call sites are cited.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a negative VS_E* code on failure;
+ *     the message is available from vs_last_error() (thread-local).
+ *   - vectors are C-contiguous float32 rows of length d (what faiss's SWIG layer
+ *     receives after np.ascontiguousarray(x, dtype="float32")).
+ *   - `flags` say where caller buffers live (VS_IN_DEVICE / VS_OUT_DEVICE);
+ *     device buffers must be on the index's device.
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream).  Calls with
+ *     host outputs synchronise that stream before returning.
+ *   - labels are int64, exactly faiss's idx_t; padding label is -1.
+ */
+#ifndef VSEARCH_H
+#define VSEARCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Metric codes equal faiss::MetricType so index.metric_type passes straight through. */
+#define VS_METRIC_INNER_PRODUCT 0
+#define VS_METRIC_L2 1
+
+/* Storage dtype of the database rows. */
+#define VS_DTYPE_F32 0
+#define VS_DTYPE_BF16 1
+
+/* Buffer-location flags. */
+#define VS_IN_DEVICE 1  /* input vectors / ids are device pointers */
+#define VS_OUT_DEVICE 2 /* output buffers are device pointers      */
+
+/* Status codes. */
+#define VS_OK 0
+#define VS_E_INVALID (-1) /* bad argument (faiss: FAISS_THROW_IF_NOT / assert) */
+#define VS_E_HIP (-2)     /* HIP runtime / launch error                        */
+#define VS_E_OOM (-3)     /* device allocation failed                          */
+#define VS_E_UNSUPPORTED (-4)
+
+/* Largest k served by the fused GPU top-k (register lists of up to 64 entries). */
+#define VS_MAX_K 64
+
+typedef struct vs_index vs_index;
+
+/* Thread-local text of the last error (faiss: FaissException::what()). */
+const char* vs_last_error(void);
+/* Library ABI version (major*10000 + minor*100 + patch). */
+int vs_version(void);
+/* Number of visible HIP devices. */
+int vs_device_count(int* n);
+
+/* ---- index lifetime -------------------------------------------------------
+ * Replaces faiss.IndexFlatL2(d) / faiss.IndexFlatIP(d), created by
+ * FAISS.from_texts (default EUCLIDEAN => IndexFlatL2) at
+ * src/ingestion_service/pipeline.py:359, src/incremental_workers/book_vector/main.py:121,469,
+ * src/recommendation_api/candidate_builder.py:69-71, src/recommendation_api/service.py:370-372. */
+int vs_create(int d, int metric, int dtype, int device, vs_index** out);
+int vs_destroy(vs_index* idx);
+
+/* Pre-size device storage for n rows (no faiss equivalent; avoids regrowth copies). */
+int vs_reserve(vs_index* idx, int64_t n);
+
+/* faiss Index::add(n, x) — appends rows; labels continue at ntotal.
+ * Callers: FAISS.add_texts at src/ingestion_service/pipeline.py:363,
+ * src/incremental_workers/book_vector/main.py:148. */
+int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream);
+
+/* Appends n rows of the deterministic counter-based synthetic corpus
+ * (row r = global row row0 + i; see vs_fill_synthetic).  Benchmark/test feed only. */
+int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void* stream);
+
+/* faiss Index::reset(). */
+int vs_reset(vs_index* idx);
+
+/* faiss Index::ntotal / ::d / ::metric_type (read at book_vector/main.py:162-170,
+ * ingestion_service/pipeline.py:186,524). */
+int vs_ntotal(const vs_index* idx, int64_t* out);
+int vs_dim(const vs_index* idx, int* out);
+int vs_metric(const vs_index* idx, int* out);
+int vs_dtype(const vs_index* idx, int* out);
+
+/* Rows [0,ntotal) get labels id_base + row.  Used by the row-sharded multi-GPU
+ * index so that per-shard results carry global faiss labels. */
+int vs_set_id_base(vs_index* idx, int64_t id_base);
+
+/* faiss IndexFlat::search(n, x, k, D, I) (knn_L2sqr / knn_inner_product):
+ * exact top-k, D ascending squared-L2 or descending inner product, ties broken
+ * by the lower label, k > ntotal padded with (+FLT_MAX | -FLT_MAX, -1).
+ * Caller: FAISS.similarity_search_with_score_by_vector, reached from
+ * src/recommendation_api/mcp_book_server.py:142, candidate_builder.py:187,321,
+ * service.py:529,627.  D is n*k float32, I is n*k int64. */
+int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int64_t* I,
+              int flags, void* stream);
+
+/* faiss Index::reconstruct_n(i0, n, out) / reconstruct(i) — rows as added
+ * (bf16 storage returns the stored bf16 value widened to float32).
+ * Callers: store.index.reconstruct at candidate_builder.py:166-168, service.py:490-494. */
+int vs_reconstruct_n(vs_index* idx, int64_t i0, int64_t n, float* out, int flags, void* stream);
+
+/* faiss IndexFlat::remove_ids(IDSelectorBatch(ids)) — stable compaction; ids
+ * outside [0,ntotal) and duplicates are ignored; *nremoved = rows removed.
+ * Caller: langchain FAISS.delete (BASELINE config 5 add/remove). */
+int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremoved);
+
+/* Cosine self-join — replaces the per-student pgvector query
+ *   SELECT student_id, 1-(vec <=> src.vec) ... WHERE student_id <> $1
+ *   ORDER BY vec <=> src.vec LIMIT 15
+ * at src/graph_refresher/main.py:339-354 and src/incremental_workers/similarity/main.py:80-87.
+ * For stored rows q in [q0, q0+nq): the k rows with largest cosine similarity
+ * dot/sqrt(|a|^2 |b|^2) (ties: lower row first), excluding row q itself when
+ * exclude_self != 0.  Entries whose similarity is < min_sim (the
+ * graph_refresher's S.similarity_threshold filter, main.py:350-354) are returned
+ * as (-FLT_MAX, -1).  Zero-norm rows never match (pgvector yields NaN for them).
+ * D is nq*k similarities, I is nq*k labels (id_base applied). */
+int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_self,
+                float min_sim, float* D, int64_t* I, int flags, void* stream);
+
+/* Merge nparts per-shard top-k lists into one (faiss: the ResultHandler merge;
+ * GPU-side half of the RCCL all-gather top-k merge).  Inputs are DEVICE arrays
+ * laid out [nparts][nq][k_in] (scores + int64 labels, -1 = empty); outputs are
+ * DEVICE arrays [nq][k].  metric picks the order (L2 ascending, IP descending). */
+int vs_merge_topk(const float* D_parts, const int64_t* I_parts, int64_t nparts, int64_t nq,
+                  int64_t k_in, int64_t k, int metric, float* D, int64_t* I, void* stream);
+
+/* Writes rows x[i][j] = ((splitmix64(seed ^ ((row0+i)*d + j)) >> 40) * 2^-23) - 1
+ * (exactly representable float32 in [-1,1)) into a DEVICE buffer of rows*d floats.
+ * The same generator is restated in python for the oracle (vsearch.synth). */
+int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_t row0,
+                      void* stream);
+
+/* ---- measurement ----------------------------------------------------------
+ * When enabled, every launch of the dominant search kernel (the fused
+ * distance+top-k kernel) is bracketed by HIP events on the launch stream.
+ * vs_timer_read synchronises those events and returns the summed kernel time in
+ * milliseconds and the launch count since the last reset. */
+int vs_timer_enable(int on);
+int vs_timer_reset(void);
+int vs_timer_read(double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSEARCH_H */

@@ -1,0 +1,346 @@
+"""GPU parity: libvsearch.so (HIP, gfx950) against the CPU oracle.
+
+Every test here runs the product path through the C-ABI on cuda:0 and checks it
+with oracle/flat.py (fp64 semantics of faiss IndexFlat::search) or the C heap
+restatement oracle/faiss_flat.c.  Acceptance (oracle.flat.mismatches): labels
+equal except documented ties, scores within 1e-5 * max(1, |s|) (for squared L2
+the scale includes |q|^2 + |x|^2, the magnitude fp32 rounding acts on)."""
+
+import numpy as np
+import pytest
+
+from oracle import cfaiss, flat
+
+pytestmark = pytest.mark.gpu
+
+L2, IP = flat.METRIC_L2, flat.METRIC_INNER_PRODUCT
+
+
+@pytest.fixture(scope="module")
+def vf():
+    from vsearch import _lib
+    from vsearch import faiss as vfaiss
+
+    assert _lib.device_count() >= 1, "gpu tests need a visible MI355X"
+    return vfaiss
+
+
+def _rand(n, d, seed, kind="normal"):
+    rng = np.random.default_rng(seed)
+    if kind == "normal":
+        return rng.standard_normal((n, d)).astype(np.float32)
+    if kind == "int":
+        return rng.integers(-2, 3, size=(n, d)).astype(np.float32)
+    raise ValueError(kind)
+
+
+def _check(vf, xb, xq, k, metric):
+    index = vf.IndexFlat(xb.shape[1], metric)
+    index.add(xb)
+    D, I = index.search(xq, k)
+    Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+    assert not bad, bad[:5]
+    return D, I
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("nq", [1, 2, 3, 5, 8, 9, 20, 37, 129])
+def test_shapes_nq(vf, metric, nq):
+    xb = _rand(3000, 96, 1)
+    xq = _rand(nq, 96, 2)
+    _check(vf, xb, xq, 10, metric)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("k", [1, 2, 4, 5, 8, 9, 16, 17, 20, 30, 33, 50, 64])
+def test_k_values(vf, metric, k):
+    xb = _rand(2000, 64, 3)
+    for nq in (1, 40):
+        _check(vf, xb, _rand(nq, 64, 4 + nq), k, metric)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("n", [1, 2, 7, 127, 128, 129, 255, 256, 257, 1000])
+def test_ragged_ntotal(vf, metric, n):
+    xb = _rand(n, 40, 5)
+    for nq in (1, 4, 33):
+        _check(vf, xb, _rand(nq, 40, 6), 10, metric)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("d", [1, 3, 31, 32, 33, 100, 768, 1536, 2049])
+def test_dims(vf, metric, d):
+    xb = _rand(700, d, 7)
+    for nq in (1, 3, 25):
+        _check(vf, xb, _rand(nq, d, 8), 5, metric)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_k_exceeds_ntotal_padding(vf, metric):
+    xb = _rand(5, 16, 9)
+    for nq in (1, 30):
+        D, I = _check(vf, xb, _rand(nq, 16, 10), 12, metric)
+        assert (I[:, 5:] == -1).all()
+        assert (D[:, 5:] == flat.neutral(metric)).all()
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_empty_index(vf, metric):
+    index = vf.IndexFlat(8, metric)
+    D, I = index.search(_rand(3, 8, 11), 4)
+    assert (I == -1).all() and (D == flat.neutral(metric)).all()
+    D, I = index.search(np.zeros((0, 8), np.float32), 4)
+    assert D.shape == (0, 4) and I.shape == (0, 4)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("k", [1, 2, 4, 5, 10, 16])
+def test_ties_match_faiss_heap(vf, metric, k):
+    """Tie-heavy integer data: labels must equal the C faiss-heap restatement exactly."""
+    xb = _rand(600, 3, 12, "int")
+    for nq in (1, 7, 40):
+        xq = _rand(nq, 3, 13 + nq, "int")
+        index = vf.IndexFlat(3, metric)
+        index.add(xb)
+        D, I = index.search(xq, k)
+        Dc, Ic = cfaiss.knn_seq(xb, xq, k, metric)
+        np.testing.assert_array_equal(I, Ic)
+        np.testing.assert_array_equal(D, Dc)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_reference_tie_stub(vf, metric, golden):
+    """The reference's embedding stub [i%3]*3 with query [0,0,0]
+    (tests/test_integration_ingestion_graph.py:40-48)."""
+    _, exp = golden
+    name = "l2" if metric == L2 else "ip"
+    xb = np.array([[float(i % 3)] * 3 for i in range(341)], dtype=np.float32)
+    index = vf.IndexFlat(3, metric)
+    index.add(xb)
+    for k in (1, 4, 5, 10):
+        D, I = index.search(np.zeros((1, 3), np.float32), k)
+        np.testing.assert_array_equal(I, exp[f"tie_{name}_k{k}_I"])
+        np.testing.assert_array_equal(D, exp[f"tie_{name}_k{k}_D"])
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_golden_csv_books(vf, metric, golden, golden_vectors):
+    """BASELINE config 1: catalog_sample.csv books with deterministic embeddings."""
+    _, exp = golden
+    xb, xq, _ = golden_vectors
+    name = "l2" if metric == L2 else "ip"
+    index = vf.IndexFlat(xb.shape[1], metric)
+    index.add(xb)
+    for k in (4, 5, 10, 20, 30):
+        for q in (xq[:1], xq[:7], xq):
+            D, I = index.search(q, k)
+            Ir = exp[f"books_{name}_I"][: q.shape[0], :k]
+            Dr = exp[f"books_{name}_D"][: q.shape[0], :k]
+            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, q)
+            assert not bad, bad[:5]
+            # fp32 vs fp64 near-ties may swap neighbours; they must stay rare
+            assert (I != Ir).mean() < 1e-3
+
+
+def test_golden_csv_students_selfjoin(vf, golden, golden_vectors):
+    """graph_refresher self-join on students_sample.csv (k=15 and 50 > N-1)."""
+    _, exp = golden
+    _, _, xs = golden_vectors
+    index = vf.IndexFlatIP(xs.shape[1])
+    index.add(xs)
+    for k in (15, 50):
+        S, I = index.selfjoin(k)
+        np.testing.assert_array_equal(I, exp[f"students_k{k}_I"])
+        np.testing.assert_allclose(S, exp[f"students_k{k}_S"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("k", [1, 5, 15, 50])
+def test_selfjoin_random(vf, k):
+    x = _rand(1500, 64, 14)
+    x[17] = 0.0  # zero-norm row: never a neighbour, no neighbours (pgvector NaN)
+    index = vf.IndexFlatL2(64)
+    index.add(x)
+    S, I = index.selfjoin(k)
+    Sr, Ir = flat.pgvector_cosine_topk(x, k)
+    assert (I[17] == -1).all()
+    assert not (I == 17).any()
+    assert not (I == np.arange(1500)[:, None]).any()
+    diff = I != Ir
+    # differing labels must be score ties within fp32 rounding
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5, (q, j)
+    ok = ~diff & (I >= 0)
+    np.testing.assert_allclose(S[ok], Sr[ok], rtol=1e-5, atol=1e-6)
+
+
+def test_selfjoin_threshold_and_subrange(vf):
+    rng = np.random.default_rng(15)
+    base = rng.standard_normal((40, 32)).astype(np.float32)
+    x = np.concatenate([base, base + 0.1 * rng.standard_normal((40, 32)).astype(np.float32)])
+    index = vf.IndexFlatIP(32)
+    index.add(x)
+    S, I = index.selfjoin(15, q0=10, nq=50, min_sim=0.75)
+    Sr, Ir = flat.pgvector_cosine_topk(x, 15, q_rows=np.arange(10, 60), min_sim=0.75)
+    np.testing.assert_array_equal(I, Ir)
+    m = I >= 0
+    np.testing.assert_allclose(S[m], Sr[m], rtol=1e-5, atol=1e-6)
+    assert (S[~m] == -flat.FLT_MAX).all()
+
+
+def test_add_incremental_reconstruct_remove(vf):
+    xb = _rand(1000, 24, 16)
+    index = vf.IndexFlatL2(24)
+    for i0 in range(0, 1000, 137):
+        index.add(xb[i0:i0 + 137])
+    assert index.ntotal == 1000
+    np.testing.assert_array_equal(index.reconstruct(0), xb[0])
+    np.testing.assert_array_equal(index.reconstruct(999), xb[999])
+    np.testing.assert_array_equal(index.reconstruct_n(100, 50), xb[100:150])
+    with pytest.raises(RuntimeError):
+        index.reconstruct(1000)
+    rm = np.array([5, 0, 999, 5, 4000, -3, 500], dtype=np.int64)
+    n = index.remove_ids(rm)
+    xr, nr = flat.remove_ids(xb, rm)
+    assert n == nr == 4
+    assert index.ntotal == 996
+    np.testing.assert_array_equal(index.reconstruct_n(0, 996), xr)
+    xq = _rand(30, 24, 17)
+    D, I = index.search(xq, 7)
+    Dr, Ir = flat.knn_exact(xr, xq, 7, L2)
+    assert not flat.mismatches(D, I, Dr, Ir, L2, xr, xq)
+    index.add(xb[:10])
+    assert index.ntotal == 1006
+    index.reset()
+    assert index.ntotal == 0
+
+
+def test_remove_many_chunks(vf):
+    """remove_ids across several compaction chunks (chunk = 256 MiB of rows)."""
+    d = 1536
+    n = 60000  # 368 MB -> two chunks
+    index = vf.IndexFlatIP(d)
+    index.add_synthetic(n, seed=77)
+    rng = np.random.default_rng(18)
+    rm = rng.choice(n, 3000, replace=False).astype(np.int64)
+    assert index.remove_ids(rm) == 3000
+    keep = np.setdiff1d(np.arange(n), rm)
+    from vsearch.synth import synthetic_rows
+
+    for r in (0, 1, 2, keep.size // 2, keep.size - 1):
+        np.testing.assert_array_equal(index.reconstruct(r), synthetic_rows(keep[r], 1, d, 77)[0])
+
+
+def test_synthetic_generator_matches_host(vf):
+    from vsearch.synth import synthetic_rows
+
+    index = vf.IndexFlatL2(1536)
+    index.add_synthetic(300, seed=1234, row0=9_999_800)
+    np.testing.assert_array_equal(index.reconstruct_n(0, 300),
+                                  synthetic_rows(9_999_800, 300, 1536, 1234))
+
+
+def test_device_pointer_search(vf):
+    torch = pytest.importorskip("torch")
+    xb = _rand(5000, 128, 19)
+    xq = _rand(64, 128, 20)
+    index = vf.IndexFlatIP(128)
+    index.add(xb)
+    q = torch.from_numpy(xq).cuda()
+    D = torch.empty((64, 10), dtype=torch.float32, device="cuda")
+    I = torch.empty((64, 10), dtype=torch.int64, device="cuda")
+    index.search_device(q.data_ptr(), 64, 10, D.data_ptr(), I.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    Dh, Ih = index.search(xq, 10)
+    np.testing.assert_array_equal(I.cpu().numpy(), Ih)
+    np.testing.assert_array_equal(D.cpu().numpy(), Dh)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_merge_topk_kernel(vf, metric):
+    """vs_merge_topk (the post-all-gather merge) equals one index over all rows."""
+    torch = pytest.importorskip("torch")
+    import ctypes
+
+    from vsearch import _lib
+
+    xb = _rand(4000, 32, 21)
+    xq = _rand(50, 32, 22)
+    k = 10
+    parts = []
+    for lo, hi in ((0, 1000), (1000, 2500), (2500, 4000)):
+        idx = vf.IndexFlat(32, metric)
+        idx.add(xb[lo:hi])
+        idx.set_id_base(lo)
+        parts.append(idx.search(xq, k))
+    Dp = torch.from_numpy(np.stack([p[0] for p in parts])).cuda()
+    Ip = torch.from_numpy(np.stack([p[1] for p in parts])).cuda()
+    D = torch.empty((50, k), dtype=torch.float32, device="cuda")
+    I = torch.empty((50, k), dtype=torch.int64, device="cuda")
+    _lib.check(_lib.load().vs_merge_topk(
+        ctypes.c_void_p(Dp.data_ptr()), ctypes.c_void_p(Ip.data_ptr()), 3, 50, k, k, metric,
+        ctypes.c_void_p(D.data_ptr()), ctypes.c_void_p(I.data_ptr()), None))
+    torch.cuda.synchronize()
+    Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+    bad = flat.mismatches(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir, metric, xb, xq)
+    assert not bad, bad[:5]
+
+
+def test_errors(vf):
+    index = vf.IndexFlatL2(16)
+    index.add(_rand(10, 16, 23))
+    with pytest.raises(AssertionError):
+        index.search(_rand(2, 15, 24), 3)
+    with pytest.raises(AssertionError):
+        index.search(_rand(2, 16, 24), 0)
+    with pytest.raises(AssertionError):
+        index.add(_rand(2, 17, 24))
+    with pytest.raises(RuntimeError):
+        index.search(_rand(2, 16, 24), 65)  # above VS_MAX_K
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_large_synthetic_sampled(vf, metric):
+    """1M x 1536 (BASELINE config 2 shape, B=1024) checked on a query sample."""
+    from vsearch.synth import synthetic_rows
+
+    n, d, k = 1_000_000, 1536, 10
+    index = vf.IndexFlat(d, metric)
+    index.reserve(n)
+    index.add_synthetic(n, seed=1234)
+    xq = synthetic_rows(50_000_000, 1024, d, 5678)
+    D, I = index.search(xq, k)
+    # property checks on every query: sorted, unique, in range
+    assert (I >= 0).all() and (I < n).all()
+    if metric == L2:
+        assert (np.diff(D, axis=1) >= 0).all()
+    else:
+        assert (np.diff(D, axis=1) <= 0).all()
+    # exact check on a sample of queries against a chunked fp64 oracle
+    sample = [0, 1, 511, 1023]
+    best_k, best_i = None, None
+    step = 100_000
+    for r0 in range(0, n, step):
+        xb = synthetic_rows(r0, step, d, 1234)
+        s = flat.exact_scores(xb, xq[sample], metric)
+        key = s if metric == L2 else -s
+        ids = np.broadcast_to(np.arange(r0, r0 + step), key.shape)
+        if best_k is None:
+            best_k, best_i = key, ids
+        else:
+            best_k = np.concatenate([best_k, key], axis=1)
+            best_i = np.concatenate([best_i, ids], axis=1)
+        part = np.argpartition(best_k, k, axis=1)[:, : k + 1]
+        best_k = np.take_along_axis(best_k, part, axis=1)
+        best_i = np.take_along_axis(best_i, part, axis=1)
+    for row, q in enumerate(sample):
+        o = np.lexsort((best_i[row], best_k[row]))[:k]
+        ref_i = best_i[row][o]
+        ref_s = best_k[row][o] if metric == L2 else -best_k[row][o]
+        got_s = D[q]
+        for j in range(k):
+            tol = 1e-5 * max(1.0, abs(ref_s[j]), 1100.0 if metric == L2 else 0.0)
+            assert abs(got_s[j] - ref_s[j]) <= tol, (q, j, got_s[j], ref_s[j])
+            if I[q, j] != ref_i[j]:
+                assert abs(ref_s[j] - got_s[j]) <= tol
