@@ -176,11 +176,11 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const float* qaux, int 
   part.KP = KP;
 
   const bool gemv = (mode == MODE_IP || mode == MODE_L2) && self0 < 0 && nq <= kGemvMaxQ &&
-                    (size_t)kGemvMaxQ * idx->ld * sizeof(float) <= 64 * 1024;
+                    (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
   if (gemv) {
     const int gmode = mode == MODE_L2 ? MODE_L2D : MODE_IP;
     int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
-    part.P = nblocks * 4;
+    part.P = nblocks;
     const int nql = nq <= 2 ? nq : (nq <= 4 ? 4 : 8);
     const size_t n = (size_t)nql * part.P * KP;
     VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
@@ -412,8 +412,16 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
     for (int64_t c0 = 0; c0 < n; c0 += chunk) {
       const int64_t nc = std::min(chunk, n - c0);
       const int64_t nq_pad = round_up(std::max<int64_t>(nc, kGemvMaxQ), kBQ);
-      VS_HIP(hipMemsetAsync(qbuf, 0, (size_t)nq_pad * idx->ld * sizeof(float), st),
-             "vs_search: zero queries");
+      // zero what the copy leaves: padding rows, and the column tail when d < ld
+      if (idx->d == idx->ld) {
+        if (nq_pad > nc)
+          VS_HIP(hipMemsetAsync(qbuf + nc * idx->ld, 0,
+                                (size_t)(nq_pad - nc) * idx->ld * sizeof(float), st),
+                 "vs_search: zero queries");
+      } else {
+        VS_HIP(hipMemsetAsync(qbuf, 0, (size_t)nq_pad * idx->ld * sizeof(float), st),
+               "vs_search: zero queries");
+      }
       VS_HIP(hipMemcpy2DAsync(qbuf, idx->ld * sizeof(float), x + c0 * idx->d,
                               (size_t)idx->d * sizeof(float), (size_t)idx->d * sizeof(float),
                               (size_t)nc, kind, st),

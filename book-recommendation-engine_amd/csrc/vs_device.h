@@ -65,4 +65,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Merges two sorted lists held in LDS (a, b) into registers (best KP of the union).
+template <int KP, typename IdT>
+__device__ __forceinline__ void merge2_sorted(const float* ak, const IdT* ai, const float* bk,
+                                              const IdT* bi, float (&ok)[KP], IdT (&oi)[KP]) {
+  int ia = 0, ib = 0;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    const float ka = ak[ia], kb = bk[ib];
+    const IdT xa = ai[ia], xb = bi[ib];
+    const bool ta = !lex_less(kb, xb, ka, xa);
+    ok[j] = ta ? ka : kb;
+    oi[j] = ta ? xa : xb;
+    ia += ta ? 1 : 0;
+    ib += ta ? 0 : 1;
+  }
+}
+
 }  // namespace vs

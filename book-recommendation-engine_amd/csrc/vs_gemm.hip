@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
   const int gq = qt * kBQ + qloc;
   float qa = 0.0f;
   if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa = qaux[gq];
-  const int64_t selfrow = self0 >= 0 ? self0 + gq : -1;
+  const int selfrow = self0 >= 0 ? (int)(self0 + gq) : -1;
 
   float lk[KP];
   int li[KP];
@@ -70,14 +70,24 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
 
   const float* Qblk = Q + (int64_t)qt * kBQ * ld;
   // glds geometry: a wave instruction moves 8 rows x 128 B; wave w stages row
-  // groups 4w..4w+3 of both operands.
+  // groups g = 4w..4w+3 of both operands.  The per-lane source offset is 32-bit
+  // on a wave-uniform base (saddr form); the swizzle (row >> 1) & 7 depends on
+  // the group only through g & 1, so two lane offsets cover all four groups.
   const int srow = lane >> 3;
   const int sphys = lane & 7;
+  const uint32_t ldb = (uint32_t)ld * 4u;  // row stride in bytes
+  uint32_t soff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int row = par * 8 + srow;  // any group with g & 1 == par has this swizzle
+    const int c = sphys ^ ((row >> 1) & 7);
+    soff[par] = (uint32_t)(w * 32 + srow) * ldb + (uint32_t)c * 16u;
+  }
   // fragment-read geometry: (row >> 1) & 7 is the same for every subtile.
   const int fsw = (c32 >> 1) & 7;
 
   for (int t = t0; t < t1; ++t) {
-    const float* Xblk = X + (int64_t)t * kBN * ld;
+    const char* Xblk = (const char*)(X + (int64_t)t * kBN * ld);
     f32x16 acc[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -88,15 +98,14 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
     auto stage = [&](int buf, int kb) {
       float* dX = smem + buf * (2 * kBN * kBK);
       float* dQ = dX + kBN * kBK;
+      const char* xs = Xblk + kb * 4;
+      const char* qs = (const char*)Qblk + kb * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int g = w * 4 + i;
-        const int row = g * 8 + srow;
-        const int c = sphys ^ ((row >> 1) & 7);
-        __builtin_amdgcn_global_load_lds(Xblk + (int64_t)row * ld + kb + c * 4,
-                                         VS_LDS(dX + g * 256), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(Qblk + (int64_t)row * ld + kb + c * 4,
-                                         VS_LDS(dQ + g * 256), 16, 0, 0);
+        const uint32_t o = soff[i & 1] + (uint32_t)(i * 8) * ldb;
+        __builtin_amdgcn_global_load_lds(xs + o, VS_LDS(dX + g * 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(qs + o, VS_LDS(dQ + g * 256), 16, 0, 0);
       }
     };
 
@@ -126,18 +135,19 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
       __syncthreads();
     }
 
-    // Epilogue.  Phase A (unrolled, branch-free): scores -> keys in place, and a
-    // 64-bit mask of the values that beat the lane's current worst entry.  The
-    // threshold only tightens while inserting, so testing against the value it
-    // had at the start admits a superset.  Phase B (rare after the first tiles):
-    // the lane parks its 64 keys in a private column of the (now idle) staging
-    // LDS and inserts the flagged ones, so the insertion code exists once.
+    // Epilogue, one 32-row subtile at a time.  Phase A (unrolled, branch-free):
+    // scores -> keys, and a 16-bit mask of the values that beat the lane's
+    // current worst entry (the threshold only tightens while inserting, so the
+    // value it had at the start of the subtile admits a superset).  Phase B (rare
+    // after the first tiles): the lane parks the 16 keys in a private column of
+    // the (now idle) staging LDS and inserts the flagged ones, so the insertion
+    // code exists once per subtile instead of once per value.
     const int r0 = t * kBN;
-    const float tk = lk[KP - 1];
-    const int ti = li[KP - 1];
-    uint64_t m = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
+      const float tk = lk[KP - 1];
+      const int ti = li[KP - 1];
+      uint32_t m = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int rb = r0 + 32 * s + 8 * j + 4 * h;
@@ -156,23 +166,20 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
             key = -(v * (qa * xa[i]));
           }
           acc[s][j * 4 + i] = key;
-          const bool cand = row < ntotal && (int64_t)row != selfrow && lex_less(key, row, tk, ti);
-          m |= (uint64_t)cand << (s * 16 + j * 4 + i);
+          const bool cand = row < ntotal && row != selfrow && lex_less(key, row, tk, ti);
+          m |= (uint32_t)cand << (j * 4 + i);
         }
       }
-    }
-    if (m) {
+      if (m) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) smem[(s * 16 + r) * 256 + tid] = acc[s][r];
+        for (int r = 0; r < 16; ++r) smem[r * 256 + tid] = acc[s][r];
+        do {
+          const int bi = __builtin_ctz(m);
+          m &= m - 1;
+          const int row = r0 + 32 * s + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+          list_insert<KP, int>(lk, li, smem[bi * 256 + tid], row);
+        } while (m);
       }
-      do {
-        const int bi = __builtin_ctzll(m);
-        m &= m - 1;
-        const int row = r0 + 32 * (bi >> 4) + (bi & 3) + 8 * ((bi >> 2) & 3) + 4 * h;
-        list_insert<KP, int>(lk, li, smem[bi * 256 + tid], row);
-      } while (m);
     }
     // The next tile's first stage overwrites the LDS the epilogue may have used.
     __syncthreads();

@@ -74,10 +74,33 @@ __global__ __launch_bounds__(256) void gemv_topk_f32(const float* __restrict__ X
     }
   }
 
+  // In-block merge: the 4 waves' lists of each query meet in LDS (after the
+  // queries), wave 0 folds them, and the block writes one list per query.
+  float* mk = sq + (int64_t)NQ * ld;      // [4][NQ][KP]
+  int* mi = (int*)(mk + 4 * NQ * KP);     // [4][NQ][KP]
   if (lane < NQ) {
-    const int P = gridDim.x * 4;
-    float* ok = pkey + ((int64_t)lane * P + blockIdx.x * 4 + w) * KP;
-    int* oi = pid + ((int64_t)lane * P + blockIdx.x * 4 + w) * KP;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      mk[(w * NQ + lane) * KP + j] = lk[j];
+      mi[(w * NQ + lane) * KP + j] = li[j];
+    }
+  }
+  __syncthreads();
+  if (w == 0 && lane < NQ) {
+#pragma unroll
+    for (int o = 1; o < 4; ++o) {
+      merge2_sorted<KP, int>(mk + lane * KP, mi + lane * KP, mk + (o * NQ + lane) * KP,
+                             mi + (o * NQ + lane) * KP, lk, li);
+      if (o < 3) {
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+          mk[lane * KP + j] = lk[j];
+          mi[lane * KP + j] = li[j];
+        }
+      }
+    }
+    float* ok = pkey + ((int64_t)lane * gridDim.x + blockIdx.x) * KP;
+    int* oi = pid + ((int64_t)lane * gridDim.x + blockIdx.x) * KP;
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
       ok[j] = lk[j];
@@ -92,7 +115,7 @@ static hipError_t gemv_dispatch_q(int mode, const float* X, const float* Q, int6
   const int ntot16 = (ntotal + 15) & ~15;
   int rpb = (ntot16 + nblocks - 1) / nblocks;
   rpb = (rpb + 15) & ~15;
-  const size_t lds = (size_t)NQ * ld * sizeof(float);
+  const size_t lds = (size_t)NQ * ld * sizeof(float) + (size_t)4 * NQ * KP * 8;
   if (mode == MODE_L2D)
     hipLaunchKernelGGL((gemv_topk_f32<NQ, KP, MODE_L2D>), dim3(nblocks), dim3(256), lds, st, X, Q,
                        ld, ntotal, rpb, part.key, part.id);
@@ -122,7 +145,7 @@ static hipError_t gemv_dispatch(int mode, int nq, const float* X, const float* Q
 
 hipError_t launch_gemv_topk(int KP, int mode, int nq, const float* X, const float* Q, int64_t ld,
                             int ntotal, int nblocks, Partials part, hipStream_t st) {
-  if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks * 4 || ld % 4 != 0)
+  if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks || ld % 4 != 0)
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:

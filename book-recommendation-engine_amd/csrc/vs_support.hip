@@ -26,7 +26,7 @@ namespace vs {
 template <int KP, typename IdT>
 __device__ __forceinline__ void wave_tree_merge(float (&lk)[KP], IdT (&li)[KP], float* sk,
                                                 IdT* si, int lane) {
-  // sk/si: LDS [64][KP]
+  // sk/si: LDS [64][KP]; on return lane 0 holds the merge of the 64 lists.
   for (int step = 1; step < 64; step <<= 1) {
     if ((lane & (step - 1)) == 0) {
 #pragma unroll
@@ -36,23 +36,9 @@ __device__ __forceinline__ void wave_tree_merge(float (&lk)[KP], IdT (&li)[KP], 
       }
     }
     __syncthreads();
-    if ((lane & (2 * step - 1)) == 0) {
-      const float* ak = sk + lane * KP;
-      const IdT* ai = si + lane * KP;
-      const float* bk = sk + (lane + step) * KP;
-      const IdT* bi = si + (lane + step) * KP;
-      int ia = 0, ib = 0;
-#pragma unroll
-      for (int j = 0; j < KP; ++j) {
-        const float ka = ak[ia], kb = bk[ib];
-        const IdT xa = ai[ia], xb = bi[ib];
-        const bool ta = !lex_less(kb, xb, ka, xa);
-        lk[j] = ta ? ka : kb;
-        li[j] = ta ? xa : xb;
-        ia += ta ? 1 : 0;
-        ib += ta ? 0 : 1;
-      }
-    }
+    if ((lane & (2 * step - 1)) == 0)
+      merge2_sorted<KP, IdT>(sk + lane * KP, si + lane * KP, sk + (lane + step) * KP,
+                             si + (lane + step) * KP, lk, li);
     __syncthreads();
   }
 }
@@ -119,27 +105,55 @@ __device__ __forceinline__ void emit_result(int mode, float key, int64_t id, int
   *I = id + id_base;
 }
 
+// Multi-level list merge.  Every partial list is sorted (entry 0 best), so a wave
+// loads one whole list per lane (vector loads, all in flight together) and
+// tree-merges 64 lists in 6 rounds; levels repeat until one list per query is
+// left, which is emitted as (D, I) rows (grid x = query, y = list group).
 template <int KP>
-__global__ __launch_bounds__(64) void merge_partials_kernel(const float* __restrict__ pkey,
-                                                            const int* __restrict__ pid, int P,
-                                                            int k, int mode, int64_t id_base,
-                                                            float min_score, float* __restrict__ D,
-                                                            int64_t* __restrict__ I, int64_t ldo) {
+__global__ __launch_bounds__(64) void merge_lists_kernel(
+    const float* __restrict__ pkey, const int* __restrict__ pid, int P, float* __restrict__ okey,
+    int* __restrict__ oid, int P2, int emit, int k, int mode, int64_t id_base, float min_score,
+    float* __restrict__ D, int64_t* __restrict__ I, int64_t ldo) {
   __shared__ float sk[64 * KP];
   __shared__ int si[64 * KP];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
+  const int g = blockIdx.y;
+  const int p = g * 64 + lane;
   float lk[KP];
   int li[KP];
-  list_init<KP, int>(lk, li);
-  const int64_t n = (int64_t)P * KP;
-  const float* ck = pkey + (int64_t)q * n;
-  const int* ci = pid + (int64_t)q * n;
-  for (int64_t c = lane; c < n; c += 64) {
-    const int id = ci[c];
-    if (id >= 0) list_insert<KP, int>(lk, li, ck[c], id);
+  if (p < P) {
+    const f32x4* ks = (const f32x4*)(pkey + ((int64_t)q * P + p) * KP);
+    const int4* is = (const int4*)(pid + ((int64_t)q * P + p) * KP);
+#pragma unroll
+    for (int j = 0; j < KP / 4; ++j) {
+      const f32x4 kv = ks[j];
+      const int4 iv = is[j];
+      lk[4 * j + 0] = kv.x;
+      lk[4 * j + 1] = kv.y;
+      lk[4 * j + 2] = kv.z;
+      lk[4 * j + 3] = kv.w;
+      li[4 * j + 0] = iv.x;
+      li[4 * j + 1] = iv.y;
+      li[4 * j + 2] = iv.z;
+      li[4 * j + 3] = iv.w;
+    }
+  } else {
+    list_init<KP, int>(lk, li);
   }
   wave_tree_merge<KP, int>(lk, li, sk, si, lane);
+  if (!emit) {
+    if (lane == 0) {
+      float* ok = okey + ((int64_t)q * P2 + g) * KP;
+      int* oi = oid + ((int64_t)q * P2 + g) * KP;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        ok[j] = lk[j];
+        oi[j] = li[j];
+      }
+    }
+    return;
+  }
   if (lane == 0) {
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
@@ -153,26 +167,59 @@ __global__ __launch_bounds__(64) void merge_partials_kernel(const float* __restr
                             I + q * ldo + lane);
 }
 
+template <int KP>
+static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t id_base,
+                               float min_score, float* D, int64_t* I, int64_t ldo,
+                               hipStream_t st) {
+  const float* ck = part.key;
+  const int* ci = part.id;
+  int P = part.P;
+  void* tmp[2] = {nullptr, nullptr};
+  int cur = 0;
+  hipError_t e = hipSuccess;
+  while (P > 64 && e == hipSuccess) {
+    const int P2 = (P + 63) / 64;
+    void* buf = nullptr;
+    e = hipMallocAsync(&buf, (size_t)nq * P2 * KP * (sizeof(float) + sizeof(int)), st);
+    if (e != hipSuccess) break;
+    float* ok = (float*)buf;
+    int* oi = (int*)(ok + (size_t)nq * P2 * KP);
+    hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, P2), dim3(64), 0, st, ck, ci, P, ok, oi,
+                       P2, 0, k, mode, id_base, min_score, D, I, ldo);
+    e = hipGetLastError();
+    if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
+    tmp[cur] = buf;
+    ck = ok;
+    ci = oi;
+    P = P2;
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, 1), dim3(64), 0, st, ck, ci, P,
+                       (float*)nullptr, (int*)nullptr, 1, 1, k, mode, id_base, min_score, D, I,
+                       ldo);
+    e = hipGetLastError();
+  }
+  if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
+  return e;
+}
+
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
                                  hipStream_t st) {
-  if (k < 1 || k > part.KP || nq < 0) return hipErrorInvalidValue;
+  if (k < 1 || k > part.KP || nq < 0 || part.P < 1) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   switch (part.KP) {
-#define VS_MERGE_CASE(KPV)                                                                     \
-  case KPV:                                                                                   \
-    hipLaunchKernelGGL((merge_partials_kernel<KPV>), dim3(nq), dim3(64), 0, st, part.key,     \
-                       part.id, part.P, k, mode, id_base, min_score, D, I, ldo);              \
-    break;
-    VS_MERGE_CASE(8)
-    VS_MERGE_CASE(16)
-    VS_MERGE_CASE(32)
-    VS_MERGE_CASE(64)
-#undef VS_MERGE_CASE
+    case 8:
+      return merge_levels<8>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+    case 16:
+      return merge_levels<16>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+    case 32:
+      return merge_levels<32>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+    case 64:
+      return merge_levels<64>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 template <int KP>

@@ -282,8 +282,9 @@ _FOURCC = {METRIC_L2: b"IxF2", METRIC_INNER_PRODUCT: b"IxFI"}
 
 def write_index(index: IndexFlat, fname) -> None:
     """faiss.write_index for flat indexes (streams rows out in bounded chunks)."""
-    if not isinstance(index, IndexFlat):
-        raise TypeError("write_index: only flat indexes are supported")
+    if not all(hasattr(index, a) for a in ("d", "ntotal", "metric_type", "reconstruct_n")) \
+            or index.metric_type not in _FOURCC:
+        raise TypeError("write_index: only flat L2 / inner-product indexes are supported")
     ntotal = index.ntotal
     with open(fname, "wb") as f:
         f.write(_FOURCC[index.metric_type])

@@ -131,11 +131,15 @@ class ShardedIndexFlat:
     def _gather(self, Dt, It):
         import torch
 
-        Dall = torch.empty((self.world,) + tuple(Dt.shape), dtype=Dt.dtype, device=Dt.device)
-        Iall = torch.empty((self.world,) + tuple(It.shape), dtype=It.dtype, device=It.device)
+        # flat (world*nq, k) outputs: the layout every backend accepts
+        Dall = torch.empty((self.world * Dt.shape[0],) + tuple(Dt.shape[1:]), dtype=Dt.dtype,
+                           device=Dt.device)
+        Iall = torch.empty((self.world * It.shape[0],) + tuple(It.shape[1:]), dtype=It.dtype,
+                           device=It.device)
         self._dist.all_gather_into_tensor(Dall, Dt.contiguous(), group=self.group)
         self._dist.all_gather_into_tensor(Iall, It.contiguous(), group=self.group)
-        return Dall, Iall
+        return (Dall.view((self.world,) + tuple(Dt.shape)),
+                Iall.view((self.world,) + tuple(It.shape)))
 
     def merge_device(self, Dall, Iall, nq: int, k_in: int, k: int, stream: int = 0):
         import torch

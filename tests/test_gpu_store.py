@@ -1,0 +1,118 @@
+"""GPU: the drop-in store and the student self-join end to end on libvsearch,
+reproducing the reference call sites on the CSV sample (BASELINE config 1)."""
+
+import numpy as np
+import pytest
+
+from oracle import flat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def catalog_store(golden):
+    from vsearch import langchain as vlc
+    from vsearch.synth import SynthEmbeddings
+
+    inputs, _ = golden
+    # book_vector/main.py:469 full rebuild: FAISS.from_texts(texts, embeddings, metadatas=...)
+    return vlc.FAISS.from_texts(inputs["book_texts"], SynthEmbeddings(),
+                                metadatas=inputs["book_metadata"])
+
+
+def test_search_catalog_flow(catalog_store, golden):
+    """mcp_book_server.py:142-146: similarity_search(keyword, k) -> book_id + snippet[:200]."""
+    inputs, exp = golden
+    for qi, kw in enumerate(inputs["keywords"][:16]):
+        docs = catalog_store.similarity_search(kw, k=5)
+        results = [{"book_id": d.metadata["book_id"], "snippet": d.page_content[:200]} for d in docs]
+        want = exp["books_l2_I"][341 + qi, :5]
+        pos = {m["book_id"]: i for i, m in enumerate(inputs["book_metadata"])}
+        assert [pos[r["book_id"]] for r in results] == want.tolist()
+        assert all(len(r["snippet"]) <= 200 for r in results)
+
+
+def test_scores_are_faiss_D(catalog_store, golden_vectors, golden):
+    _, exp = golden
+    _, xq, _ = golden_vectors
+    res = catalog_store.similarity_search_with_score_by_vector(xq[400], k=10)
+    D = np.array([s for _, s in res], dtype=np.float32)
+    np.testing.assert_allclose(D, exp["books_l2_D"][400, :10], rtol=1e-5, atol=1e-5)
+
+
+def test_delete_add_save_load(tmp_path, golden):
+    from vsearch import langchain as vlc
+    from vsearch.synth import SynthEmbeddings
+
+    inputs, _ = golden
+    emb = SynthEmbeddings()
+    texts = inputs["book_texts"][:50]
+    metas = inputs["book_metadata"][:50]
+    ids = [m["book_id"] for m in metas]
+    store = vlc.FAISS.from_texts(texts, emb, metadatas=metas, ids=ids)
+    assert store.delete(["B002", "B010"])
+    assert store.index.ntotal == 48
+    assert "B002" not in store.index_to_docstore_id.values()
+    store.add_texts([texts[1]], metadatas=[metas[1]], ids=["B002-v2"])
+    assert store.index_to_docstore_id[48] == "B002-v2"
+    top = store.similarity_search(texts[1], k=1)
+    assert top[0].id == "B002-v2"
+    store.save_local(str(tmp_path))
+    loaded = vlc.FAISS.load_local(str(tmp_path), emb, allow_dangerous_deserialization=True)
+    assert loaded.index.ntotal == 49
+    np.testing.assert_array_equal(loaded.index.reconstruct_n(0, 49),
+                                  store.index.reconstruct_n(0, 49))
+    q = emb.embed_query("dragons and magic")
+    a = [d.id for d in store.similarity_search_by_vector(q, k=7)]
+    b = [d.id for d in loaded.similarity_search_by_vector(q, k=7)]
+    assert a == b
+
+
+def test_student_neighbours(golden, golden_vectors):
+    from vsearch.students import pgvector_quantize, student_neighbours, student_neighbours_of
+
+    inputs, _ = golden
+    keys = inputs["student_keys"]
+    _, _, xs = golden_vectors
+    rows = student_neighbours(keys, xs, k=15, threshold=None)
+    xq = pgvector_quantize(xs)
+    S, I = flat.pgvector_cosine_topk(xq, 15)
+    want = [(keys[a], keys[int(b)], float(S[a, j])) for a in range(25) for j, b in enumerate(I[a])
+            if b >= 0]
+    assert [(a, b) for a, b, _ in rows] == [(a, b) for a, b, _ in want]
+    np.testing.assert_allclose([s for *_, s in rows], [s for *_, s in want], rtol=1e-5, atol=1e-6)
+    # the refresher's threshold: random synthetic students are far below 0.75
+    assert student_neighbours(keys, xs, k=15, threshold=0.75) == []
+    one = student_neighbours_of(keys[3], keys, xs, k=15)
+    assert one == [r for r in rows if r[0] == keys[3]]
+
+
+def test_sharded_single_rank_nccl():
+    """The multi-GPU code path with world_size 1 over RCCL (merge kernel included)."""
+    import os
+
+    torch = pytest.importorskip("torch")
+    import torch.distributed as dist
+
+    from vsearch import faiss as vfaiss
+    from vsearch.sharded import ShardedIndexFlat
+    from vsearch.synth import synthetic_rows
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        idx = ShardedIndexFlat(64, vfaiss.METRIC_INNER_PRODUCT, device=0)
+        idx.add_synthetic(20000, seed=3)
+        xq = synthetic_rows(10**6, 40, 64, 4)
+        D, I = idx.search(xq, 10)
+        xb = synthetic_rows(0, 20000, 64, 3)
+        Dr, Ir = flat.knn_exact(xb, xq, 10, vfaiss.METRIC_INNER_PRODUCT)
+        assert not flat.mismatches(D, I, Dr, Ir, vfaiss.METRIC_INNER_PRODUCT, xb, xq)
+        Dd, Id = idx.search_device(torch.from_numpy(xq).cuda(), 10,
+                                   stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(Id.cpu().numpy(), I)
+    finally:
+        dist.destroy_process_group()

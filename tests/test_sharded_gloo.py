@@ -1,0 +1,93 @@
+"""CPU, world_size 2 (gloo): the row-sharded index's layout, label bases,
+all-gather and merge reproduce the single-index result, ties included.
+
+Each rank's shard is the oracle-backed test double and the merge is the
+oracle's (faiss tie rule), because there is no GPU here; on the GPU the shard is
+libvsearch and the merge is vs_merge_topk (test_gpu_parity.py::test_merge_topk_kernel)."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, metric, q):
+    import sys
+
+    sys.path[:0] = q["paths"]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from helpers import OracleIndex, oracle_merge
+        from oracle import flat
+        from vsearch.sharded import ShardedIndexFlat, shard_bounds
+
+        rng = np.random.default_rng(0)
+        x = rng.integers(-2, 3, size=(203, 4)).astype(np.float32)  # tie-heavy
+        xq = rng.integers(-2, 3, size=(9, 4)).astype(np.float32)
+        idx = ShardedIndexFlat(4, metric, shard=OracleIndex(4, metric), merge=oracle_merge)
+        idx.add_global(x)
+        assert idx.ntotal == 203
+        lo, hi = shard_bounds(203, world, rank)
+        assert idx.shard.ntotal == hi - lo
+        res = {}
+        for k in (1, 4, 10):
+            D, I = idx.search(xq, k)
+            Dr, Ir = flat.knn_exact(x, xq, k, metric)
+            res[k] = (np.array_equal(I, Ir), np.array_equal(D, Dr))
+        # removals compact inside shards and shift later bases
+        rm = np.array([0, 5, 150, 202, 999], dtype=np.int64)
+        n = idx.remove_ids(rm)
+        xr, nr = flat.remove_ids(x, rm)
+        D, I = idx.search(xq, 6)
+        Dr, Ir = flat.knn_exact(xr, xq, 6, metric)
+        res["remove"] = (n == nr, np.array_equal(I, Ir), idx.ntotal == xr.shape[0])
+        # appends land on the last shard with labels continuing at ntotal
+        idx.add_global(x[:7])
+        x2 = np.concatenate([xr, x[:7]])
+        D, I = idx.search(xq, 8)
+        Dr, Ir = flat.knn_exact(x2, xq, 8, metric)
+        res["append"] = (np.array_equal(I, Ir),)
+        if rank == 0:
+            q["out"] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_sharded_search_equals_single_index(metric):
+    import sys
+
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    q = mgr.dict()
+    q["paths"] = [p for p in sys.path if p]
+    mp.spawn(_worker, args=(world, port, metric, q), nprocs=world, join=True)
+    out = dict(q["out"])
+    for key, flags in out.items():
+        assert all(flags), (key, flags)
+
+
+def test_shard_bounds_cover_rows():
+    from vsearch.sharded import shard_bounds
+
+    for n in (0, 1, 7, 10_000_000):
+        for g in (1, 2, 3, 8):
+            spans = [shard_bounds(n, g, r) for r in range(g)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(g - 1))

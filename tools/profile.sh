@@ -1,0 +1,21 @@
+#!/bin/bash
+# Collects the rocprofv3 evidence for bench.py on one MI355X (run through gpurun):
+#   1) --kernel-trace --stats       per-kernel durations (must agree with bench.py's HIP events)
+#   2) --pmc FETCH_SIZE             HBM read traffic per dispatch (own pass)
+#   3) --pmc WRITE_SIZE             HBM write traffic per dispatch (own pass)
+# Usage: tools/profile.sh <tag> [bench args...]
+set -u
+TAG=${1:-r01}; shift || true
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_${TAG}
+mkdir -p "$OUT"
+ARGS=("$@")
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
+  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "${ARGS[@]}" > "$OUT/bench_trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
+  -- python3 bench.py --steps 1 --warmup 0 --batch1-steps 3 --no-cpu-baseline "${ARGS[@]}" > "$OUT/bench_fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
+  -- python3 bench.py --steps 1 --warmup 0 --batch1-steps 3 --no-cpu-baseline "${ARGS[@]}" > "$OUT/bench_write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 1; }
+find "$OUT" -name "*.csv" | head -20
+echo "profile ok"
