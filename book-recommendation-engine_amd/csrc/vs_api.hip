@@ -1,8 +1,8 @@
 // vs_api.hip — the C-ABI of libvsearch.so (declared in include/vsearch.h).
 //
 // A vs_index is one device's exact flat index: library-owned row storage in HBM
-// (fp32, stride `ld` floats, zero padding), the squared norms of every row, and
-// ntotal.  It mirrors faiss::IndexFlat (faiss-cpu 1.11.0, not vendored; see
+// (fp32 or bf16 elements, stride `ld` elements = a multiple of 128 B, zero
+// padding), the squared norms of every row, and ntotal.  It mirrors faiss::IndexFlat (faiss-cpu 1.11.0, not vendored; see
 // /root/reference/poetry.lock:866-867): add copies the caller's rows, search
 // writes caller-allocated D/I, remove_ids compacts stably.
 //
@@ -28,11 +28,14 @@ struct vs_index {
   int metric = VS_METRIC_L2;
   int dtype = VS_DTYPE_F32;
   int device = 0;
-  int64_t ld = 0;        // row stride in floats (multiple of kBK)
+  int esize = 4;         // bytes per stored element (4 fp32, 2 bf16)
+  int64_t ld = 0;        // row stride in elements (ld * esize is a multiple of 128)
   int64_t ntotal = 0;
   int64_t capacity = 0;  // rows allocated (multiple of kRowPad, >= ntotal + kBQ)
   int64_t id_base = 0;
-  float* codes = nullptr;  // [capacity][ld]
+  char* codes = nullptr;   // [capacity][ld] elements
+  int64_t rowbytes() const { return ld * esize; }
+  char* row(int64_t r) const { return codes + r * rowbytes(); }
   float* norms = nullptr;  // [capacity] squared L2 norms
   std::shared_mutex mu;
 };
@@ -123,13 +126,13 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   const int64_t need = round_up(rows + kBQ, kRowPad);
   if (need <= idx->capacity) return VS_OK;
   int64_t cap = std::max(need, round_up(idx->capacity + idx->capacity / 2, kRowPad));
-  float* codes = nullptr;
+  char* codes = nullptr;
   float* norms = nullptr;
-  hipError_t e = hipMalloc(&codes, (size_t)cap * idx->ld * sizeof(float));
+  hipError_t e = hipMalloc(&codes, (size_t)cap * idx->rowbytes());
   if (e != hipSuccess) {
     // retry without the growth headroom
     cap = need;
-    e = hipMalloc(&codes, (size_t)cap * idx->ld * sizeof(float));
+    e = hipMalloc(&codes, (size_t)cap * idx->rowbytes());
     if (e != hipSuccess) return hip_fail(e, "vs: allocating row storage");
   }
   e = hipMalloc(&norms, (size_t)cap * sizeof(float));
@@ -139,13 +142,13 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   }
   // zero the whole tail (tile reads past ntotal must see zeros, never NaN garbage)
   const int64_t keep = idx->ntotal;
-  VS_HIP(hipMemsetAsync(codes + keep * idx->ld, 0, (size_t)(cap - keep) * idx->ld * sizeof(float),
+  VS_HIP(hipMemsetAsync(codes + keep * idx->rowbytes(), 0, (size_t)(cap - keep) * idx->rowbytes(),
                         st),
          "vs: zeroing storage");
   VS_HIP(hipMemsetAsync(norms + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
          "vs: zeroing norms");
   if (idx->codes && keep > 0) {
-    VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->ld * sizeof(float),
+    VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->rowbytes(),
                           hipMemcpyDeviceToDevice, st),
            "vs: copying storage");
     VS_HIP(hipMemcpyAsync(norms, idx->norms, (size_t)keep * sizeof(float),
@@ -164,9 +167,9 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
 
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
 // zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
-int run_topk(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq, int nq_pad,
-             int k, int64_t self0, float min_score, float* D, int64_t* I, hipStream_t st,
-             const float* xaux) {
+int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
+             int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
+             hipStream_t st, const float* xaux) {
   // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
   // lowest 2k-1 (key, label) entries of every partial list to be exact.
   const int KP = mode == MODE_IP ? kp_for(std::min(2 * k - 1, VS_MAX_K)) : kp_for(k);
@@ -177,6 +180,8 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const float* qaux, int 
 
   const bool gemv = (mode == MODE_IP || mode == MODE_L2) && self0 < 0 && nq <= kGemvMaxQ &&
                     (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
+  // bf16 indexes hand the GEMM a bf16 copy of the (already rounded) queries
+  const void* qmat = qb16 ? qb16 : (const void*)qbuf;
   if (gemv) {
     const int gmode = mode == MODE_L2 ? MODE_L2D : MODE_IP;
     int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
@@ -186,7 +191,8 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const float* qaux, int 
     VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
     KernelTimer tm(st);
-    VS_HIP(launch_gemv_topk(KP, gmode, nq, idx->codes, qbuf, idx->ld, ntotal, nblocks, part, st),
+    VS_HIP(launch_gemv_topk(KP, gmode, nq, idx->codes, idx->esize, qbuf, idx->ld, ntotal, nblocks,
+                            part, st),
            "vs: gemv_topk launch");
     tm.stop();
     VS_HIP(launch_merge_partials(gmode, part, nq, k, idx->id_base, min_score, D, I, k, st),
@@ -203,8 +209,8 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const float* qaux, int 
   VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
   KernelTimer tm(st);
-  VS_HIP(launch_gemm_topk(KP, mode, idx->codes, xaux, qbuf, qaux, idx->ld, ntotal, nq_pad, nsplit,
-                          self0, part, st),
+  VS_HIP(launch_gemm_topk(KP, mode, idx->codes, xaux, qmat, qaux, idx->ld, idx->esize, ntotal,
+                          nq_pad, nsplit, self0, part, st),
          "vs: gemm_topk launch");
   tm.stop();
   VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
@@ -238,8 +244,8 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
   if (d <= 0) return fail(VS_E_INVALID, "vs_create: d must be > 0");
   if (metric != VS_METRIC_L2 && metric != VS_METRIC_INNER_PRODUCT)
     return fail(VS_E_INVALID, "vs_create: metric must be METRIC_L2 or METRIC_INNER_PRODUCT");
-  if (dtype != VS_DTYPE_F32)
-    return fail(VS_E_UNSUPPORTED, "vs_create: only float32 storage is built in this version");
+  if (dtype != VS_DTYPE_F32 && dtype != VS_DTYPE_BF16)
+    return fail(VS_E_INVALID, "vs_create: dtype must be VS_DTYPE_F32 or VS_DTYPE_BF16");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return fail(VS_E_HIP, "vs_create: no HIP device available");
@@ -258,7 +264,8 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
   idx->metric = metric;
   idx->dtype = dtype;
   idx->device = device;
-  idx->ld = round_up(d, kBK);
+  idx->esize = dtype == VS_DTYPE_BF16 ? 2 : 4;
+  idx->ld = round_up(d, 128 / idx->esize);  // 128-B rows per GEMM stage
   *out = idx;
   return VS_OK;
 }
@@ -296,11 +303,30 @@ int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
   int rc = ensure_capacity(idx, idx->ntotal + n, st);
   if (rc) return rc;
   const hipMemcpyKind kind = (flags & VS_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-  VS_HIP(hipMemcpy2DAsync(idx->codes + idx->ntotal * idx->ld, idx->ld * sizeof(float), x,
-                          (size_t)idx->d * sizeof(float), (size_t)idx->d * sizeof(float), (size_t)n,
-                          kind, st),
-         "vs_add: copying rows");
-  VS_HIP(launch_row_norms(idx->codes, idx->ld, idx->ntotal, n, idx->norms, st), "vs_add: norms");
+  if (idx->esize == 4) {
+    VS_HIP(hipMemcpy2DAsync(idx->row(idx->ntotal), idx->rowbytes(), x,
+                            (size_t)idx->d * sizeof(float), (size_t)idx->d * sizeof(float),
+                            (size_t)n, kind, st),
+           "vs_add: copying rows");
+  } else {
+    // bf16 storage: stage fp32 rows on the device in bounded chunks, round into place
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)(64ull << 20) / (idx->d * 4));
+    Scratch scr(st);
+    float* tmp = nullptr;
+    VS_HIP(scr.alloc((void**)&tmp, (size_t)std::min(chunk, n) * idx->d * sizeof(float)),
+           "vs_add: scratch");
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+      const int64_t m = std::min(chunk, n - r0);
+      VS_HIP(hipMemcpyAsync(tmp, x + r0 * idx->d, (size_t)m * idx->d * sizeof(float), kind, st),
+             "vs_add: staging rows");
+      VS_HIP(launch_f32_to_bf16(tmp, idx->d, (uint16_t*)idx->row(idx->ntotal + r0), idx->ld, m,
+                                idx->d, st),
+             "vs_add: rounding to bf16");
+    }
+    VS_HIP(hipStreamSynchronize(st), "vs_add: synchronise");
+  }
+  VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
+         "vs_add: norms");
   // Source host buffers may be released by the caller as soon as we return.
   VS_HIP(hipStreamSynchronize(st), "vs_add: synchronise");
   idx->ntotal += n;
@@ -318,10 +344,10 @@ int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void
   DeviceGuard g(idx->device);
   int rc = ensure_capacity(idx, idx->ntotal + n, st);
   if (rc) return rc;
-  VS_HIP(launch_fill_synthetic(idx->codes + idx->ntotal * idx->ld, n, idx->d, idx->ld, seed, row0,
+  VS_HIP(launch_fill_synthetic(idx->row(idx->ntotal), idx->esize, n, idx->d, idx->ld, seed, row0,
                                st),
          "vs_add_synthetic: fill");
-  VS_HIP(launch_row_norms(idx->codes, idx->ld, idx->ntotal, n, idx->norms, st),
+  VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add_synthetic: norms");
   VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic: synchronise");
   idx->ntotal += n;
@@ -407,6 +433,10 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
     const int64_t qrows = round_up(std::max<int64_t>(cmax, kGemvMaxQ), kBQ);
     VS_HIP(scr.alloc((void**)&qbuf, (size_t)qrows * idx->ld * sizeof(float)), "vs_search: scratch");
     VS_HIP(scr.alloc((void**)&qaux, (size_t)qrows * sizeof(float)), "vs_search: scratch");
+    uint16_t* qb16 = nullptr;
+    if (idx->esize == 2)
+      VS_HIP(scr.alloc((void**)&qb16, (size_t)qrows * idx->ld * sizeof(uint16_t)),
+             "vs_search: scratch");
     const hipMemcpyKind kind =
         (flags & VS_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     for (int64_t c0 = 0; c0 < n; c0 += chunk) {
@@ -426,9 +456,16 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
                               (size_t)idx->d * sizeof(float), (size_t)idx->d * sizeof(float),
                               (size_t)nc, kind, st),
              "vs_search: staging queries");
+      if (idx->esize == 2) {
+        // bf16 index: queries are rounded to bf16 too, so every path (GEMV in fp32
+        // on the rounded values, GEMM on bf16 operands) scores the same numbers
+        VS_HIP(launch_round_bf16(qbuf, nq_pad * idx->ld, st), "vs_search: rounding queries");
+        VS_HIP(launch_f32_to_bf16(qbuf, idx->ld, qb16, idx->ld, nq_pad, idx->ld, st),
+               "vs_search: bf16 queries");
+      }
       if (mode == MODE_L2)
-        VS_HIP(launch_row_norms(qbuf, idx->ld, 0, nq_pad, qaux, st), "vs_search: query norms");
-      int rc = run_topk(idx, mode, qbuf, qaux, (int)nc, (int)nq_pad, (int)k, -1, 0.0f,
+        VS_HIP(launch_row_norms(qbuf, 4, idx->ld, 0, nq_pad, qaux, st), "vs_search: query norms");
+      int rc = run_topk(idx, mode, qbuf, qb16, qaux, (int)nc, (int)nq_pad, (int)k, -1, 0.0f,
                         Dd + c0 * k, Id + c0 * k, st, idx->norms);
       if (rc) return rc;
     }
@@ -456,10 +493,27 @@ int vs_reconstruct_n(vs_index* idx, int64_t i0, int64_t n, float* out, int flags
   DeviceGuard g(idx->device);
   const hipMemcpyKind kind =
       (flags & VS_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-  VS_HIP(hipMemcpy2DAsync(out, (size_t)idx->d * sizeof(float), idx->codes + i0 * idx->ld,
-                          idx->ld * sizeof(float), (size_t)idx->d * sizeof(float), (size_t)n, kind,
-                          st),
-         "vs_reconstruct_n: copy");
+  if (idx->esize == 4) {
+    VS_HIP(hipMemcpy2DAsync(out, (size_t)idx->d * sizeof(float), idx->row(i0), idx->rowbytes(),
+                            (size_t)idx->d * sizeof(float), (size_t)n, kind, st),
+           "vs_reconstruct_n: copy");
+  } else {
+    // widen bf16 rows in bounded chunks, then copy out
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)(64ull << 20) / (idx->d * 4));
+    Scratch scr(st);
+    float* tmp = nullptr;
+    VS_HIP(scr.alloc((void**)&tmp, (size_t)std::min(chunk, n) * idx->d * sizeof(float)),
+           "vs_reconstruct_n: scratch");
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+      const int64_t m = std::min(chunk, n - r0);
+      VS_HIP(launch_bf16_to_f32((const uint16_t*)idx->row(i0 + r0), idx->ld, tmp, idx->d, m,
+                                idx->d, st),
+             "vs_reconstruct_n: widen");
+      VS_HIP(hipMemcpyAsync(out + r0 * idx->d, tmp, (size_t)m * idx->d * sizeof(float), kind, st),
+             "vs_reconstruct_n: copy");
+    }
+    VS_HIP(hipStreamSynchronize(st), "vs_reconstruct_n: synchronise");
+  }
   if (!(flags & VS_OUT_DEVICE)) VS_HIP(hipStreamSynchronize(st), "vs_reconstruct_n: synchronise");
   return VS_OK;
 }
@@ -496,10 +550,10 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
   // rows are packed into scratch, then copied down to their final position.
   // Destinations never exceed the chunk's own source range, and earlier chunks
   // are already consumed, so the in-place move is safe with O(chunk) scratch.
-  const int64_t chunk = std::max<int64_t>(1024, (int64_t)(256ull << 20) / (idx->ld * 4));
-  float* tmp = nullptr;
+  const int64_t chunk = std::max<int64_t>(1024, (int64_t)(256ull << 20) / idx->rowbytes());
+  char* tmp = nullptr;
   float* tmpn = nullptr;
-  VS_HIP(scr.alloc((void**)&tmp, (size_t)chunk * idx->ld * sizeof(float)), "vs_remove_ids: scratch");
+  VS_HIP(scr.alloc((void**)&tmp, (size_t)chunk * idx->rowbytes()), "vs_remove_ids: scratch");
   VS_HIP(scr.alloc((void**)&tmpn, (size_t)chunk * sizeof(float)), "vs_remove_ids: scratch");
   const int64_t first = rm[0];
   for (int64_t s0 = first; s0 < idx->ntotal; s0 += chunk) {
@@ -508,10 +562,11 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
     const int64_t in_chunk = std::lower_bound(rm.begin(), rm.end(), s0 + cn) - rm.begin() - before;
     const int64_t kept = cn - in_chunk;
     const int64_t dst = s0 - before;
-    VS_HIP(launch_gather_kept(idx->codes, idx->norms, idx->ld, s0, cn, drm, nrem, tmp, tmpn, st),
+    VS_HIP(launch_gather_kept(idx->codes, idx->norms, idx->rowbytes(), s0, cn, drm, nrem, tmp, tmpn,
+                              st),
            "vs_remove_ids: gather");
     if (kept > 0) {
-      VS_HIP(hipMemcpyAsync(idx->codes + dst * idx->ld, tmp, (size_t)kept * idx->ld * sizeof(float),
+      VS_HIP(hipMemcpyAsync(idx->row(dst), tmp, (size_t)kept * idx->rowbytes(),
                             hipMemcpyDeviceToDevice, st),
              "vs_remove_ids: move rows");
       VS_HIP(hipMemcpyAsync(idx->norms + dst, tmpn, (size_t)kept * sizeof(float),
@@ -520,7 +575,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
     }
   }
   const int64_t nt = idx->ntotal - nrem;
-  VS_HIP(hipMemsetAsync(idx->codes + nt * idx->ld, 0, (size_t)nrem * idx->ld * sizeof(float), st),
+  VS_HIP(hipMemsetAsync(idx->row(nt), 0, (size_t)nrem * idx->rowbytes(), st),
          "vs_remove_ids: zero tail");
   VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),
          "vs_remove_ids: zero tail");
@@ -559,7 +614,9 @@ int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_se
     const int64_t nc = std::min(chunk, nq - c0);
     const int64_t nq_pad = round_up(nc, kBQ);
     const int64_t qrow = q0 + c0;
-    int rc = run_topk(idx, MODE_COS, idx->codes + qrow * idx->ld, rinv + qrow, (int)nc,
+    const bool b16 = idx->esize == 2;
+    int rc = run_topk(idx, MODE_COS, b16 ? nullptr : (const float*)idx->row(qrow),
+                      b16 ? (const void*)idx->row(qrow) : nullptr, rinv + qrow, (int)nc,
                       (int)nq_pad, (int)k, exclude_self ? qrow : -1, min_sim, Dd + c0 * k,
                       Id + c0 * k, st, rinv);
     if (rc) return rc;
@@ -594,7 +651,7 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
   if (rows < 0 || d <= 0 || row0 < 0) return fail(VS_E_INVALID, "vs_fill_synthetic: bad sizes");
   if (rows == 0) return VS_OK;
   if (!out) return fail(VS_E_INVALID, "vs_fill_synthetic: null output");
-  VS_HIP(launch_fill_synthetic(out, rows, d, d, seed, row0, (hipStream_t)stream),
+  VS_HIP(launch_fill_synthetic(out, 4, rows, d, d, seed, row0, (hipStream_t)stream),
          "vs_fill_synthetic: launch");
   return VS_OK;
 }

@@ -1,4 +1,5 @@
-// vs_gemm.hip — fused fp32 MFMA distance + top-k kernel (large query batches).
+// vs_gemm.hip — fused MFMA distance + top-k kernel (large query batches), for
+// fp32 rows (v_mfma_f32_32x32x2_f32) and bf16 rows (v_mfma_f32_32x32x16_bf16).
 // List semantics and key conventions: vs_device.h / vs_internal.h.
 #include "vs_device.h"
 
@@ -24,20 +25,25 @@ namespace vs {
 // distinct 16-B slots).  glds writes LDS lane-linearly, so the swizzle is applied
 // to the per-lane GLOBAL source address instead.
 //
-// Fragment k-order: for MFMA step t (0..3) lane half h supplies k = 4h + t of the
-// current 8-wide k chunk, on both operands, so each lane reads one 16-B chunk per
-// operand per 4 MFMAs.  The summation order differs from faiss's sgemm, which is
-// inside the documented fp32 tolerance.
+// Fragment k-order: every lane reads one 16-B chunk per operand per step (chunk
+// c = 2*step + h of the 128-B stage row).  fp32: the chunk holds 4 floats and
+// feeds 4 x32x32x2 MFMAs (instruction t uses k = 4h + t of the 8-wide step);
+// bf16: the chunk holds 8 bf16 = exactly the 32x32x16 operand of lane l
+// (k = 8h + j).  A and B use the same mapping, so the product is the plain dot
+// product; the summation order differs from faiss's sgemm, inside the
+// documented fp32 tolerance.  Each stage moves 128 B per row: 32 floats or 64 bf16.
 //
 // Workgroup -> (query tile, split) mapping is XCD-aware: consecutive logical ids
 // (which share a database split and differ in query tile) are packed onto one XCD
 // so the 4 MiB L2 there serves each database tile to all query tiles in flight.
-template <int KP, int MODE>
-__global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
-    const float* __restrict__ X, const float* __restrict__ xaux, const float* __restrict__ Q,
+template <int KP, int MODE, typename T>
+__global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
+    const T* __restrict__ X, const float* __restrict__ xaux, const T* __restrict__ Q,
     const float* __restrict__ qaux, int64_t ld, int nstage, int ntotal, int ntiles, int nsplit,
     int nqt, int64_t self0, float* __restrict__ pkey, int* __restrict__ pid) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * kBN * kBK];  // [buf][X|Q][128][32]
+  static_assert(sizeof(T) == 4 || sizeof(T) == 2, "fp32 or bf16 rows");
+  // [buf][X|Q][128 rows][128 B]; viewed as floats (32 per row) for addressing.
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * kBN * kBK];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -68,14 +74,14 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
   int li[KP];
   list_init<KP, int>(lk, li);
 
-  const float* Qblk = Q + (int64_t)qt * kBQ * ld;
+  const T* Qblk = Q + (int64_t)qt * kBQ * ld;
   // glds geometry: a wave instruction moves 8 rows x 128 B; wave w stages row
   // groups g = 4w..4w+3 of both operands.  The per-lane source offset is 32-bit
   // on a wave-uniform base (saddr form); the swizzle (row >> 1) & 7 depends on
   // the group only through g & 1, so two lane offsets cover all four groups.
   const int srow = lane >> 3;
   const int sphys = lane & 7;
-  const uint32_t ldb = (uint32_t)ld * 4u;  // row stride in bytes
+  const uint32_t ldb = (uint32_t)ld * (uint32_t)sizeof(T);  // row stride in bytes
   uint32_t soff[2];
 #pragma unroll
   for (int par = 0; par < 2; ++par) {
@@ -98,8 +104,8 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
     auto stage = [&](int buf, int kb) {
       float* dX = smem + buf * (2 * kBN * kBK);
       float* dQ = dX + kBN * kBK;
-      const char* xs = Xblk + kb * 4;
-      const char* qs = (const char*)Qblk + kb * 4;
+      const char* xs = Xblk + kb;
+      const char* qs = (const char*)Qblk + kb;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int g = w * 4 + i;
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
     __syncthreads();
 
     for (int st = 0; st < nstage; ++st) {
-      if (st + 1 < nstage) stage((st + 1) & 1, (st + 1) * kBK);
+      if (st + 1 < nstage) stage((st + 1) & 1, (st + 1) * 128);
       const float* cX = smem + (st & 1) * (2 * kBN * kBK);
       const float* cQ = cX + kBN * kBK;
 #pragma unroll
@@ -124,11 +130,19 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
         f32x4 ax[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) ax[s] = *(const f32x4*)(cX + (32 * s + c32) * kBK + coff);
+        if constexpr (sizeof(T) == 4) {
 #pragma unroll
-        for (int tt = 0; tt < 4; ++tt) {
+          for (int tt = 0; tt < 4; ++tt) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+              acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(ax[s][tt], bq[tt], acc[s], 0, 0, 0);
+          }
+        } else {
 #pragma unroll
           for (int s = 0; s < 4; ++s)
-            acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(ax[s][tt], bq[tt], acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ax[s]),
+                                                            __builtin_bit_cast(bf16x8, bq),
+                                                            acc[s], 0, 0, 0);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -196,50 +210,59 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk_f32(
 }
 
 template <int KP, int MODE>
-static hipError_t gemm_dispatch_mode(const float* X, const float* xaux, const float* Q,
-                                     const float* qaux, int64_t ld, int ntotal, int nq_pad,
-                                     int nsplit, int64_t self0, Partials part, hipStream_t st) {
+static hipError_t gemm_dispatch_mode(const void* X, const float* xaux, const void* Q,
+                                     const float* qaux, int64_t ld, int esize, int ntotal,
+                                     int nq_pad, int nsplit, int64_t self0, Partials part,
+                                     hipStream_t st) {
   const int ntiles = (ntotal + kBN - 1) / kBN;
   const int nqt = nq_pad / kBQ;
   const int nblk = nqt * nsplit;
-  hipLaunchKernelGGL((gemm_topk_f32<KP, MODE>), dim3(nblk), dim3(256), 0, st, X, xaux, Q, qaux,
-                     ld, (int)(ld / kBK), ntotal, ntiles, nsplit, nqt, self0, part.key, part.id);
+  const int nstage = (int)(ld * esize / 128);
+  if (esize == 4)
+    hipLaunchKernelGGL((gemm_topk<KP, MODE, float>), dim3(nblk), dim3(256), 0, st,
+                       (const float*)X, xaux, (const float*)Q, qaux, ld, nstage, ntotal, ntiles,
+                       nsplit, nqt, self0, part.key, part.id);
+  else
+    hipLaunchKernelGGL((gemm_topk<KP, MODE, uint16_t>), dim3(nblk), dim3(256), 0, st,
+                       (const uint16_t*)X, xaux, (const uint16_t*)Q, qaux, ld, nstage, ntotal,
+                       ntiles, nsplit, nqt, self0, part.key, part.id);
   return hipGetLastError();
 }
 
 template <int KP>
-static hipError_t gemm_dispatch(int mode, const float* X, const float* xaux, const float* Q,
-                                const float* qaux, int64_t ld, int ntotal, int nq_pad,
+static hipError_t gemm_dispatch(int mode, const void* X, const float* xaux, const void* Q,
+                                const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
                                 int nsplit, int64_t self0, Partials part, hipStream_t st) {
   switch (mode) {
     case MODE_IP:
-      return gemm_dispatch_mode<KP, MODE_IP>(X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0,
+      return gemm_dispatch_mode<KP, MODE_IP>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0,
                                              part, st);
     case MODE_L2:
-      return gemm_dispatch_mode<KP, MODE_L2>(X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0,
+      return gemm_dispatch_mode<KP, MODE_L2>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0,
                                              part, st);
     case MODE_COS:
-      return gemm_dispatch_mode<KP, MODE_COS>(X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit,
-                                              self0, part, st);
+      return gemm_dispatch_mode<KP, MODE_COS>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
+                                              nsplit, self0, part, st);
     default:
       return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_gemm_topk(int KP, int mode, const float* X, const float* xaux, const float* Q,
-                            const float* qaux, int64_t ld, int ntotal, int nq_pad, int nsplit,
-                            int64_t self0, Partials part, hipStream_t st) {
-  if (nq_pad % kBQ != 0 || ld % kBK != 0 || part.KP != KP || part.P != 2 * nsplit)
+hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, const void* Q,
+                            const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
+                            int nsplit, int64_t self0, Partials part, hipStream_t st) {
+  if (nq_pad % kBQ != 0 || (ld * esize) % 128 != 0 || part.KP != KP || part.P != 2 * nsplit ||
+      (esize != 4 && esize != 2))
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:
-      return gemm_dispatch<8>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<8>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
     case 16:
-      return gemm_dispatch<16>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<16>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
     case 32:
-      return gemm_dispatch<32>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<32>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
     case 64:
-      return gemm_dispatch<64>(mode, X, xaux, Q, qaux, ld, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<64>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
     default:
       return hipErrorInvalidValue;
   }

@@ -8,13 +8,32 @@ namespace vs {
 // chunks l, l+64, ... of every row (1 KiB per wave instruction, fully
 // coalesced), the queries sit in LDS, partial sums are reduced across the wave,
 // and lane q keeps query q's list.  MODE_L2D computes sum (x-q)^2 directly, as
-// faiss does for nq < 20 (fvec_L2sqr); MODE_IP the plain dot product.
-template <int NQ, int KP, int MODE>
-__global__ __launch_bounds__(256) void gemv_topk_f32(const float* __restrict__ X,
-                                                      const float* __restrict__ Q, int64_t ld,
-                                                      int ntotal, int rows_per_block,
-                                                      float* __restrict__ pkey,
-                                                      int* __restrict__ pid) {
+// faiss does for nq < 20 (fvec_L2sqr); MODE_IP the plain dot product.  Rows are
+// fp32 or bf16 (widened in registers); a 16-B chunk is 4 or 8 elements.
+template <typename T>
+__device__ __forceinline__ void widen_chunk(const uint4 v, float (&f)[16 / sizeof(T)]) {
+  if constexpr (sizeof(T) == 4) {
+    f[0] = __uint_as_float(v.x);
+    f[1] = __uint_as_float(v.y);
+    f[2] = __uint_as_float(v.z);
+    f[3] = __uint_as_float(v.w);
+  } else {
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(u[i] << 16);
+      f[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  }
+}
+
+template <int NQ, int KP, int MODE, typename T>
+__global__ __launch_bounds__(256) void gemv_topk(const T* __restrict__ X,
+                                                 const float* __restrict__ Q, int64_t ld,
+                                                 int ntotal, int rows_per_block,
+                                                 float* __restrict__ pkey,
+                                                 int* __restrict__ pid) {
+  constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   extern __shared__ __attribute__((aligned(16))) float sq[];  // [NQ][ld]
   const int tid = threadIdx.x;
   for (int64_t i = (int64_t)tid * 4; i < (int64_t)NQ * ld; i += 1024)
@@ -23,7 +42,7 @@ __global__ __launch_bounds__(256) void gemv_topk_f32(const float* __restrict__ X
 
   const int lane = tid & 63;
   const int w = tid >> 6;
-  const int ld4 = (int)(ld >> 2);
+  const int cpr = (int)(ld / EPC);  // chunks per row
   const int rb0 = blockIdx.x * rows_per_block;
   const int ntot16 = (ntotal + 15) & ~15;
   const int rb1 = min(rb0 + rows_per_block, ntot16);
@@ -39,22 +58,42 @@ __global__ __launch_bounds__(256) void gemv_topk_f32(const float* __restrict__ X
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[a][q] = 0.0f;
 
-    const float* xr = X + (int64_t)r * ld;
-    for (int c = lane; c < ld4; c += 64) {
-      f32x4 xv[4];
+    const T* xr = X + (int64_t)r * ld;
+    for (int c = lane; c < cpr; c += 64) {
+      uint4 xv[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) xv[a] = __builtin_nontemporal_load((const f32x4*)(xr + a * ld) + c);
+      for (int a = 0; a < 4; ++a) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(xr + a * ld) + c);
+        xv[a] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      float xf[4][EPC];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) widen_chunk<T>(xv[a], xf[a]);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        const f32x4 qv = *(const f32x4*)(sq + q * ld + c * 4);
+        float qf[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; e += 4) {
+          const f32x4 qv = *(const f32x4*)(sq + q * ld + c * EPC + e);
+          qf[e] = qv.x;
+          qf[e + 1] = qv.y;
+          qf[e + 2] = qv.z;
+          qf[e + 3] = qv.w;
+        }
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          if constexpr (MODE == MODE_L2D) {
-            const f32x4 dv = xv[a] - qv;
-            acc[a][q] += dv.x * dv.x + dv.y * dv.y + dv.z * dv.z + dv.w * dv.w;
-          } else {
-            acc[a][q] += xv[a].x * qv.x + xv[a].y * qv.y + xv[a].z * qv.z + xv[a].w * qv.w;
+          float sacc = 0.0f;
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            if constexpr (MODE == MODE_L2D) {
+              const float dv = xf[a][e] - qf[e];
+              sacc += dv * dv;
+            } else {
+              sacc += xf[a][e] * qf[e];
+            }
           }
+          acc[a][q] += sacc;
         }
       }
     }
@@ -109,53 +148,64 @@ __global__ __launch_bounds__(256) void gemv_topk_f32(const float* __restrict__ X
   }
 }
 
-template <int NQ, int KP>
-static hipError_t gemv_dispatch_q(int mode, const float* X, const float* Q, int64_t ld,
+template <int NQ, int KP, typename T>
+static hipError_t gemv_dispatch_t(int mode, const T* X, const float* Q, int64_t ld,
                                   int ntotal, int nblocks, Partials part, hipStream_t st) {
   const int ntot16 = (ntotal + 15) & ~15;
   int rpb = (ntot16 + nblocks - 1) / nblocks;
   rpb = (rpb + 15) & ~15;
   const size_t lds = (size_t)NQ * ld * sizeof(float) + (size_t)4 * NQ * KP * 8;
   if (mode == MODE_L2D)
-    hipLaunchKernelGGL((gemv_topk_f32<NQ, KP, MODE_L2D>), dim3(nblocks), dim3(256), lds, st, X, Q,
+    hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_L2D, T>), dim3(nblocks), dim3(256), lds, st, X, Q,
                        ld, ntotal, rpb, part.key, part.id);
   else if (mode == MODE_IP)
-    hipLaunchKernelGGL((gemv_topk_f32<NQ, KP, MODE_IP>), dim3(nblocks), dim3(256), lds, st, X, Q,
+    hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_IP, T>), dim3(nblocks), dim3(256), lds, st, X, Q,
                        ld, ntotal, rpb, part.key, part.id);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
+template <int NQ, int KP>
+static hipError_t gemv_dispatch_q(int mode, const void* X, int esize, const float* Q, int64_t ld,
+                                  int ntotal, int nblocks, Partials part, hipStream_t st) {
+  if (esize == 4)
+    return gemv_dispatch_t<NQ, KP, float>(mode, (const float*)X, Q, ld, ntotal, nblocks, part, st);
+  return gemv_dispatch_t<NQ, KP, uint16_t>(mode, (const uint16_t*)X, Q, ld, ntotal, nblocks, part,
+                                           st);
+}
+
 template <int KP>
-static hipError_t gemv_dispatch(int mode, int nq, const float* X, const float* Q, int64_t ld,
-                                int ntotal, int nblocks, Partials part, hipStream_t st) {
+static hipError_t gemv_dispatch(int mode, int nq, const void* X, int esize, const float* Q,
+                                int64_t ld, int ntotal, int nblocks, Partials part,
+                                hipStream_t st) {
   switch (nq) {
     case 1:
-      return gemv_dispatch_q<1, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<1, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
     case 2:
-      return gemv_dispatch_q<2, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<2, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
     case 3:
     case 4:
-      return gemv_dispatch_q<4, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<4, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
     default:
-      return gemv_dispatch_q<8, KP>(mode, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<8, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
   }
 }
 
-hipError_t launch_gemv_topk(int KP, int mode, int nq, const float* X, const float* Q, int64_t ld,
-                            int ntotal, int nblocks, Partials part, hipStream_t st) {
-  if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks || ld % 4 != 0)
+hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, const float* Q,
+                            int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st) {
+  if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks || (ld * esize) % 16 != 0 ||
+      (esize != 4 && esize != 2))
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:
-      return gemv_dispatch<8>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<8>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
     case 16:
-      return gemv_dispatch<16>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<16>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
     case 32:
-      return gemv_dispatch<32>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<32>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
     case 64:
-      return gemv_dispatch<64>(mode, nq, X, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<64>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
     default:
       return hipErrorInvalidValue;
   }

@@ -29,6 +29,15 @@ constexpr int kRowPad = 256;
 // The GEMV (small batch) path handles up to this many queries per launch.
 constexpr int kGemvMaxQ = 8;
 
+__host__ __device__ inline uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu))  // NaN stays a (quiet) NaN
+    return (uint16_t)((u >> 16) | 0x0040u);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
 // Merge-buffer record: key + local row id (int32; a shard never holds 2^31 rows).
 struct Partials {
   float* key = nullptr;
@@ -39,14 +48,14 @@ struct Partials {
 
 // ---- launchers (return the launch status; all asynchronous on `st`) -------
 // Fused MFMA distance + top-k over database tiles, writing 2*nsplit lists/query.
-hipError_t launch_gemm_topk(int KP, int mode, const float* X, const float* xaux,
-                            const float* Q, const float* qaux, int64_t ld, int ntotal,
-                            int nq_pad, int nsplit, int64_t self0, Partials part,
-                            hipStream_t st);
+// X / Q are fp32 (esize 4) or bf16 (esize 2) rows of stride ld elements.
+hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, const void* Q,
+                            const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
+                            int nsplit, int64_t self0, Partials part, hipStream_t st);
 // Streaming (HBM-bound) distance + top-k for nq <= kGemvMaxQ.
-hipError_t launch_gemv_topk(int KP, int mode, int nq, const float* X, const float* Q,
-                            int64_t ld, int ntotal, int nblocks, Partials part,
-                            hipStream_t st);
+// X fp32 or bf16 rows; Q always fp32 (values already rounded for bf16 indexes).
+hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, const float* Q,
+                            int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
@@ -54,20 +63,29 @@ hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t
 // Shard lists [nparts][nq][k_in] (scores, int64 labels) -> [nq][k].
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts,
                               int nq, int k_in, int k, float* D, int64_t* I, hipStream_t st);
-// out[r] = sum_j X[r][j]^2 for rows [r0, r0+n).
-hipError_t launch_row_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
-                            hipStream_t st);
+// out[r] = sum_j X[r][j]^2 for rows [r0, r0+n) (fp32 or bf16 rows).
+hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, int64_t n,
+                            float* out, hipStream_t st);
+// Pitched conversions: fp32 -> bf16 (round to nearest even, NaN kept) with zero
+// padding of columns [cols, ldo); bf16 -> fp32 (exact widening); fp32 -> fp32
+// rounded through bf16 (the value a bf16 index stores).
+hipError_t launch_f32_to_bf16(const float* in, int64_t ldi, uint16_t* out, int64_t ldo,
+                              int64_t rows, int64_t cols, hipStream_t st);
+hipError_t launch_bf16_to_f32(const uint16_t* in, int64_t ldi, float* out, int64_t ldo,
+                              int64_t rows, int64_t cols, hipStream_t st);
+hipError_t launch_round_bf16(float* x, int64_t n, hipStream_t st);
 // out[r] = 1/sqrt(norm[r]) (double-precision rsqrt rounded to float).
 hipError_t launch_rsqrt(const float* norm, int64_t n, float* out, hipStream_t st);
-// Counter-based synthetic rows into a pitched buffer (zero padding d..ldo).
-hipError_t launch_fill_synthetic(float* out, int64_t rows, int64_t d, int64_t ldo,
+// Counter-based synthetic rows into a pitched fp32 or bf16 buffer (zero padding d..ldo).
+hipError_t launch_fill_synthetic(void* out, int esize, int64_t rows, int64_t d, int64_t ldo,
                                  uint64_t seed, int64_t row0, hipStream_t st);
 // Fill n (D, I) pairs with the empty-result sentinel of `mode`.
 hipError_t launch_fill_empty(int mode, float* D, int64_t* I, int64_t n, hipStream_t st);
 // Stable compaction helper: copy the kept rows of [src0, src0+n) into tmp,
 // given the sorted removed-row list (device).  Also moves the norms.
-hipError_t launch_gather_kept(const float* X, const float* norms, int64_t ld, int64_t src0,
-                              int64_t n, const int64_t* removed, int64_t nrem, float* tmp,
+// Rows are `rowbytes` long (multiple of 16).
+hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbytes, int64_t src0,
+                              int64_t n, const int64_t* removed, int64_t nrem, void* tmp,
                               float* tmp_norms, hipStream_t st);
 
 }  // namespace vs

@@ -284,27 +284,96 @@ hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int 
 
 // ---------------------------------------------------------------------------
 // Support kernels.
-__global__ __launch_bounds__(256) void row_norms_kernel(const float* __restrict__ X, int64_t ld,
+template <typename T>
+__global__ __launch_bounds__(256) void row_norms_kernel(const T* __restrict__ X, int64_t ld,
                                                         int64_t r0, int64_t n,
                                                         float* __restrict__ out) {
+  constexpr int EPC = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
-  const float* xr = X + (r0 + row) * ld;
+  const uint4* xr = (const uint4*)(X + (r0 + row) * ld);
   float s = 0.0f;
-  for (int64_t c = lane; c < (ld >> 2); c += 64) {
-    const f32x4 v = *(const f32x4*)(xr + c * 4);
-    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  for (int64_t c = lane; c < ld / EPC; c += 64) {
+    const uint4 v = xr[c];
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (sizeof(T) == 4) {
+        const float f = __uint_as_float(u[i]);
+        s += f * f;
+      } else {
+        const float a = __uint_as_float(u[i] << 16), b = __uint_as_float(u[i] & 0xFFFF0000u);
+        s += a * a + b * b;
+      }
+    }
   }
   s = wave_sum(s);
   if (lane == 0) out[r0 + row] = s;
 }
 
-hipError_t launch_row_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
-                            hipStream_t st) {
+hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, int64_t n,
+                            float* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = (n + 3) / 4;
-  hipLaunchKernelGGL(row_norms_kernel, dim3((unsigned)nb), dim3(256), 0, st, X, ld, r0, n, out);
+  if (esize == 4)
+    hipLaunchKernelGGL(row_norms_kernel<float>, dim3((unsigned)nb), dim3(256), 0, st,
+                       (const float*)X, ld, r0, n, out);
+  else
+    hipLaunchKernelGGL(row_norms_kernel<uint16_t>, dim3((unsigned)nb), dim3(256), 0, st,
+                       (const uint16_t*)X, ld, r0, n, out);
+  return hipGetLastError();
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ in, int64_t ldi,
+                                   uint16_t* __restrict__ out, int64_t ldo, int64_t rows,
+                                   int64_t cols) {
+  const int64_t row = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (row >= rows) return;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < ldo; j += (int64_t)gridDim.x * 256)
+    out[row * ldo + j] = j < cols ? f32_to_bf16_rne(in[row * ldi + j]) : (uint16_t)0;
+}
+
+__global__ void bf16_to_f32_kernel(const uint16_t* __restrict__ in, int64_t ldi,
+                                   float* __restrict__ out, int64_t ldo, int64_t rows,
+                                   int64_t cols) {
+  const int64_t row = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (row >= rows) return;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < ldo; j += (int64_t)gridDim.x * 256)
+    out[row * ldo + j] = j < cols ? __uint_as_float((uint32_t)in[row * ldi + j] << 16) : 0.0f;
+}
+
+static dim3 pitched_grid(int64_t rows, int64_t ldo) {
+  const int64_t gy = rows < 65535 ? rows : 65535;
+  const int64_t gz = (rows + 65534) / 65535;
+  const int64_t gx = (ldo + 255) / 256 < 8 ? (ldo + 255) / 256 : 8;
+  return dim3((unsigned)gx, (unsigned)gy, (unsigned)gz);
+}
+
+hipError_t launch_f32_to_bf16(const float* in, int64_t ldi, uint16_t* out, int64_t ldo,
+                              int64_t rows, int64_t cols, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, pitched_grid(rows, ldo), dim3(256), 0, st, in, ldi, out,
+                     ldo, rows, cols);
+  return hipGetLastError();
+}
+
+hipError_t launch_bf16_to_f32(const uint16_t* in, int64_t ldi, float* out, int64_t ldo,
+                              int64_t rows, int64_t cols, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bf16_to_f32_kernel, pitched_grid(rows, ldo), dim3(256), 0, st, in, ldi, out,
+                     ldo, rows, cols);
+  return hipGetLastError();
+}
+
+__global__ void round_bf16_kernel(float* __restrict__ x, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = __uint_as_float((uint32_t)f32_to_bf16_rne(x[i]) << 16);
+}
+
+hipError_t launch_round_bf16(float* x, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(round_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n);
   return hipGetLastError();
 }
 
@@ -327,7 +396,8 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ __launch_bounds__(256) void fill_synthetic_kernel(float* __restrict__ out, int64_t rows,
+template <typename T>
+__global__ __launch_bounds__(256) void fill_synthetic_kernel(T* __restrict__ out, int64_t rows,
                                                              int64_t d, int64_t ldo, uint64_t seed,
                                                              int64_t row0) {
   const int64_t row = blockIdx.y + (int64_t)blockIdx.z * 65535;
@@ -339,18 +409,20 @@ __global__ __launch_bounds__(256) void fill_synthetic_kernel(float* __restrict__
       const uint64_t z = splitmix64(seed ^ (base + (uint64_t)j));
       v = (float)(z >> 40) * (1.0f / 8388608.0f) - 1.0f;
     }
-    out[row * ldo + j] = v;
+    if constexpr (sizeof(T) == 4) out[row * ldo + j] = v;
+    else out[row * ldo + j] = f32_to_bf16_rne(v);
   }
 }
 
-hipError_t launch_fill_synthetic(float* out, int64_t rows, int64_t d, int64_t ldo, uint64_t seed,
-                                 int64_t row0, hipStream_t st) {
+hipError_t launch_fill_synthetic(void* out, int esize, int64_t rows, int64_t d, int64_t ldo,
+                                 uint64_t seed, int64_t row0, hipStream_t st) {
   if (rows <= 0) return hipSuccess;
-  const int64_t gy = rows < 65535 ? rows : 65535;
-  const int64_t gz = (rows + 65534) / 65535;
-  const int gx = (int)((ldo + 255) / 256 < 8 ? (ldo + 255) / 256 : 8);
-  hipLaunchKernelGGL(fill_synthetic_kernel, dim3(gx, (unsigned)gy, (unsigned)gz), dim3(256), 0, st,
-                     out, rows, d, ldo, seed, row0);
+  if (esize == 4)
+    hipLaunchKernelGGL(fill_synthetic_kernel<float>, pitched_grid(rows, ldo), dim3(256), 0, st,
+                       (float*)out, rows, d, ldo, seed, row0);
+  else
+    hipLaunchKernelGGL(fill_synthetic_kernel<uint16_t>, pitched_grid(rows, ldo), dim3(256), 0,
+                       st, (uint16_t*)out, rows, d, ldo, seed, row0);
   return hipGetLastError();
 }
 
@@ -382,11 +454,12 @@ __device__ __forceinline__ int64_t count_less(const int64_t* a, int64_t n, int64
 
 // One wave per source row: kept rows of [src0, src0+n) are packed, in order,
 // into tmp (and their norms into tmp_norms).
-__global__ __launch_bounds__(256) void gather_kept_kernel(const float* __restrict__ X,
+__global__ __launch_bounds__(256) void gather_kept_kernel(const char* __restrict__ X,
                                                           const float* __restrict__ norms,
-                                                          int64_t ld, int64_t src0, int64_t n,
+                                                          int64_t rowbytes, int64_t src0,
+                                                          int64_t n,
                                                           const int64_t* __restrict__ removed,
-                                                          int64_t nrem, float* __restrict__ tmp,
+                                                          int64_t nrem, char* __restrict__ tmp,
                                                           float* __restrict__ tmp_norms) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -396,18 +469,19 @@ __global__ __launch_bounds__(256) void gather_kept_kernel(const float* __restric
   if (before_row < nrem && removed[before_row] == row) return;  // removed
   const int64_t before_src0 = count_less(removed, nrem, src0);
   const int64_t dst = i - (before_row - before_src0);
-  const f32x4* s = (const f32x4*)(X + row * ld);
-  f32x4* dd = (f32x4*)(tmp + dst * ld);
-  for (int64_t c = lane; c < (ld >> 2); c += 64) dd[c] = s[c];
+  const uint4* s = (const uint4*)(X + row * rowbytes);
+  uint4* dd = (uint4*)(tmp + dst * rowbytes);
+  for (int64_t c = lane; c < (rowbytes >> 4); c += 64) dd[c] = s[c];
   if (lane == 0) tmp_norms[dst] = norms[row];
 }
 
-hipError_t launch_gather_kept(const float* X, const float* norms, int64_t ld, int64_t src0,
-                              int64_t n, const int64_t* removed, int64_t nrem, float* tmp,
+hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbytes, int64_t src0,
+                              int64_t n, const int64_t* removed, int64_t nrem, void* tmp,
                               float* tmp_norms, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X,
-                     norms, ld, src0, n, removed, nrem, tmp, tmp_norms);
+  hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st,
+                     (const char*)X, norms, rowbytes, src0, n, removed, nrem, (char*)tmp,
+                     tmp_norms);
   return hipGetLastError();
 }
 

@@ -84,8 +84,11 @@ class Index:
 class IndexFlat(Index):
     """Exact flat index (faiss::IndexFlat) on one GPU.
 
-    ``dtype="bf16"`` requests bf16 row storage (approximate; reported with
-    recall@k) — not available in this build yet.
+    ``dtype="bf16"`` stores rows as bf16 (round to nearest even) — half the HBM
+    of fp32, for corpora that do not fit otherwise (BASELINE config 5).  Queries
+    are rounded to bf16 as well and products accumulate in fp32, so the search is
+    exact over the rounded vectors; against fp32 vectors it is reported as
+    recall@k.  ``reconstruct`` returns the stored (rounded) values.
     """
 
     def __init__(self, d: int, metric: int = METRIC_L2, *, device: int | None = None,
@@ -100,6 +103,7 @@ class IndexFlat(Index):
                    "vs_create")
         self._d = d
         self._metric = int(metric)
+        self._dtype = "bf16" if code == _lib.DTYPE_BF16 else "f32"
 
     # -- attributes faiss exposes -------------------------------------------------
     @property
@@ -113,6 +117,10 @@ class IndexFlat(Index):
     @property
     def device(self) -> int:
         return self._device
+
+    @property
+    def dtype(self) -> str:
+        return self._dtype
 
     @property
     def ntotal(self) -> int:

@@ -41,6 +41,16 @@ METRIC_L2 = 1
 FLT_MAX = np.float32(np.finfo(np.float32).max)
 
 
+def round_bf16(x) -> np.ndarray:
+    """float32 -> nearest-even bf16 -> float32 (what a bf16 index stores)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    nan = np.isnan(np.asarray(x, dtype=np.float32))
+    out = r.astype(np.uint32).view(np.float32)
+    out = np.where(nan, np.float32(np.nan), out)
+    return out.astype(np.float32)
+
+
 def neutral(metric: int) -> np.float32:
     """faiss heap neutral value: CMax -> FLT_MAX (L2), CMin -> lowest (IP)."""
     return FLT_MAX if metric == METRIC_L2 else -FLT_MAX

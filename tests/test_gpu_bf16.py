@@ -1,0 +1,112 @@
+"""GPU: bf16 row storage (BASELINE config 5).
+
+A bf16 index rounds rows and queries to bf16 (nearest even) and accumulates
+products in fp32, so it is EXACT with respect to the rounded vectors (checked
+against the fp64 oracle on round_bf16 inputs, same tolerance as fp32) and
+APPROXIMATE with respect to the original fp32 vectors (reported as recall@k)."""
+
+import numpy as np
+import pytest
+
+from oracle import flat
+
+pytestmark = pytest.mark.gpu
+
+L2, IP = flat.METRIC_L2, flat.METRIC_INNER_PRODUCT
+
+
+@pytest.fixture(scope="module")
+def vf():
+    from vsearch import _lib
+    from vsearch import faiss as vfaiss
+
+    assert _lib.device_count() >= 1
+    return vfaiss
+
+
+def _rand(n, d, seed):
+    return np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("nq", [1, 3, 8, 9, 40, 130])
+@pytest.mark.parametrize("k", [1, 5, 10, 32])
+def test_bf16_exact_on_rounded_vectors(vf, metric, nq, k):
+    xb = _rand(2500, 200, 1)
+    xq = _rand(nq, 200, 2)
+    index = vf.IndexFlat(200, metric, dtype="bf16")
+    index.add(xb)
+    D, I = index.search(xq, k)
+    rb, rq = flat.round_bf16(xb), flat.round_bf16(xq)
+    Dr, Ir = flat.knn_exact(rb, rq, k, metric)
+    bad = flat.mismatches(D, I, Dr, Ir, metric, rb, rq)
+    assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("d", [3, 64, 100, 1536])
+def test_bf16_dims_and_reconstruct(vf, d):
+    xb = _rand(300, d, 3)
+    index = vf.IndexFlatL2(d, dtype="bf16")
+    assert index.dtype == "bf16"
+    index.add(xb)
+    np.testing.assert_array_equal(index.reconstruct_n(0, 300), flat.round_bf16(xb))
+    np.testing.assert_array_equal(index.reconstruct(299), flat.round_bf16(xb[299:]).ravel())
+    xq = _rand(5, d, 4)
+    D, I = index.search(xq, 7)
+    rb, rq = flat.round_bf16(xb), flat.round_bf16(xq)
+    Dr, Ir = flat.knn_exact(rb, rq, 7, L2)
+    assert not flat.mismatches(D, I, Dr, Ir, L2, rb, rq)
+
+
+def test_bf16_remove_and_add(vf):
+    xb = _rand(5000, 64, 5)
+    index = vf.IndexFlatIP(64, dtype="bf16")
+    index.add(xb)
+    rm = np.arange(0, 5000, 7, dtype=np.int64)
+    assert index.remove_ids(rm) == rm.size
+    xr, _ = flat.remove_ids(flat.round_bf16(xb), rm)
+    np.testing.assert_array_equal(index.reconstruct_n(0, index.ntotal), xr)
+    index.add(xb[:100])
+    xr = np.concatenate([xr, flat.round_bf16(xb[:100])])
+    xq = _rand(20, 64, 6)
+    D, I = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xr, flat.round_bf16(xq), 10, IP)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xr, flat.round_bf16(xq))
+
+
+def test_bf16_synthetic_matches_rounded_generator(vf):
+    from vsearch.synth import synthetic_rows
+
+    index = vf.IndexFlatIP(1536, dtype="bf16")
+    index.add_synthetic(257, seed=1234, row0=123)
+    np.testing.assert_array_equal(index.reconstruct_n(0, 257),
+                                  flat.round_bf16(synthetic_rows(123, 257, 1536, 1234)))
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_bf16_recall_vs_fp32(vf, metric):
+    """recall@10 of the bf16 index against fp32 exact search (C5's reported metric)."""
+    rng = np.random.default_rng(7)
+    cent = rng.standard_normal((64, 256)).astype(np.float32)
+    xb = (cent[rng.integers(0, 64, 20000)] + 0.5 * rng.standard_normal((20000, 256))).astype(np.float32)
+    xb /= np.linalg.norm(xb, axis=1, keepdims=True)
+    xq = (cent[rng.integers(0, 64, 200)] + 0.5 * rng.standard_normal((200, 256))).astype(np.float32)
+    xq /= np.linalg.norm(xq, axis=1, keepdims=True)
+    index = vf.IndexFlat(256, metric, dtype="bf16")
+    index.add(xb)
+    _, I = index.search(xq, 10)
+    _, Ir = flat.knn_exact(xb, xq, 10, metric)
+    recall = np.mean([len(set(I[q]) & set(Ir[q])) / 10 for q in range(200)])
+    assert recall >= 0.9, recall
+
+
+def test_bf16_selfjoin(vf):
+    x = _rand(700, 48, 8)
+    index = vf.IndexFlatIP(48, dtype="bf16")
+    index.add(x)
+    S, I = index.selfjoin(15)
+    Sr, Ir = flat.pgvector_cosine_topk(flat.round_bf16(x), 15)
+    diff = I != Ir
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
+    np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
