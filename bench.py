@@ -1,29 +1,39 @@
 """Headline benchmark: exact top-10 queries/sec over 10M x 1536 fp32 (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--ntotal 10000000]
-                    [--batch 4096] [--k 10] [--metric ip|l2] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+                    [--ntotal N] [--batch B] [--k K] [--metric ip|l2] [--no-cpu-baseline]
 
-One step = one exact search of a batch of B synthetic queries over the whole
-corpus (BASELINE config 3, batch-4096 throughput).  The corpus is row-sharded
-over the N ranks (one process per GPU, launched by torch.distributed.run);
-every rank searches its shard with the fused MFMA distance+top-k kernel and the
-per-shard lists are merged after an RCCL all-gather.  Corpus and queries are
-generated on the device (counter-based generator; no dataset exists offline)
-and are resident in HBM before the timed region.
+Workloads (BASELINE.json configs; the default is the one the metric is quoted on):
+  c3  10M x 1536 fp32, batch 4096, top-10 IP.  One step = one exact search of the
+      batch over the whole corpus, row-sharded over the N ranks (one process per
+      GPU) with an RCCL all-gather + GPU merge of the per-shard lists.
+  c2  1M x 1536 fp32, batch 1024, top-10 IP (same path, smaller corpus).
+  c4  graph_refresher self-join: 1M student rows, cosine top-50 excluding self;
+      the corpus is replicated and the query rows are split over the ranks.
+  c5  50M x 1536 bf16-stored corpus (row-sharded), batches of 8 queries with a
+      1 % remove + 1 % append mutation every 10 batches (seed 91011); recall@10
+      of the final index against fp32 exact search on 1000 queries (1 GPU).
+Corpus and queries are generated on the device by the counter-based generator
+(no dataset exists offline) and are resident in HBM before the timed region.
 
-Rank 0 prints ONE JSON line with, besides the driver's fields:
-  roofline      dominant kernel (gemm_topk_f32): algorithmic FLOP per launch
-                (2 * N_shard * d * B) / mean launch time from HIP events recorded
-                on the launch stream, against the fp32 matrix peak (157.3 TFLOP/s)
-  batch1        the B=1 latency path (gemv_topk_f32, HBM-bound) on the same corpus
-  cpu_baseline  the faiss-semantics CPU port (oracle/flat.knn_faiss_fp32: blocked
-                numpy-BLAS sgemm + top-k, all host threads) on a bounded sample,
-                extrapolated to the full corpus (flat scan cost is linear in N)
+Rank 0 prints ONE JSON line.  Besides the driver's fields:
+  roofline      the dominant kernel: algorithmic work per launch (FLOP for the
+                MFMA kernels, bytes for the HBM-bound GEMV) / mean launch time from
+                HIP events recorded on the launch stream (vs_timer_*), against the
+                fp32 (157.3 TFLOP/s) / bf16 (2.5 PFLOP/s) matrix peak or 8 TB/s HBM;
+                `traffic` is the PMC-measured HBM bytes per launch when a rocprofv3
+                summary for this workload exists in profiles/ (tools/pmc_summary.py)
+  batch1        (c3/c2) the B=1 latency path (gemv_topk, HBM-bound), same corpus
+  cpu_baseline  (c3/c2, N=1) the faiss-semantics CPU port (oracle/flat.knn_faiss_fp32:
+                blocked numpy-BLAS sgemm + top-k, all host threads) on a bounded
+                sample, extrapolated linearly in N (a flat scan is linear in N)
 """
 
 from __future__ import annotations
 
 import argparse
+import ctypes
+import glob
 import json
 import os
 import sys
@@ -34,36 +44,64 @@ sys.path.insert(0, os.path.join(ROOT, "book-recommendation-engine_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC_NAME = "exact top-10 queries/sec at 10M×1536 fp32 (1/8 GPU) + % HBM/MFMA roofline"
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (matrix)
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA (dense)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+DEFAULTS = {
+    "c3": dict(ntotal=10_000_000, batch=4096, k=10, metric="ip", dtype="f32"),
+    "c2": dict(ntotal=1_000_000, batch=1024, k=10, metric="ip", dtype="f32"),
+    "c4": dict(ntotal=1_000_000, batch=0, k=50, metric="cos", dtype="f32"),
+    "c5": dict(ntotal=50_000_000, batch=8, k=10, metric="ip", dtype="bf16"),
+}
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--ntotal", type=int, default=10_000_000)
+    p.add_argument("--workload", choices=sorted(DEFAULTS), default="c3")
+    p.add_argument("--ntotal", type=int, default=None)
     p.add_argument("--d", type=int, default=1536)
-    p.add_argument("--batch", type=int, default=4096)
-    p.add_argument("--k", type=int, default=10)
-    p.add_argument("--metric", choices=["ip", "l2"], default="ip")
+    p.add_argument("--batch", type=int, default=None)
+    p.add_argument("--k", type=int, default=None)
+    p.add_argument("--metric", choices=["ip", "l2"], default=None)
     p.add_argument("--batch1-steps", type=int, default=20)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=1024)
-    return p.parse_args()
+    p.add_argument("--recall-queries", type=int, default=1000)
+    a = p.parse_args()
+    for key, val in DEFAULTS[a.workload].items():
+        if getattr(a, key, None) is None:
+            setattr(a, key, val)
+    if a.steps is None:
+        a.steps = {"c3": 5, "c2": 10, "c4": 2, "c5": 30}[a.workload]
+    return a
 
 
-def cpu_baseline(index, args, xq_host):
+def pmc_traffic(workload: str, kernel_prefix: str):
+    """HBM bytes per launch of `kernel_prefix` from the newest PMC summary in profiles/."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{workload}.json")))
+    if not files:
+        return None, None
+    with open(files[-1], encoding="utf-8") as f:
+        summ = json.load(f)
+    for name, rec in summ.get("kernels", {}).items():
+        if name.startswith(kernel_prefix):
+            return rec.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    return None, os.path.relpath(files[-1], ROOT)
+
+
+def cpu_baseline(shard, args, xq_host):
     """faiss-semantics CPU port timed on a bounded sample of the same workload."""
-    import numpy as np
     from threadpoolctl import threadpool_info
 
     from oracle import flat
 
-    n = min(args.cpu_rows, index.shard.ntotal)
-    xb = index.shard.reconstruct_n(0, n)  # the same synthetic rows, copied to host
+    n = min(args.cpu_rows, shard.ntotal)
+    xb = shard.reconstruct_n(0, n)  # the same synthetic rows, copied to host
     xq = xq_host[: args.cpu_queries]
     metric = flat.METRIC_INNER_PRODUCT if args.metric == "ip" else flat.METRIC_L2
     flat.knn_faiss_fp32(xb[:1000], xq[:8], args.k, metric)  # warm BLAS threads
@@ -71,9 +109,7 @@ def cpu_baseline(index, args, xq_host):
     flat.knn_faiss_fp32(xb, xq, args.k, metric)
     dt = time.perf_counter() - t0
     threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    qps_sample = xq.shape[0] / dt
-    qps_full = qps_sample * n / args.ntotal
-    del xb
+    qps_full = xq.shape[0] / dt * n / args.ntotal
     return {
         "value": round(qps_full, 3),
         "unit": "queries/s",
@@ -86,154 +122,315 @@ def cpu_baseline(index, args, xq_host):
     }
 
 
-def main():
-    args = parse()
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.args = torch, dist, args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={self.world}; using WORLD_SIZE",
+                  file=sys.stderr)
+        torch.cuda.set_device(self.local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=self.rank, world_size=self.world,
+                                device_id=torch.device("cuda", self.local))
+        from vsearch import _lib
+
+        self.lib = _lib
+        self.stream = torch.cuda.current_stream().cuda_stream
+
+    def sync_all(self):
+        self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max_over_ranks(self, x: float) -> float:
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def queries(self, n, d, row0=50_000_000, seed=5678):
+        q = self.torch.empty((n, d), dtype=self.torch.float32, device="cuda")
+        self.lib.check(self.lib.load().vs_fill_synthetic(
+            ctypes.c_void_p(q.data_ptr()), n, d, seed, row0, ctypes.c_void_p(self.stream)))
+        self.torch.cuda.synchronize()
+        return q
+
+    def timed(self, fn, steps, warmup):
+        """W untimed steps; K timed steps bracketed by barrier + synchronize;
+        max over ranks.  Returns (seconds, kernel_ms_total, kernel_launches, last)."""
+        last = None
+        for _ in range(warmup):
+            last = fn(-1)
+        self.torch.cuda.synchronize()
+        self.lib.timer_reset()
+        self.lib.timer_enable(True)
+        self.sync_all()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            last = fn(i)
+        self.torch.cuda.synchronize()
+        self.dist.barrier()
+        t1 = time.perf_counter()
+        self.lib.timer_enable(False)
+        kms, nl = self.lib.timer_read()
+        return self.max_over_ranks(t1 - t0), kms, nl, last
+
+
+def base_result(args, ctx, value, elapsed, unit="queries/s"):
+    return {
+        "metric": METRIC_NAME,
+        "value": round(value, 3),
+        "unit": unit,
+        "n_gpus": ctx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32" if args.dtype == "f32" else "bf16",
+        "data": "synthetic: counter-based splitmix64 rows in [-1,1) generated on device "
+                "(corpus seed 1234, queries seed 5678)",
+    }
+
+
+def roofline(kind, achieved, launches, mean_s, per_launch, kernel, traffic, traffic_src):
+    if kind == "mfma32":
+        peak, unit, bound = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
+    elif kind == "mfma16":
+        peak, unit, bound = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
+    else:
+        peak, unit, bound = HBM_PEAK_GBS, "GB/s", "hbm"
+    r = {"bound": bound, "kernel": kernel, "achieved": round(achieved, 3), "peak": peak,
+         "unit": unit, "frac": round(achieved / peak, 4) if peak else None,
+         "traffic": traffic,
+         "per_launch": f"{per_launch}; mean launch {mean_s * 1e3:.3f} ms over {launches} launches"}
+    if traffic_src:
+        r["traffic_source"] = traffic_src
+    return r
+
+
+def run_knn(args, ctx):
     import numpy as np
-    import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
-              file=sys.stderr)
-    torch.cuda.set_device(local)
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29517")
-    dist.init_process_group("nccl", rank=rank, world_size=world,
-                            device_id=torch.device("cuda", local))
-
-    from vsearch import _lib
     from vsearch import faiss as vfaiss
     from vsearch.sharded import ShardedIndexFlat
 
+    torch = ctx.torch
     metric = vfaiss.METRIC_INNER_PRODUCT if args.metric == "ip" else vfaiss.METRIC_L2
-    index = ShardedIndexFlat(args.d, metric, device=local)
+    index = ShardedIndexFlat(args.d, metric, device=ctx.local, dtype=args.dtype)
     index.add_synthetic(args.ntotal, seed=1234)
     n_shard = index.shard.ntotal
-
     B, d, k = args.batch, args.d, args.k
-    stream = torch.cuda.current_stream().cuda_stream
-    xq = torch.empty((B, d), dtype=torch.float32, device="cuda")
-    _lib.check(_lib.load().vs_fill_synthetic(
-        __import__("ctypes").c_void_p(xq.data_ptr()), B, d, 5678, 50_000_000,
-        __import__("ctypes").c_void_p(stream)))
-    torch.cuda.synchronize()
+    xq = ctx.queries(B, d)
 
-    def step():
-        return index.search_device(xq, k, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    _lib.timer_reset()
-    _lib.timer_enable(True)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        D, I = step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t1 = time.perf_counter()
-    _lib.timer_enable(False)
-    kern_ms, launches = _lib.timer_read()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
-
-    # sanity on the result of the last step (sorted, in range)
+    elapsed, kms, nl, (D, I) = ctx.timed(
+        lambda i: index.search_device(xq, k, stream=ctx.stream), args.steps, args.warmup)
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
-    ok = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
-    ok &= bool((np.diff(Dh, axis=1) <= 0).all() if metric == vfaiss.METRIC_INNER_PRODUCT
-               else (np.diff(Dh, axis=1) >= 0).all())
+    sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
+    sane &= bool((np.diff(Dh, axis=1) <= 0).all() if metric == vfaiss.METRIC_INNER_PRODUCT
+                 else (np.diff(Dh, axis=1) >= 0).all())
+    mean_s = kms / max(1, nl) / 1e3
+    flops = 2.0 * n_shard * d * B
+    esz = 4 if args.dtype == "f32" else 2
+    gemv = B <= 8
+    kname = "gemv_topk" if gemv else "gemm_topk"
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname)
+    if gemv:
+        rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
+                      f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
+                      kname, traffic, tsrc)
+    else:
+        rf = roofline("mfma32" if esz == 4 else "mfma16", flops / mean_s / 1e12, nl, mean_s,
+                      f"2*{n_shard}*{d}*{B} FLOP (one launch = whole batch over the rank's shard)",
+                      kname, traffic, tsrc)
 
-    mean_kern_s = kern_ms / max(1, launches) / 1e3
-    flops_launch = 2.0 * n_shard * d * B
-    achieved_tf = flops_launch / mean_kern_s / 1e12 if mean_kern_s > 0 else 0.0
-
-    # batch-1 latency path (HBM-bound GEMV kernel)
     batch1 = None
-    if args.batch1_steps > 0:
+    if args.batch1_steps > 0 and not gemv:
         q1 = xq[:1].contiguous()
-        for _ in range(3):
-            index.search_device(q1, k, stream=stream)
-        torch.cuda.synchronize()
-        _lib.timer_reset()
-        _lib.timer_enable(True)
-        dist.barrier()
-        torch.cuda.synchronize()
-        b0 = time.perf_counter()
-        for _ in range(args.batch1_steps):
-            index.search_device(q1, k, stream=stream)
-        torch.cuda.synchronize()
-        dist.barrier()
-        b1 = time.perf_counter()
-        _lib.timer_enable(False)
-        k1_ms, k1_n = _lib.timer_read()
-        bt = torch.tensor([b1 - b0], dtype=torch.float64, device="cuda")
-        dist.all_reduce(bt, op=dist.ReduceOp.MAX)
-        lat = float(bt.item()) / args.batch1_steps
-        kern1 = k1_ms / max(1, k1_n) / 1e3
-        bytes1 = n_shard * d * 4.0
-        batch1 = {
-            "ms_per_query": round(lat * 1e3, 4),
-            "qps": round(1.0 / lat, 2),
-            "kernel": "gemv_topk_f32",
-            "kernel_ms": round(kern1 * 1e3, 4),
-            "achieved_GBs": round(bytes1 / kern1 / 1e9, 1) if kern1 > 0 else None,
-            "frac_hbm_peak": round(bytes1 / kern1 / 1e9 / HBM_PEAK_GBS, 4) if kern1 > 0 else None,
-        }
+        t1, k1, n1, _ = ctx.timed(lambda i: index.search_device(q1, k, stream=ctx.stream),
+                                  args.batch1_steps, 3)
+        kern1 = k1 / max(1, n1) / 1e3
+        bytes1 = n_shard * d * esz
+        batch1 = {"ms_per_query": round(t1 / args.batch1_steps * 1e3, 4),
+                  "qps": round(args.batch1_steps / t1, 2), "kernel": "gemv_topk",
+                  "kernel_ms": round(kern1 * 1e3, 4),
+                  "achieved_GBs": round(bytes1 / kern1 / 1e9, 1) if kern1 > 0 else None,
+                  "frac_hbm_peak": round(bytes1 / kern1 / 1e9 / HBM_PEAK_GBS, 4)
+                  if kern1 > 0 else None}
 
-    result = None
-    if rank == 0:
+    if ctx.rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            xq_host = xq.cpu().numpy()
-            cpu = cpu_baseline(index, args, xq_host)
-        value = args.steps * B / elapsed
-        result = {
-            "metric": METRIC_NAME,
-            "value": round(value, 3),
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic: counter-based splitmix64 rows in [-1,1) generated on device "
-                    "(corpus seed 1234, queries seed 5678)",
-            "config": {
-                "workload": f"C3: {args.ntotal}x{d} fp32 exact flat "
-                            f"{'inner-product' if args.metric == 'ip' else 'L2'}, "
-                            f"batch {B}, top-{k}",
-                "ntotal": args.ntotal, "d": d, "batch": B, "k": k,
-                "metric": args.metric,
-                "parallelism": f"row-shard x{world} + RCCL all-gather top-k merge",
-            },
-            "roofline": {
-                "bound": "mfma",
-                "kernel": "gemm_topk_f32",
-                "achieved": round(achieved_tf, 3),
-                "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tf / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None,
-                "per_launch": f"2*{n_shard}*{d}*{B} FLOP (one launch = whole batch over the "
-                              f"rank's shard); mean launch {mean_kern_s * 1e3:.3f} ms over "
-                              f"{launches} launches",
-            },
-            "batch1": batch1,
-            "cpu_baseline": cpu,
-            "result_sane": ok,
-        }
-        print(json.dumps(result), flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
+        if not args.no_cpu_baseline and ctx.world == 1 and args.dtype == "f32":
+            cpu = cpu_baseline(index.shard, args, xq.cpu().numpy())
+        res = base_result(args, ctx, args.steps * B / elapsed, elapsed)
+        res["config"] = {
+            "workload": f"{args.workload.upper()}: {args.ntotal}x{d} {args.dtype} exact flat "
+                        f"{'inner-product' if args.metric == 'ip' else 'L2'}, batch {B}, top-{k}",
+            "ntotal": args.ntotal, "d": d, "batch": B, "k": k, "metric": args.metric,
+            "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge"}
+        res["roofline"] = rf
+        res["batch1"] = batch1
+        res["cpu_baseline"] = cpu
+        res["result_sane"] = sane
+        return res
+    return None
+
+
+def run_selfjoin(args, ctx):
+    """C4: graph_refresher self-join (cosine top-k excluding self); the corpus is
+    replicated on every rank and the query rows are split (no collective)."""
+    from vsearch import faiss as vfaiss
+    from vsearch.sharded import shard_bounds
+
+    torch = ctx.torch
+    N, d, k = args.ntotal, args.d, args.k
+    index = vfaiss.IndexFlat(d, vfaiss.METRIC_INNER_PRODUCT, device=ctx.local, dtype=args.dtype)
+    index.reserve(N)
+    index.add_synthetic(N, seed=1234)
+    lo, hi = shard_bounds(N, ctx.world, ctx.rank)
+    nq = hi - lo
+    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+
+    def step(i):
+        index.selfjoin_device(k, lo, nq, D.data_ptr(), I.data_ptr(), stream=ctx.stream)
+        return None
+
+    elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
+    Ih = I.cpu()
+    sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
+        (Ih == torch.arange(lo, hi)[:, None]).any())
+    mean_s = kms / max(1, nl) / 1e3
+    flops_total = 2.0 * N * d * nq
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::gemm_topk")
+    esz = 4 if args.dtype == "f32" else 2
+    rf = roofline("mfma32" if esz == 4 else "mfma16",
+                  flops_total / (kms / 1e3) / 1e12 if kms > 0 else 0.0, nl, mean_s,
+                  f"2*{N}*{d}*(<=65536 query rows per launch); {nq} query rows per rank per step",
+                  "gemm_topk", traffic, tsrc)
+    if ctx.rank == 0:
+        res = base_result(args, ctx, args.steps * N / elapsed, elapsed, unit="students/s")
+        res["config"] = {"workload": f"C4: self-join {N}x{d} cosine top-{k} excluding self",
+                         "ntotal": N, "d": d, "k": k,
+                         "parallelism": f"replicated corpus, query rows split x{ctx.world}"}
+        res["roofline"] = rf
+        res["result_sane"] = sane
+        res["cpu_baseline"] = None
+        return res
+    return None
+
+
+def run_c5(args, ctx):
+    """C5: bf16-stored corpus, interleaved mutations and small query batches,
+    recall@10 against fp32 exact search on the final corpus."""
+    import numpy as np
+
+    from vsearch import faiss as vfaiss
+    from vsearch.sharded import ShardedIndexFlat
+
+    torch = ctx.torch
+    metric = vfaiss.METRIC_INNER_PRODUCT if args.metric == "ip" else vfaiss.METRIC_L2
+    N, d, k, B = args.ntotal, args.d, args.k, args.batch
+    index = ShardedIndexFlat(d, metric, device=ctx.local, dtype=args.dtype)
+    index.add_synthetic(N, seed=1234)
+    gen = np.arange(N, dtype=np.int64)  # generator row of every current label
+    next_gen = N
+    rng = np.random.default_rng(91011)
+    xq = ctx.queries(max(B, args.recall_queries), d)
+    nmut = max(1, N // 100)
+    mut_time = 0.0
+
+    def step(i):
+        nonlocal gen, next_gen, mut_time
+        if i >= 0 and i % 10 == 9:  # 1 % removes + 1 % appends every 10 batches
+            t0 = time.perf_counter()
+            rm = np.sort(rng.choice(gen.size, nmut, replace=False)).astype(np.int64)
+            index.remove_ids(rm)
+            gen = np.delete(gen, rm)
+            add = np.arange(next_gen, next_gen + nmut, dtype=np.int64)
+            next_gen += nmut
+            index.append_synthetic_ids(add, seed=1234)
+            gen = np.concatenate([gen, add])
+            mut_time += time.perf_counter() - t0
+        j = (max(i, 0) * B) % (xq.shape[0] - B + 1)
+        return index.search_device(xq[j:j + B], k, stream=ctx.stream)
+
+    elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
+    assert index.ntotal == gen.size
+    mean_s = kms / max(1, nl) / 1e3
+    n_shard = index.shard.ntotal
+    esz = 2 if args.dtype == "bf16" else 4
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::gemv_topk")
+    rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
+                  f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
+                  "gemv_topk", traffic, tsrc)
+    recall = None
+    if ctx.world == 1 and args.recall_queries > 0:
+        nr = args.recall_queries
+        q = xq[:nr].contiguous()
+        Dg, Ig = index.search_device(q, k, stream=ctx.stream)
+        Ig = Ig.cpu().numpy()
+        # fp32 exact reference over the same (mutated) corpus, rebuilt chunk by chunk
+        chunk = 4_000_000
+        parts_D, parts_I = [], []
+        for a in range(0, gen.size, chunk):
+            ref = vfaiss.IndexFlat(d, metric, device=ctx.local)
+            ref.add_synthetic_ids(gen[a:a + chunk], seed=1234)
+            ref.set_id_base(a)
+            Dr = torch.empty((nr, k), dtype=torch.float32, device="cuda")
+            Ir = torch.empty((nr, k), dtype=torch.int64, device="cuda")
+            ref.search_device(q.data_ptr(), nr, k, Dr.data_ptr(), Ir.data_ptr(), ctx.stream)
+            torch.cuda.synchronize()
+            parts_D.append(Dr)
+            parts_I.append(Ir)
+            del ref
+        Dm = torch.empty((nr, k), dtype=torch.float32, device="cuda")
+        Im = torch.empty((nr, k), dtype=torch.int64, device="cuda")
+        Dall = torch.stack(parts_D).contiguous()
+        Iall = torch.stack(parts_I).contiguous()
+        ctx.lib.check(ctx.lib.load().vs_merge_topk(
+            ctypes.c_void_p(Dall.data_ptr()), ctypes.c_void_p(Iall.data_ptr()), len(parts_D), nr,
+            k, k, metric, ctypes.c_void_p(Dm.data_ptr()), ctypes.c_void_p(Im.data_ptr()),
+            ctypes.c_void_p(ctx.stream)))
+        torch.cuda.synchronize()
+        Im = Im.cpu().numpy()
+        recall = float(np.mean([len(set(Ig[i]) & set(Im[i])) / k for i in range(nr)]))
+    mt = ctx.max_over_ranks(mut_time)
+    if ctx.rank == 0:
+        res = base_result(args, ctx, args.steps * B / elapsed, elapsed)
+        res["config"] = {"workload": f"C5: {N}x{d} {args.dtype}-stored flat "
+                                     f"{'IP' if args.metric == 'ip' else 'L2'}, batch {B}, "
+                                     f"top-{k}, 1% remove + 1% append every 10 batches",
+                         "ntotal": N, "d": d, "batch": B, "k": k,
+                         "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge"}
+        res["roofline"] = rf
+        res["recall_at_10_vs_fp32"] = recall
+        res["recall_queries"] = args.recall_queries if recall is not None else 0
+        res["mutation_seconds_in_timed_region"] = round(mt, 3)
+        res["cpu_baseline"] = None
+        return res
+    return None
+
+
+def main():
+    args = parse()
+    ctx = Ctx(args)
+    if args.workload in ("c3", "c2"):
+        res = run_knn(args, ctx)
+    elif args.workload == "c4":
+        res = run_selfjoin(args, ctx)
+    else:
+        res = run_c5(args, ctx)
+    if ctx.rank == 0 and res is not None:
+        print(json.dumps(res), flush=True)
+    ctx.dist.barrier()
+    ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

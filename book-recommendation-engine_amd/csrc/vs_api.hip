@@ -354,6 +354,34 @@ int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void
   return VS_OK;
 }
 
+int vs_add_synthetic_ids(vs_index* idx, const int64_t* ids, int64_t n, uint64_t seed,
+                         void* stream) {
+  if (!idx) return fail(VS_E_INVALID, "vs_add_synthetic_ids: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_add_synthetic_ids: n < 0");
+  if (n == 0) return VS_OK;
+  if (!ids) return fail(VS_E_INVALID, "vs_add_synthetic_ids: null ids");
+  if (idx->ntotal + n >= (int64_t)INT32_MAX - 2 * kRowPad)
+    return fail(VS_E_UNSUPPORTED, "vs_add_synthetic_ids: a shard holds fewer than 2^31 rows");
+  hipStream_t st = (hipStream_t)stream;
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  DeviceGuard g(idx->device);
+  int rc = ensure_capacity(idx, idx->ntotal + n, st);
+  if (rc) return rc;
+  Scratch scr(st);
+  int64_t* dids = nullptr;
+  VS_HIP(scr.alloc((void**)&dids, (size_t)n * sizeof(int64_t)), "vs_add_synthetic_ids: scratch");
+  VS_HIP(hipMemcpyAsync(dids, ids, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, st),
+         "vs_add_synthetic_ids: upload");
+  VS_HIP(launch_fill_synthetic_ids(idx->row(idx->ntotal), idx->esize, dids, n, idx->d, idx->ld,
+                                   seed, st),
+         "vs_add_synthetic_ids: fill");
+  VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
+         "vs_add_synthetic_ids: norms");
+  VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic_ids: synchronise");
+  idx->ntotal += n;
+  return VS_OK;
+}
+
 int vs_reset(vs_index* idx) {
   if (!idx) return fail(VS_E_INVALID, "vs_reset: null index");
   std::unique_lock<std::shared_mutex> lk(idx->mu);

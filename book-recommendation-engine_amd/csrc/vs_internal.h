@@ -79,6 +79,9 @@ hipError_t launch_rsqrt(const float* norm, int64_t n, float* out, hipStream_t st
 // Counter-based synthetic rows into a pitched fp32 or bf16 buffer (zero padding d..ldo).
 hipError_t launch_fill_synthetic(void* out, int esize, int64_t rows, int64_t d, int64_t ldo,
                                  uint64_t seed, int64_t row0, hipStream_t st);
+// Same generator for an explicit list of generator row numbers (device int64).
+hipError_t launch_fill_synthetic_ids(void* out, int esize, const int64_t* ids, int64_t rows,
+                                     int64_t d, int64_t ldo, uint64_t seed, hipStream_t st);
 // Fill n (D, I) pairs with the empty-result sentinel of `mode`.
 hipError_t launch_fill_empty(int mode, float* D, int64_t* I, int64_t n, hipStream_t st);
 // Stable compaction helper: copy the kept rows of [src0, src0+n) into tmp,

@@ -426,6 +426,37 @@ hipError_t launch_fill_synthetic(void* out, int esize, int64_t rows, int64_t d, 
   return hipGetLastError();
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void fill_synthetic_ids_kernel(T* __restrict__ out,
+                                                                 const int64_t* __restrict__ ids,
+                                                                 int64_t rows, int64_t d,
+                                                                 int64_t ldo, uint64_t seed) {
+  const int64_t row = blockIdx.y + (int64_t)blockIdx.z * 65535;
+  if (row >= rows) return;
+  const uint64_t base = (uint64_t)ids[row] * (uint64_t)d;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < ldo; j += (int64_t)gridDim.x * 256) {
+    float v = 0.0f;
+    if (j < d) {
+      const uint64_t z = splitmix64(seed ^ (base + (uint64_t)j));
+      v = (float)(z >> 40) * (1.0f / 8388608.0f) - 1.0f;
+    }
+    if constexpr (sizeof(T) == 4) out[row * ldo + j] = v;
+    else out[row * ldo + j] = f32_to_bf16_rne(v);
+  }
+}
+
+hipError_t launch_fill_synthetic_ids(void* out, int esize, const int64_t* ids, int64_t rows,
+                                     int64_t d, int64_t ldo, uint64_t seed, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  if (esize == 4)
+    hipLaunchKernelGGL(fill_synthetic_ids_kernel<float>, pitched_grid(rows, ldo), dim3(256), 0,
+                       st, (float*)out, ids, rows, d, ldo, seed);
+  else
+    hipLaunchKernelGGL(fill_synthetic_ids_kernel<uint16_t>, pitched_grid(rows, ldo), dim3(256), 0,
+                       st, (uint16_t*)out, ids, rows, d, ldo, seed);
+  return hipGetLastError();
+}
+
 __global__ void fill_empty_kernel(int asc, float* __restrict__ D, int64_t* __restrict__ I,
                                   int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -44,6 +44,7 @@ SIGNATURES = {
     "vs_reserve": (_c_int, [_vp, _c_i64]),
     "vs_add": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp]),
     "vs_add_synthetic": (_c_int, [_vp, _c_i64, ctypes.c_uint64, _c_i64, _vp]),
+    "vs_add_synthetic_ids": (_c_int, [_vp, _vp, _c_i64, ctypes.c_uint64, _vp]),
     "vs_reset": (_c_int, [_vp]),
     "vs_ntotal": (_c_int, [_vp, _i64p]),
     "vs_dim": (_c_int, [_vp, ctypes.POINTER(_c_int)]),

@@ -160,6 +160,15 @@ class IndexFlat(Index):
                                               int(row0), ctypes.c_void_p(stream)),
                    "vs_add_synthetic")
 
+    def add_synthetic_ids(self, ids, seed: int, stream: int = 0) -> None:
+        """Append the synthetic corpus rows with generator row numbers `ids`."""
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        if ids.size:
+            _lib.check(self._lib.vs_add_synthetic_ids(self._h, ids.ctypes.data, ids.size,
+                                                      ctypes.c_uint64(seed),
+                                                      ctypes.c_void_p(stream)),
+                       "vs_add_synthetic_ids")
+
     def reserve(self, n: int) -> None:
         _lib.check(self._lib.vs_reserve(self._h, int(n)), "vs_reserve")
 

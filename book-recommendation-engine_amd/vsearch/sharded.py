@@ -35,7 +35,7 @@ class ShardedIndexFlat:
     initialised (any backend for host tensors; "nccl" for device tensors)."""
 
     def __init__(self, d: int, metric: int = vfaiss.METRIC_L2, *, device: Optional[int] = None,
-                 group=None, shard=None, merge=None):
+                 group=None, shard=None, merge=None, dtype: str = "f32"):
         """`shard` / `merge` let tests substitute the per-rank index and the list
         merge (e.g. the CPU oracle under gloo); production uses the GPU ones."""
         import torch.distributed as dist
@@ -44,7 +44,8 @@ class ShardedIndexFlat:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.shard = shard if shard is not None else vfaiss.IndexFlat(d, metric, device=device)
+        self.shard = (shard if shard is not None
+                      else vfaiss.IndexFlat(d, metric, device=device, dtype=dtype))
         self._merge = merge
         self.d = d
         self.metric_type = metric
@@ -81,6 +82,13 @@ class ShardedIndexFlat:
         if hi > lo:
             self.shard.reserve(hi - lo)
             self.shard.add_synthetic(hi - lo, seed, row0=lo)
+        self._sync_counts()
+
+    def append_synthetic_ids(self, gen_ids, seed: int) -> None:
+        """Append synthetic rows (by generator row number) at the end of the
+        global label space, i.e. on the last shard."""
+        if self.rank == self.world - 1:
+            self.shard.add_synthetic_ids(gen_ids, seed)
         self._sync_counts()
 
     def add_global(self, x: np.ndarray) -> None:

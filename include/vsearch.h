@@ -83,6 +83,12 @@ int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream);
  * (row r = global row row0 + i; see vs_fill_synthetic).  Benchmark/test feed only. */
 int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void* stream);
 
+/* Appends n rows whose synthetic generator row numbers are ids[0..n) (host int64
+ * array): row j of the append equals row ids[j] of vs_fill_synthetic's corpus.
+ * Lets a benchmark rebuild any mutated corpus exactly.  Benchmark/test feed only. */
+int vs_add_synthetic_ids(vs_index* idx, const int64_t* ids, int64_t n, uint64_t seed,
+                         void* stream);
+
 /* faiss Index::reset(). */
 int vs_reset(vs_index* idx);
 
