@@ -238,8 +238,8 @@ def run_knn(args, ctx):
     mean_s = kms / max(1, nl) / 1e3
     flops = 2.0 * n_shard * d * B
     esz = 4 if args.dtype == "f32" else 2
-    gemv = B <= 8
-    kname = "gemv_topk" if gemv else "gemm_topk"
+    kname = ctx.lib.timer_kernel()
+    gemv = kname != "gemm_topk"  # the small-batch kernels are HBM-bound
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname)
     if gemv:
         rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
@@ -258,7 +258,7 @@ def run_knn(args, ctx):
         kern1 = k1 / max(1, n1) / 1e3
         bytes1 = n_shard * d * esz
         batch1 = {"ms_per_query": round(t1 / args.batch1_steps * 1e3, 4),
-                  "qps": round(args.batch1_steps / t1, 2), "kernel": "gemv_topk",
+                  "qps": round(args.batch1_steps / t1, 2), "kernel": ctx.lib.timer_kernel(),
                   "kernel_ms": round(kern1 * 1e3, 4),
                   "achieved_GBs": round(bytes1 / kern1 / 1e9, 1) if kern1 > 0 else None,
                   "frac_hbm_peak": round(bytes1 / kern1 / 1e9 / HBM_PEAK_GBS, 4)
@@ -366,10 +366,11 @@ def run_c5(args, ctx):
     mean_s = kms / max(1, nl) / 1e3
     n_shard = index.shard.ntotal
     esz = 2 if args.dtype == "bf16" else 4
-    traffic, tsrc = pmc_traffic(args.workload, "void vs::gemv_topk")
+    kname = ctx.lib.timer_kernel()
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname)
     rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
                   f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
-                  "gemv_topk", traffic, tsrc)
+                  kname, traffic, tsrc)
     recall = None
     if ctx.world == 1 and args.recall_queries > 0:
         nr = args.recall_queries

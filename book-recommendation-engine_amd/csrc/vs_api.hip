@@ -96,10 +96,16 @@ std::mutex g_timer_mu;
 bool g_timer_on = false;
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_timer_events;
 
+const char* g_timer_kernel = "";
+
 struct KernelTimer {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;
-  explicit KernelTimer(hipStream_t s) : st(s) {
+  KernelTimer(hipStream_t s, const char* name) : st(s) {
+    {
+      std::lock_guard<std::mutex> g(g_timer_mu);
+      g_timer_kernel = name;
+    }
     std::lock_guard<std::mutex> g(g_timer_mu);
     if (!g_timer_on) return;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
@@ -178,8 +184,47 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   Partials part;
   part.KP = KP;
 
-  const bool gemv = (mode == MODE_IP || mode == MODE_L2) && self0 < 0 && nq <= kGemvMaxQ &&
-                    (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
+  // Small batches stream the corpus once: the skinny MFMA kernel (any metric /
+  // dtype), except fp32 L2 with nq <= 8, which keeps faiss's direct sum (x-q)^2
+  // branch on the GEMV kernel.  VS_SMALL_BATCH=gemv|skinny overrides (A/B runs).
+  static const char* pref = getenv("VS_SMALL_BATCH");
+  const bool small_ok = (mode == MODE_IP || mode == MODE_L2) && self0 < 0;
+  const bool gemv_ok = small_ok && nq <= kGemvMaxQ &&
+                       (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <=
+                           64 * 1024;
+  const bool skinny_ok = small_ok && nq <= kSkinnyMaxQ && KP <= 32 && (nq <= 16 || KP <= 16) &&
+                         (idx->ld * idx->esize) % 64 == 0;
+  bool gemv;
+  bool skinny;
+  if (pref && strcmp(pref, "gemv") == 0) {
+    gemv = gemv_ok;
+    skinny = !gemv && skinny_ok;
+  } else if (pref && strcmp(pref, "skinny") == 0) {
+    skinny = skinny_ok;
+    gemv = !skinny && gemv_ok;
+  } else {
+    // measured (MI355X, 10M x 1536): fp32 batch-1 GEMV 83 % of HBM vs skinny 76 %;
+    // bf16 batch-8 skinny 80 % vs GEMV 29 % (profiles/r01_small_batch_ab.txt)
+    gemv = gemv_ok && idx->esize == 4 && (nq <= 2 || mode == MODE_L2);
+    skinny = !gemv && skinny_ok;
+  }
+  if (skinny) {
+    const int nblocks =
+        (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
+    part.P = nblocks;
+    const size_t n = (size_t)nq * part.P * KP;
+    VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
+    const void* qsk = qb16 ? qb16 : (const void*)qbuf;
+    KernelTimer tm(st, "skinny_topk");
+    VS_HIP(launch_skinny_topk(KP, mode, nq, idx->codes, idx->esize, xaux, qsk, qaux, idx->ld,
+                              ntotal, nblocks, part, st),
+           "vs: skinny_topk launch");
+    tm.stop();
+    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+           "vs: merge launch");
+    return VS_OK;
+  }
   // bf16 indexes hand the GEMM a bf16 copy of the (already rounded) queries
   const void* qmat = qb16 ? qb16 : (const void*)qbuf;
   if (gemv) {
@@ -190,7 +235,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     const size_t n = (size_t)nql * part.P * KP;
     VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
-    KernelTimer tm(st);
+    KernelTimer tm(st, "gemv_topk");
     VS_HIP(launch_gemv_topk(KP, gmode, nq, idx->codes, idx->esize, qbuf, idx->ld, ntotal, nblocks,
                             part, st),
            "vs: gemv_topk launch");
@@ -208,7 +253,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   const size_t n = (size_t)nq_pad * part.P * KP;
   VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
-  KernelTimer tm(st);
+  KernelTimer tm(st, "gemm_topk");
   VS_HIP(launch_gemm_topk(KP, mode, idx->codes, xaux, qmat, qaux, idx->ld, idx->esize, ntotal,
                           nq_pad, nsplit, self0, part, st),
          "vs: gemm_topk launch");
@@ -698,6 +743,11 @@ int vs_timer_reset(void) {
   }
   g_timer_events.clear();
   return VS_OK;
+}
+
+const char* vs_timer_kernel(void) {
+  std::lock_guard<std::mutex> g(g_timer_mu);
+  return g_timer_kernel;
 }
 
 int vs_timer_read(double* total_ms, int64_t* launches) {

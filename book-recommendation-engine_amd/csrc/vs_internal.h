@@ -28,6 +28,8 @@ constexpr int kBK = 32;
 constexpr int kRowPad = 256;
 // The GEMV (small batch) path handles up to this many queries per launch.
 constexpr int kGemvMaxQ = 8;
+// The skinny MFMA (small batch) path handles up to this many queries per launch.
+constexpr int kSkinnyMaxQ = 32;
 
 __host__ __device__ inline uint16_t f32_to_bf16_rne(float f) {
   uint32_t u;
@@ -56,6 +58,11 @@ hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, 
 // X fp32 or bf16 rows; Q always fp32 (values already rounded for bf16 indexes).
 hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, const float* Q,
                             int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st);
+// Small-batch MFMA path (nq <= kSkinnyMaxQ, KP <= 32, IP or L2 via norms):
+// one list per query per block, part.P == nblocks.
+hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
+                              const float* xaux, const void* Q, const float* qaux, int64_t ld,
+                              int ntotal, int nblocks, Partials part, hipStream_t st);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,

@@ -1,0 +1,288 @@
+// vs_skinny.hip — small-batch (nq <= 32) fused distance + top-k, HBM-bound.
+//
+// Every database row is used once per launch: the corpus streams through LDS
+// once (whole 128-B lines per row, the access pattern HBM wants) into 16x16 MFMA
+// tiles whose N dimension is the (padded) query batch — v_mfma_f32_16x16x4_f32
+// for fp32 rows, v_mfma_f32_16x16x32_bf16 for bf16 rows.  Padding the batch to 16
+// costs MFMA cycles the memory system does not wait for (10M x 1536 x 16 queries
+// is 0.49 TFLOP = 3 ms of fp32 matrix time against 9.6 ms of HBM time), and
+// unlike a dot-product GEMV it needs no cross-lane reductions.
+//
+// Geometry (16x16 C/D layout: column = lane & 15, row = 4 * (lane >> 4) + reg):
+//   A = 16 database rows, B = 16 queries.  A workgroup (4 waves) owns a tile of
+//   256 rows (64 per wave = 4 row groups of 16) against all the batch's queries
+//   and walks K in 128-B slices: global_load_lds_dwordx4 stages 8 rows x 128 B per
+//   wave instruction (whole cache lines, double-buffered), and fragments are read
+//   from LDS with the same XOR swizzle as the GEMM (16-B chunk c of row r at
+//   c ^ ((r >> 1) & 7): conflict-free ds_read_b128).  Per 64-B k-chunk, lane l
+//   takes the 16 B at chunk offset 16 * (l >> 4) of row l & 15 — of the X row for
+//   A, of query row l & 15 for B.  fp32: the 4 floats feed 4 MFMAs (instruction t
+//   uses element t, so lane group g covers k = 4g + t); bf16: the 8 bf16 are the
+//   operand (k = 8g + j).  Each query fragment serves all 4 row groups.
+//   After the K loop lane l holds, for query l & 15 (+16 for the second query
+//   group), the scores of rows rowbase + 16 * grp + 4 * (l >> 4) + reg: 4 lanes
+//   share a query, each with its own register list; the block folds its 16
+//   lists per query in LDS and emits one.
+#include "vs_device.h"
+
+namespace vs {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int KP, int MODE, typename T, int NQG>
+__global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
+                                                      const float* __restrict__ xaux,
+                                                      const T* __restrict__ Q,
+                                                      const float* __restrict__ qaux, int64_t ld,
+                                                      int nq, int ntotal, int rows_per_block,
+                                                      float* __restrict__ pkey,
+                                                      int* __restrict__ pid) {
+  static_assert(KP <= 32, "skinny path keeps at most 32 entries per list");
+  // LDS, three lives: [2 buffers][256 X rows + 16*NQG query rows][128 B] during
+  // the K loop; per-thread key parking (16 x 256 floats) in the epilogue; the
+  // per-query list fold ([16 queries][16 lists][KP] keys + ids) at the end.
+  constexpr int kRowsPerBuf = 256 + 16 * NQG;
+  constexpr int kStageWords = 2 * kRowsPerBuf * 32;
+  constexpr int kFold = 16 * 16 * KP;
+  constexpr int kWords0 = kStageWords > 2 * kFold ? kStageWords : 2 * kFold;
+  constexpr int kWords = kWords0 > 16 * 256 ? kWords0 : 16 * 256;
+  __shared__ __attribute__((aligned(16))) float lds[kWords];
+  float* spark = lds;
+  float* mk = lds;
+  int* mi = (int*)(lds + kFold);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int g = lane >> 4;  // lane group: 16-B offset inside a 64-B k-chunk
+  const int c16 = lane & 15;
+  const int nslice = (int)(ld * (int64_t)sizeof(T) / 128);
+  const uint32_t ldb = (uint32_t)(ld * (int64_t)sizeof(T));
+
+  float qa[NQG];
+  int qcol[NQG];
+#pragma unroll
+  for (int qg = 0; qg < NQG; ++qg) {
+    qcol[qg] = qg * 16 + c16;
+    qa[qg] = 0.0f;
+    if constexpr (MODE == MODE_L2) qa[qg] = qaux[qcol[qg]];
+  }
+
+  float lk[NQG][KP];
+  int li[NQG][KP];
+#pragma unroll
+  for (int qg = 0; qg < NQG; ++qg) list_init<KP, int>(lk[qg], li[qg]);
+
+  const int rb0 = blockIdx.x * rows_per_block;
+  const int rb1 = min(rb0 + rows_per_block, (ntotal + 255) & ~255);
+  // glds geometry: lane L of a wave instruction moves 16 B of row (L >> 3) of an
+  // 8-row group; the swizzle depends on the group only through its parity.
+  const int srow = lane >> 3;
+  uint32_t soff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int row = par * 8 + srow;
+    soff[par] = (uint32_t)srow * ldb + (uint32_t)((lane & 7) ^ ((row >> 1) & 7)) * 16u;
+  }
+  const int fsw = (c16 >> 1) & 7;  // fragment rows 16*grp + c16 share (row >> 1) & 7
+
+  for (int tb = rb0; tb < rb1; tb += 256) {
+    f32x4v acc[NQG][4];
+#pragma unroll
+    for (int qg = 0; qg < NQG; ++qg)
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) acc[qg][grp] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+    const char* xt = (const char*)(X + (int64_t)(tb + 64 * w) * ld);
+
+    auto stage = [&](int buf, int sl) {
+      float* base = lds + buf * kRowsPerBuf * 32;
+      const char* xs = xt + sl * 128;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)  // this wave's 64 rows
+        __builtin_amdgcn_global_load_lds(xs + soff[i & 1] + (uint32_t)(i * 8) * ldb,
+                                         VS_LDS(base + (64 * w + 8 * i) * 32), 16, 0, 0);
+      // query rows: 2 instructions per query group, spread over the waves
+#pragma unroll
+      for (int i = 0; i < 2 * NQG; ++i) {
+        if (w == (i & 3)) {
+          const char* qs = (const char*)Q + sl * 128;
+          __builtin_amdgcn_global_load_lds(qs + soff[i & 1] + (uint32_t)(i * 8) * ldb,
+                                           VS_LDS(base + (256 + 8 * i) * 32), 16, 0, 0);
+        }
+      }
+    };
+
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int sl = 0; sl < nslice; ++sl) {
+      if (sl + 1 < nslice) stage((sl + 1) & 1, sl + 1);
+      const float* cb = lds + (sl & 1) * kRowsPerBuf * 32;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int coff = ((4 * c + g) ^ fsw) * 4;  // in floats
+        f32x4v qf[NQG];
+#pragma unroll
+        for (int qg = 0; qg < NQG; ++qg)
+          qf[qg] = *(const f32x4v*)(cb + (256 + 16 * qg + c16) * 32 + coff);
+        f32x4v xf[4];
+#pragma unroll
+        for (int grp = 0; grp < 4; ++grp)
+          xf[grp] = *(const f32x4v*)(cb + (64 * w + 16 * grp + c16) * 32 + coff);
+#pragma unroll
+        for (int qg = 0; qg < NQG; ++qg) {
+#pragma unroll
+          for (int grp = 0; grp < 4; ++grp) {
+            if constexpr (sizeof(T) == 4) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                acc[qg][grp] = __builtin_amdgcn_mfma_f32_16x16x4f32(xf[grp][t], qf[qg][t],
+                                                                    acc[qg][grp], 0, 0, 0);
+            } else {
+              acc[qg][grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, xf[grp]), __builtin_bit_cast(bf16x8, qf[qg]),
+                  acc[qg][grp], 0, 0, 0);
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+
+    // Epilogue: keys, 16-bit candidate mask per query group, park + insert.
+    const int r = tb + 64 * w;
+#pragma unroll
+    for (int qg = 0; qg < NQG; ++qg) {
+      const float tk = lk[qg][KP - 1];
+      const int ti = li[qg][KP - 1];
+      const bool qvalid = qcol[qg] < nq;
+      uint32_t m = 0;
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        const int rowb = r + 16 * grp + 4 * g;
+        f32x4v xa = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == MODE_L2) xa = *(const f32x4v*)(xaux + rowb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = acc[qg][grp][i];
+          const float key = MODE == MODE_L2 ? l2_from_ip(qa[qg], xa[i], v) : -v;
+          acc[qg][grp][i] = key;
+          const bool cand = qvalid && (rowb + i) < ntotal && lex_less(key, rowb + i, tk, ti);
+          m |= (uint32_t)cand << (grp * 4 + i);
+        }
+      }
+      if (m) {
+#pragma unroll
+        for (int grp = 0; grp < 4; ++grp)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) spark[(grp * 4 + i) * 256 + tid] = acc[qg][grp][i];
+        do {
+          const int bi = __builtin_ctz(m);
+          m &= m - 1;
+          const int row = r + 16 * (bi >> 2) + 4 * g + (bi & 3);
+          list_insert<KP, int>(lk[qg], li[qg], spark[bi * 256 + tid], row);
+        } while (m);
+      }
+    }
+    __syncthreads();  // the next tile's first stage overwrites the parking area
+  }
+
+  // Fold the 16 lists of each query (4 lane groups x 4 waves) in LDS, one
+  // query group at a time; thread t < 16 folds query t with a 4-round tree.
+  const int slot = w * 4 + g;  // 0..15
+#pragma unroll
+  for (int qg = 0; qg < NQG; ++qg) {
+    __syncthreads();  // previous use of the LDS (parking or the last fold) is done
+    const int base = (c16 * 16 + slot) * KP;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      mk[base + j] = lk[qg][j];
+      mi[base + j] = li[qg][j];
+    }
+    __syncthreads();
+    for (int step = 1; step < 16; step <<= 1) {
+      const int q = tid >> 4, s = tid & 15;
+      if (q < 16 && (s & (2 * step - 1)) == 0) {
+        float ok[KP];
+        int oi[KP];
+        const int a = (q * 16 + s) * KP, b = (q * 16 + s + step) * KP;
+        merge2_sorted<KP, int>(mk + a, mi + a, mk + b, mi + b, ok, oi);
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+          mk[a + j] = ok[j];
+          mi[a + j] = oi[j];
+        }
+      }
+      __syncthreads();
+    }
+    const int qglob = qg * 16 + tid;
+    if (tid < 16 && qglob < nq) {
+      const int a = tid * 16 * KP;
+      float* ok = pkey + ((int64_t)qglob * gridDim.x + blockIdx.x) * KP;
+      int* oi = pid + ((int64_t)qglob * gridDim.x + blockIdx.x) * KP;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        ok[j] = mk[a + j];
+        oi[j] = mi[a + j];
+      }
+    }
+  }
+}
+
+template <int KP, int MODE, typename T>
+static hipError_t skinny_launch_t(int nq, const T* X, const float* xaux, const T* Q,
+                                  const float* qaux, int64_t ld, int ntotal, int nblocks,
+                                  Partials part, hipStream_t st) {
+  const int nt256 = (ntotal + 255) & ~255;
+  int rpb = (nt256 + nblocks - 1) / nblocks;
+  rpb = (rpb + 255) & ~255;  // whole 256-row tiles
+  if (nq <= 16)
+    hipLaunchKernelGGL((skinny_topk<KP, MODE, T, 1>), dim3(nblocks), dim3(256), 0, st, X, xaux,
+                       Q, qaux, ld, nq, ntotal, rpb, part.key, part.id);
+  else
+    hipLaunchKernelGGL((skinny_topk<KP, MODE, T, 2>), dim3(nblocks), dim3(256), 0, st, X, xaux,
+                       Q, qaux, ld, nq, ntotal, rpb, part.key, part.id);
+  return hipGetLastError();
+}
+
+template <int KP>
+static hipError_t skinny_launch_kp(int mode, int nq, const void* X, int esize, const float* xaux,
+                                   const void* Q, const float* qaux, int64_t ld, int ntotal,
+                                   int nblocks, Partials part, hipStream_t st) {
+  if (esize == 4) {
+    if (mode == MODE_L2)
+      return skinny_launch_t<KP, MODE_L2, float>(nq, (const float*)X, xaux, (const float*)Q, qaux,
+                                                 ld, ntotal, nblocks, part, st);
+    return skinny_launch_t<KP, MODE_IP, float>(nq, (const float*)X, xaux, (const float*)Q, qaux,
+                                               ld, ntotal, nblocks, part, st);
+  }
+  if (mode == MODE_L2)
+    return skinny_launch_t<KP, MODE_L2, uint16_t>(nq, (const uint16_t*)X, xaux,
+                                                  (const uint16_t*)Q, qaux, ld, ntotal, nblocks,
+                                                  part, st);
+  return skinny_launch_t<KP, MODE_IP, uint16_t>(nq, (const uint16_t*)X, xaux, (const uint16_t*)Q,
+                                                qaux, ld, ntotal, nblocks, part, st);
+}
+
+hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
+                              const float* xaux, const void* Q, const float* qaux, int64_t ld,
+                              int ntotal, int nblocks, Partials part, hipStream_t st) {
+  if (nq < 1 || nq > kSkinnyMaxQ || part.KP != KP || part.P != nblocks ||
+      (ld * esize) % 128 != 0 || (esize != 4 && esize != 2) || (mode != MODE_IP && mode != MODE_L2))
+    return hipErrorInvalidValue;
+  switch (KP) {
+    case 8:
+      return skinny_launch_kp<8>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part, st);
+    case 16:
+      return skinny_launch_kp<16>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part,
+                                  st);
+    case 32:
+      return skinny_launch_kp<32>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part,
+                                  st);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace vs

@@ -66,6 +66,7 @@ SIGNATURES = {
     "vs_timer_enable": (_c_int, [_c_int]),
     "vs_timer_reset": (_c_int, []),
     "vs_timer_read": (_c_int, [ctypes.POINTER(ctypes.c_double), _i64p]),
+    "vs_timer_kernel": (ctypes.c_char_p, []),
 }
 
 _lock = threading.Lock()
@@ -154,6 +155,11 @@ def timer_enable(on: bool = True) -> None:
 
 def timer_reset() -> None:
     check(load().vs_timer_reset())
+
+
+def timer_kernel() -> str:
+    """Name of the fused search kernel launched by the last search."""
+    return load().vs_timer_kernel().decode()
 
 
 def timer_read():

@@ -156,6 +156,9 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
 int vs_timer_enable(int on);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
+/* Name of the fused search kernel the last search launched ("gemm_topk",
+ * "skinny_topk" or "gemv_topk"). */
+const char* vs_timer_kernel(void);
 
 #ifdef __cplusplus
 }

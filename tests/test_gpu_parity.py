@@ -344,3 +344,21 @@ def test_large_synthetic_sampled(vf, metric):
             assert abs(got_s[j] - ref_s[j]) <= tol, (q, j, got_s[j], ref_s[j])
             if I[q, j] != ref_i[j]:
                 assert abs(ref_s[j] - got_s[j]) <= tol
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("nq", [1, 2, 5, 8, 13, 16, 17, 24, 32, 33])
+def test_small_batch_paths(vf, metric, nq):
+    """nq <= 32 runs the skinny MFMA kernel (fp32 L2 with nq <= 8: the GEMV)."""
+    xb = _rand(5000, 128, 30)
+    xq = _rand(nq, 128, 31)
+    for k in (1, 10, 16, 30):
+        _check(vf, xb, xq, k, metric)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_small_batch_ragged_rows(vf, metric):
+    for n in (1, 63, 64, 65, 255, 256, 257, 4097):
+        xb = _rand(n, 64, 32)
+        for nq in (3, 20):
+            _check(vf, xb, _rand(nq, 64, 33), 8, metric)
