@@ -47,6 +47,16 @@ METRIC_NAME = "exact top-10 queries/sec at 10M×1536 fp32 (1/8 GPU) + % HBM/MFMA
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA (dense)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
+# gemm_topk_x3 computes each fp32 product as 6 exact bf16 MFMA products (three-plane
+# split), so its fp32-equivalent ceiling is the dense bf16 peak / 6.
+X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
+HBM_KERNELS = ("gemv_topk", "skinny_topk")
+
+
+def mfma_kind(kname: str, esz: int) -> str:
+    if kname == "gemm_topk_x3":
+        return "mfma_x3"
+    return "mfma32" if esz == 4 else "mfma16"
 
 DEFAULTS = {
     "c3": dict(ntotal=10_000_000, batch=4096, k=10, metric="ip", dtype="f32"),
@@ -204,12 +214,18 @@ def roofline(kind, achieved, launches, mean_s, per_launch, kernel, traffic, traf
         peak, unit, bound = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
     elif kind == "mfma16":
         peak, unit, bound = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
+    elif kind == "mfma_x3":
+        peak, unit, bound = round(X3_PEAK_TFLOPS, 3), "TFLOP/s", "mfma"
     else:
         peak, unit, bound = HBM_PEAK_GBS, "GB/s", "hbm"
     r = {"bound": bound, "kernel": kernel, "achieved": round(achieved, 3), "peak": peak,
          "unit": unit, "frac": round(achieved / peak, 4) if peak else None,
          "traffic": traffic,
          "per_launch": f"{per_launch}; mean launch {mean_s * 1e3:.3f} ms over {launches} launches"}
+    if kind == "mfma_x3":
+        r["peak_note"] = ("fp32 FLOP on the bf16 matrix cores via the exact 3-plane split "
+                          "(6 bf16 MFMA products per fp32 product): 2500/6 TFLOP/s; "
+                          f"fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS}")
     if traffic_src:
         r["traffic_source"] = traffic_src
     return r
@@ -239,14 +255,14 @@ def run_knn(args, ctx):
     flops = 2.0 * n_shard * d * B
     esz = 4 if args.dtype == "f32" else 2
     kname = ctx.lib.timer_kernel()
-    gemv = kname != "gemm_topk"  # the small-batch kernels are HBM-bound
-    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname)
+    gemv = kname in HBM_KERNELS  # the small-batch kernels are HBM-bound
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     if gemv:
         rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
                       f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
                       kname, traffic, tsrc)
     else:
-        rf = roofline("mfma32" if esz == 4 else "mfma16", flops / mean_s / 1e12, nl, mean_s,
+        rf = roofline(mfma_kind(kname, esz), flops / mean_s / 1e12, nl, mean_s,
                       f"2*{n_shard}*{d}*{B} FLOP (one launch = whole batch over the rank's shard)",
                       kname, traffic, tsrc)
 
@@ -273,7 +289,8 @@ def run_knn(args, ctx):
             "workload": f"{args.workload.upper()}: {args.ntotal}x{d} {args.dtype} exact flat "
                         f"{'inner-product' if args.metric == 'ip' else 'L2'}, batch {B}, top-{k}",
             "ntotal": args.ntotal, "d": d, "batch": B, "k": k, "metric": args.metric,
-            "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge"}
+            "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge",
+            "kernel": kname}
         res["roofline"] = rf
         res["batch1"] = batch1
         res["cpu_baseline"] = cpu
@@ -308,12 +325,13 @@ def run_selfjoin(args, ctx):
         (Ih == torch.arange(lo, hi)[:, None]).any())
     mean_s = kms / max(1, nl) / 1e3
     flops_total = 2.0 * N * d * nq
-    traffic, tsrc = pmc_traffic(args.workload, "void vs::gemm_topk")
+    kname = ctx.lib.timer_kernel()
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     esz = 4 if args.dtype == "f32" else 2
-    rf = roofline("mfma32" if esz == 4 else "mfma16",
+    rf = roofline(mfma_kind(kname, esz),
                   flops_total / (kms / 1e3) / 1e12 if kms > 0 else 0.0, nl, mean_s,
                   f"2*{N}*{d}*(<=65536 query rows per launch); {nq} query rows per rank per step",
-                  "gemm_topk", traffic, tsrc)
+                  kname, traffic, tsrc)
     if ctx.rank == 0:
         res = base_result(args, ctx, args.steps * N / elapsed, elapsed, unit="students/s")
         res["config"] = {"workload": f"C4: self-join {N}x{d} cosine top-{k} excluding self",
@@ -367,7 +385,7 @@ def run_c5(args, ctx):
     n_shard = index.shard.ntotal
     esz = 2 if args.dtype == "bf16" else 4
     kname = ctx.lib.timer_kernel()
-    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname)
+    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
                   f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
                   kname, traffic, tsrc)
@@ -409,7 +427,8 @@ def run_c5(args, ctx):
                                      f"{'IP' if args.metric == 'ip' else 'L2'}, batch {B}, "
                                      f"top-{k}, 1% remove + 1% append every 10 batches",
                          "ntotal": N, "d": d, "batch": B, "k": k,
-                         "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge"}
+                         "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge",
+            "kernel": kname}
         res["roofline"] = rf
         res["recall_at_10_vs_fp32"] = recall
         res["recall_queries"] = args.recall_queries if recall is not None else 0

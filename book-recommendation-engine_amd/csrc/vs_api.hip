@@ -37,6 +37,13 @@ struct vs_index {
   int64_t rowbytes() const { return ld * esize; }
   char* row(int64_t r) const { return codes + r * rowbytes(); }
   float* norms = nullptr;  // [capacity] squared L2 norms
+  // fp32 indexes: the 3 bf16 planes of every row (hi, mid, lo; exact split) for
+  // the bf16-MFMA fp32-accurate GEMM, derived lazily from `codes`; valid for rows
+  // [0, planes_rows).  [3][capacity][ld].
+  uint16_t* planes = nullptr;
+  int64_t planes_rows = 0;
+  int engine = VS_ENGINE_AUTO;
+  std::mutex planes_mu;
   std::shared_mutex mu;
 };
 
@@ -127,6 +134,49 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
 
+void drop_planes(vs_index* idx) {
+  if (idx->planes) (void)hipFree(idx->planes);
+  idx->planes = nullptr;
+  idx->planes_rows = 0;
+}
+
+// Makes planes valid for all rows (called under the shared lock; builds are
+// serialised by planes_mu).  Returns false when the planes cannot be allocated
+// (the caller then uses the fp32 MFMA kernel).
+bool ensure_planes(vs_index* idx, hipStream_t st) {
+  std::lock_guard<std::mutex> g(idx->planes_mu);
+  if (!idx->planes) {
+    if (hipMalloc(&idx->planes, (size_t)3 * idx->capacity * idx->ld * sizeof(uint16_t)) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      idx->planes = nullptr;
+      return false;
+    }
+    idx->planes_rows = 0;
+    // padding rows must hold zeros, like the fp32 rows
+    if (hipMemsetAsync(idx->planes, 0, (size_t)3 * idx->capacity * idx->ld * sizeof(uint16_t),
+                       st) != hipSuccess)
+      return false;
+  }
+  if (idx->planes_rows < idx->ntotal) {
+    // rows up to the capacity slack are zero in codes, so splitting them keeps zeros
+    if (launch_split_planes((const float*)idx->codes, idx->ld, idx->planes_rows,
+                            idx->ntotal - idx->planes_rows, idx->planes,
+                            idx->capacity * idx->ld, st) != hipSuccess)
+      return false;
+    idx->planes_rows = idx->ntotal;
+  }
+  return true;
+}
+
+int engine_from_env() {
+  const char* e = getenv("VS_ENGINE");
+  if (!e) return VS_ENGINE_AUTO;
+  if (strcmp(e, "fp32") == 0) return VS_ENGINE_FP32_MFMA;
+  if (strcmp(e, "bf16x3") == 0) return VS_ENGINE_BF16X3;
+  return VS_ENGINE_AUTO;
+}
+
 // Grows storage to hold `rows` rows (plus the tile slack), preserving content.
 int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   const int64_t need = round_up(rows + kBQ, kRowPad);
@@ -163,6 +213,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   }
   // In-flight searches (any stream) may still read the old storage.
   VS_HIP(hipDeviceSynchronize(), "vs: storage growth");
+  drop_planes(idx);  // rebuilt lazily at the new capacity
   if (idx->codes) (void)hipFree(idx->codes);
   if (idx->norms) (void)hipFree(idx->norms);
   idx->codes = codes;
@@ -245,6 +296,45 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     return VS_OK;
   }
 
+  // fp32 indexes run the large-batch GEMM on the bf16 matrix cores through the
+  // exact 3-plane split (vs_gemm_x3.hip) unless disabled (VS_ENGINE=fp32 /
+  // vs_set_engine) or the planes do not fit in HBM.
+  int engine = idx->engine != VS_ENGINE_AUTO ? idx->engine : engine_from_env();
+  if (engine == VS_ENGINE_AUTO) engine = VS_ENGINE_BF16X3;
+  if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KP <= 32 && ensure_planes(idx, st)) {
+    const int nqt3 = nq_pad / 128;
+    const int ntiles3 = (ntotal + 255) / 256;
+    // one 8-wave workgroup per CU on 256 CUs
+    const int nsplit3 = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles3, (256 + nqt3 - 1) / nqt3));
+    part.P = 4 * nsplit3;
+    const size_t n3 = (size_t)nq_pad * part.P * KP;
+    VS_HIP(scr.alloc((void**)&part.key, n3 * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, n3 * sizeof(int)), "vs: scratch");
+    // query planes: a self-join's queries are stored rows, whose planes the index
+    // already holds (rows up to the capacity slack are zero); searches split theirs
+    const uint16_t* qp;
+    int64_t qstride;
+    const float* rows = (const float*)idx->codes;
+    if (qbuf >= rows && qbuf < rows + idx->capacity * idx->ld) {
+      qp = idx->planes + (qbuf - rows);
+      qstride = idx->capacity * idx->ld;
+    } else {
+      uint16_t* t = nullptr;
+      qstride = (int64_t)nq_pad * idx->ld;
+      VS_HIP(scr.alloc((void**)&t, (size_t)3 * qstride * sizeof(uint16_t)), "vs: scratch");
+      VS_HIP(launch_split_planes(qbuf, idx->ld, 0, nq_pad, t, qstride, st), "vs: query planes");
+      qp = t;
+    }
+    KernelTimer tm(st, "gemm_topk_x3");
+    VS_HIP(launch_gemm_topk_x3(KP, mode, idx->planes, idx->capacity * idx->ld, xaux, qp, qstride,
+                               qaux, idx->ld, ntotal, nq_pad, nsplit3, self0, part, st),
+           "vs: gemm_topk_x3 launch");
+    tm.stop();
+    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+           "vs: merge launch");
+    return VS_OK;
+  }
+
   const int nqt = nq_pad / kBQ;
   const int ntiles = (ntotal + kBN - 1) / kBN;
   // ~2 workgroups per CU on 256 CUs; never more splits than database tiles.
@@ -320,6 +410,7 @@ int vs_destroy(vs_index* idx) {
   {
     DeviceGuard g(idx->device);
     (void)hipDeviceSynchronize();
+    drop_planes(idx);
     if (idx->codes) (void)hipFree(idx->codes);
     if (idx->norms) (void)hipFree(idx->norms);
   }
@@ -432,6 +523,7 @@ int vs_reset(vs_index* idx) {
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
   VS_HIP(hipDeviceSynchronize(), "vs_reset");
+  drop_planes(idx);
   if (idx->codes) (void)hipFree(idx->codes);
   if (idx->norms) (void)hipFree(idx->norms);
   idx->codes = nullptr;
@@ -462,6 +554,15 @@ int vs_metric(const vs_index* idx, int* out) {
 int vs_dtype(const vs_index* idx, int* out) {
   if (!idx || !out) return fail(VS_E_INVALID, "vs_dtype: null argument");
   *out = idx->dtype;
+  return VS_OK;
+}
+
+int vs_set_engine(vs_index* idx, int engine) {
+  if (!idx) return fail(VS_E_INVALID, "vs_set_engine: null index");
+  if (engine != VS_ENGINE_AUTO && engine != VS_ENGINE_FP32_MFMA && engine != VS_ENGINE_BF16X3)
+    return fail(VS_E_INVALID, "vs_set_engine: unknown engine");
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  idx->engine = engine;
   return VS_OK;
 }
 
@@ -648,6 +749,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
     }
   }
   const int64_t nt = idx->ntotal - nrem;
+  idx->planes_rows = std::min(idx->planes_rows, first);  // rows from `first` on moved
   VS_HIP(hipMemsetAsync(idx->row(nt), 0, (size_t)nrem * idx->rowbytes(), st),
          "vs_remove_ids: zero tail");
   VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),

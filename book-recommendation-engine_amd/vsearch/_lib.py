@@ -22,6 +22,9 @@ DTYPE_BF16 = 1
 IN_DEVICE = 1
 OUT_DEVICE = 2
 MAX_K = 64
+ENGINE_AUTO = 0
+ENGINE_FP32_MFMA = 1
+ENGINE_BF16X3 = 2
 
 E_INVALID = -1
 E_HIP = -2
@@ -51,6 +54,7 @@ SIGNATURES = {
     "vs_metric": (_c_int, [_vp, ctypes.POINTER(_c_int)]),
     "vs_dtype": (_c_int, [_vp, ctypes.POINTER(_c_int)]),
     "vs_set_id_base": (_c_int, [_vp, _c_i64]),
+    "vs_set_engine": (_c_int, [_vp, _c_int]),
     "vs_search": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
     "vs_reconstruct_n": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp]),
     "vs_remove_ids": (_c_int, [_vp, _vp, _c_i64, _i64p]),

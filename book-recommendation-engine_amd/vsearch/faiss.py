@@ -189,6 +189,13 @@ class IndexFlat(Index):
                                            ctypes.byref(nrem)), "vs_remove_ids")
         return int(nrem.value)
 
+    def set_engine(self, engine: str) -> None:
+        """Large-batch arithmetic of fp32 indexes: "auto", "fp32" (fp32 MFMA) or
+        "bf16x3" (fp32-accurate 3-plane bf16 split on the bf16 matrix cores)."""
+        code = {"auto": _lib.ENGINE_AUTO, "fp32": _lib.ENGINE_FP32_MFMA,
+                "bf16x3": _lib.ENGINE_BF16X3}[engine]
+        _lib.check(self._lib.vs_set_engine(self._h, code), "vs_set_engine")
+
     def set_id_base(self, base: int) -> None:
         _lib.check(self._lib.vs_set_id_base(self._h, int(base)), "vs_set_id_base")
 

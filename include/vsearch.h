@@ -99,6 +99,19 @@ int vs_dim(const vs_index* idx, int* out);
 int vs_metric(const vs_index* idx, int* out);
 int vs_dtype(const vs_index* idx, int* out);
 
+/* Arithmetic engine of the large-batch path of fp32 indexes:
+ *   VS_ENGINE_AUTO       library default (currently BF16X3; env VS_ENGINE=fp32|bf16x3)
+ *   VS_ENGINE_FP32_MFMA  v_mfma_f32_32x32x2_f32 on the fp32 rows
+ *   VS_ENGINE_BF16X3     v_mfma_f32_32x32x16_bf16 on an exact 3-plane bf16 split of
+ *                        every fp32 value (hi+mid+lo == v), 6 products per term
+ *                        (dropped terms < 2^-24 |x q|): fp32-accurate, 2.7x the
+ *                        fp32 matrix rate; costs 6 extra bytes per stored element
+ * bf16 indexes ignore it. */
+#define VS_ENGINE_AUTO 0
+#define VS_ENGINE_FP32_MFMA 1
+#define VS_ENGINE_BF16X3 2
+int vs_set_engine(vs_index* idx, int engine);
+
 /* Rows [0,ntotal) get labels id_base + row.  Used by the row-sharded multi-GPU
  * index so that per-shard results carry global faiss labels. */
 int vs_set_id_base(vs_index* idx, int64_t id_base);

@@ -362,3 +362,106 @@ def test_small_batch_ragged_rows(vf, metric):
         xb = _rand(n, 64, 32)
         for nq in (3, 20):
             _check(vf, xb, _rand(nq, 64, 33), 8, metric)
+
+
+@pytest.mark.parametrize("engine", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_large_batch_engines(vf, engine, metric):
+    """Both large-batch engines of fp32 indexes meet the fp32 tolerance."""
+    xb = _rand(9000, 1536, 40) * 0.05
+    xq = _rand(300, 1536, 41) * 0.05
+    index = vf.IndexFlat(1536, metric)
+    index.set_engine(engine)
+    index.add(xb)
+    for k in (1, 10, 32):
+        D, I = index.search(xq, k)
+        Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        assert not bad, (engine, k, bad[:5])
+
+
+def test_bf16x3_planes_follow_mutations(vf):
+    """The lazily built bf16 planes track add / remove_ids / reset."""
+    xb = _rand(3000, 96, 42)
+    xq = _rand(150, 96, 43)
+    index = vf.IndexFlatIP(96)
+    index.set_engine("bf16x3")
+    index.add(xb[:2000])
+    D, I = index.search(xq, 10)  # builds planes for 2000 rows
+    index.add(xb[2000:])  # planes now stale for the tail
+    D, I = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+    rm = np.arange(100, 3000, 3, dtype=np.int64)
+    index.remove_ids(rm)
+    xr, _ = flat.remove_ids(xb, rm)
+    D, I = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xr, xq, 10, IP)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xr, xq)
+    index.reset()
+    index.add(xb[:50])
+    D, I = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xb[:50], xq, 10, IP)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq)
+
+
+@pytest.mark.parametrize("engine", ["fp32", "bf16x3"])
+def test_selfjoin_engines(vf, engine):
+    x = _rand(2000, 256, 44)
+    index = vf.IndexFlatIP(256)
+    index.set_engine(engine)
+    index.add(x)
+    S, I = index.selfjoin(15)
+    Sr, Ir = flat.pgvector_cosine_topk(x, 15)
+    diff = I != Ir
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
+    np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_bf16x3_ragged_shapes(vf, metric):
+    """Odd d (column padding), ragged row tiles and several query tiles per split."""
+    for n, d, nq in ((5000, 100, 1000), (257, 1536, 129), (70001, 32, 256)):
+        xb = _rand(n, d, 45)
+        xq = _rand(nq, d, 46)
+        index = vf.IndexFlat(d, metric)
+        index.set_engine("bf16x3")
+        index.add(xb)
+        D, I = index.search(xq, 7)
+        Dr, Ir = flat.knn_exact(xb, xq, 7, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        assert not bad, (n, d, nq, bad[:5])
+
+
+def test_bf16x3_repeatable(vf):
+    """Race screen for the 4-buffer LDS-DMA pipeline: repeated launches over a
+    corpus large enough to keep every CU busy give identical, correct lists."""
+    xb = _rand(120000, 256, 47)
+    xq = _rand(640, 256, 48)
+    index = vf.IndexFlatIP(256)
+    index.set_engine("bf16x3")
+    index.add(xb)
+    D0, I0 = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    assert not flat.mismatches(D0, I0, Dr, Ir, IP, xb, xq)
+    for _ in range(6):
+        D, I = index.search(xq, 10)
+        np.testing.assert_array_equal(I, I0)
+        np.testing.assert_array_equal(D, D0)
+
+
+def test_bf16x3_selfjoin_offsets(vf):
+    """Self-join query tiles taken from the index's own planes at an offset, with
+    and without self exclusion."""
+    x = _rand(3000, 128, 49)
+    index = vf.IndexFlatIP(128)
+    index.set_engine("bf16x3")
+    index.add(x)
+    Sr, Ir = flat.pgvector_cosine_topk(x, 12)
+    S, I = index.selfjoin(12, q0=1000, nq=700)
+    diff = I != Ir[1000:1700]
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[1000 + q, j]) - float(S[q, j])) < 1e-5
+    S2, I2 = index.selfjoin(12, q0=5, nq=300, exclude_self=False)
+    assert (I2[:, 0] == np.arange(5, 305)).mean() > 0.99  # a row is its own best match
