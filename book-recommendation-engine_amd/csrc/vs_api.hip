@@ -162,7 +162,7 @@ bool ensure_planes(vs_index* idx, hipStream_t st) {
     // rows up to the capacity slack are zero in codes, so splitting them keeps zeros
     if (launch_split_planes((const float*)idx->codes, idx->ld, idx->planes_rows,
                             idx->ntotal - idx->planes_rows, idx->planes,
-                            idx->capacity * idx->ld, st) != hipSuccess)
+                            idx->capacity * idx->ld, 256, st) != hipSuccess)
       return false;
     idx->planes_rows = idx->ntotal;
   }
@@ -302,32 +302,37 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   int engine = idx->engine != VS_ENGINE_AUTO ? idx->engine : engine_from_env();
   if (engine == VS_ENGINE_AUTO) engine = VS_ENGINE_BF16X3;
   if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KP <= 32 && ensure_planes(idx, st)) {
-    const int nqt3 = nq_pad / 128;
+    X3Args a;
+    a.nq_pad = (int)round_up(nq_pad, kX3Q);
+    const int nqt3 = a.nq_pad / kX3Q;
     const int ntiles3 = (ntotal + 255) / 256;
-    // one 8-wave workgroup per CU on 256 CUs
-    const int nsplit3 = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles3, (256 + nqt3 - 1) / nqt3));
-    part.P = 4 * nsplit3;
-    const size_t n3 = (size_t)nq_pad * part.P * KP;
+    // one 4-wave workgroup per CU on 256 CUs
+    a.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles3, (256 + nqt3 - 1) / nqt3));
+    part.P = 2 * a.nsplit;
+    const size_t n3 = (size_t)a.nq_pad * part.P * KP;
     VS_HIP(scr.alloc((void**)&part.key, n3 * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, n3 * sizeof(int)), "vs: scratch");
-    // query planes: a self-join's queries are stored rows, whose planes the index
-    // already holds (rows up to the capacity slack are zero); searches split theirs
-    const uint16_t* qp;
-    int64_t qstride;
-    const float* rows = (const float*)idx->codes;
-    if (qbuf >= rows && qbuf < rows + idx->capacity * idx->ld) {
-      qp = idx->planes + (qbuf - rows);
-      qstride = idx->capacity * idx->ld;
-    } else {
-      uint16_t* t = nullptr;
-      qstride = (int64_t)nq_pad * idx->ld;
-      VS_HIP(scr.alloc((void**)&t, (size_t)3 * qstride * sizeof(uint16_t)), "vs: scratch");
-      VS_HIP(launch_split_planes(qbuf, idx->ld, 0, nq_pad, t, qstride, st), "vs: query planes");
-      qp = t;
-    }
+    // query planes (self-join queries are stored rows: split from the fp32 rows
+    // too); rows past nq_pad stay zero
+    uint16_t* qp = nullptr;
+    a.qstride = (int64_t)a.nq_pad * idx->ld;
+    VS_HIP(scr.alloc((void**)&qp, (size_t)3 * a.qstride * sizeof(uint16_t)), "vs: scratch");
+    if (a.nq_pad > nq_pad)
+      VS_HIP(hipMemsetAsync(qp, 0, (size_t)3 * a.qstride * sizeof(uint16_t), st),
+             "vs: query planes");
+    VS_HIP(launch_split_planes(qbuf, idx->ld, 0, nq_pad, qp, a.qstride, 256, st),
+           "vs: query planes");
+    a.XP = idx->planes;
+    a.pstride = idx->capacity * idx->ld;
+    a.xaux = xaux;
+    a.QP = qp;
+    a.qaux = qaux;
+    a.nqa = nq_pad;
+    a.ld = idx->ld;
+    a.ntotal = ntotal;
+    a.self0 = self0;
     KernelTimer tm(st, "gemm_topk_x3");
-    VS_HIP(launch_gemm_topk_x3(KP, mode, idx->planes, idx->capacity * idx->ld, xaux, qp, qstride,
-                               qaux, idx->ld, ntotal, nq_pad, nsplit3, self0, part, st),
+    VS_HIP(launch_gemm_topk_x3(KP, mode, a, part, st),
            "vs: gemm_topk_x3 launch");
     tm.stop();
     VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),

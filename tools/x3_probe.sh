@@ -1,11 +1,14 @@
 #!/bin/bash
-# Builds diagnostic variants of libvsearch.so (VS_X3_PROBE=1: no MFMA, 2: no
-# staging loads) next to the real one, for load-path vs MFMA-path attribution.
+# Builds timing-only diagnostic variants of libvsearch.so next to the real one
+# (results are wrong by design):  _pN = VS_X3_PROBE=N (see vs_gemm_x3.hip).
 set -e
 cd "$(dirname "$0")/../book-recommendation-engine_amd/csrc"
-for p in 1 2; do
-  mkdir -p build_p$p
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -DVS_X3_PROBE=$p -c vs_gemm_x3.hip -o build_p$p/vs_gemm_x3.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../vsearch/libvsearch_p$p.so \
-    build/vs_api.o build/vs_gemm.o build_p$p/vs_gemm_x3.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
-done
+build() {  # <suffix> <defines...>
+  local sfx=$1; shift
+  mkdir -p build$sfx
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c vs_gemm_x3.hip -o build$sfx/vs_gemm_x3.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../vsearch/libvsearch$sfx.so \
+    build/vs_api.o build/vs_gemm.o build$sfx/vs_gemm_x3.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
+}
+for p in ${PROBES:-1 2 3 4 5}; do build _p$p -DVS_X3_PROBE=$p & done
+wait
