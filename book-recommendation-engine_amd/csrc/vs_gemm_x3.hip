@@ -34,7 +34,8 @@
 
 // Diagnostic builds only (tools/x3_probe.sh; timing only, results are wrong):
 // 1 = no MFMA, 2 = no staging loads, 3 = no vmcnt wait, 4 = no stage barrier,
-// 5 = neither.
+// 5 = neither, 6 = database planes only, 7 = query planes only, 8 = every load
+// from tile 0 (L2-resident).
 #ifndef VS_X3_PROBE
 #define VS_X3_PROBE 0
 #endif
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_topk_x3(
   // of 256 rows x 32 B, so every fetched line is used whole.
   const int srow = lane >> 1;
   const uint32_t loff = (uint32_t)srow * kRowB + (uint32_t)swz32(srow, lane & 1) * 16u;
-  const char* qbase = (const char*)(QP + (int64_t)qt * nstage * kXQ * 16);
+  const char* qbase = (const char*)(QP + (int64_t)(VS_X3_PROBE == 8 ? 0 : qt) * nstage * kXQ * 16);
   const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
   const int fsw = (c32 >> 3) & 1;  // fragment rows 32*i + c32 share (row >> 3) & 1
   const int coff = (h ^ fsw) * 16;
@@ -211,12 +212,14 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_topk_x3(
   // fragment reads the MFMAs wait on.
   auto issue_one = [&](int v) {
     if (VS_X3_PROBE == 2) return;
+    if (VS_X3_PROBE == 6 && (v & 1)) return;
+    if (VS_X3_PROBE == 7 && !(v & 1)) return;
     const uint32_t base = lds0 + (uint32_t)(ibuf * kBufB);
     const int u = v >> 1;
     const int p = u / NJ;
     const int grp = NJ * w + u % NJ;
     if ((v & 1) == 0) {
-      const char* xb = (const char*)(XP + (int64_t)it * nstage * kXN * 16);
+      const char* xb = (const char*)(XP + (int64_t)(VS_X3_PROBE == 8 ? 0 : it) * nstage * kXN * 16);
       glds16(xb + (int64_t)p * pstride * 2 + ist * kXPlaneB + grp * 1024 + loff,
              __builtin_amdgcn_readfirstlane(base + p * kXPlaneB + grp * 1024));
     } else {
