@@ -209,19 +209,34 @@ def base_result(args, ctx, value, elapsed, unit="queries/s"):
     }
 
 
-def roofline(kind, achieved, launches, mean_s, per_launch, kernel, traffic, traffic_src):
+def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src):
+    """Roofline record of the dominant kernel over the timed region.
+
+    work_total  algorithmic FLOP (MFMA kinds) or bytes (hbm) of all timed steps
+    kms, nl     summed HIP-event time (ms) of those launches and their dispatch
+                count (gemm_topk_x3 cuts one search into several dispatches)
+    achieved = work_total / kernel time = work per dispatch / mean dispatch time,
+    the figure rocprofv3's per-kernel average duration reproduces."""
     if kind == "mfma32":
-        peak, unit, bound = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
+        peak, unit, bound, scale = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma", 1e12
     elif kind == "mfma16":
-        peak, unit, bound = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
+        peak, unit, bound, scale = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma", 1e12
     elif kind == "mfma_x3":
-        peak, unit, bound = round(X3_PEAK_TFLOPS, 3), "TFLOP/s", "mfma"
+        peak, unit, bound, scale = round(X3_PEAK_TFLOPS, 3), "TFLOP/s", "mfma", 1e12
     else:
-        peak, unit, bound = HBM_PEAK_GBS, "GB/s", "hbm"
+        peak, unit, bound, scale = HBM_PEAK_GBS, "GB/s", "hbm", 1e9
+    secs = kms / 1e3
+    achieved = work_total / secs / scale if secs > 0 else 0.0
+    nl = max(1, nl)
     r = {"bound": bound, "kernel": kernel, "achieved": round(achieved, 3), "peak": peak,
          "unit": unit, "frac": round(achieved / peak, 4) if peak else None,
          "traffic": traffic,
-         "per_launch": f"{per_launch}; mean launch {mean_s * 1e3:.3f} ms over {launches} launches"}
+         "per_launch": f"{unit_desc}; {work_total / nl:.4g} "
+                       f"{'FLOP' if bound == 'mfma' else 'B'} per dispatch, "
+                       f"mean dispatch {kms / nl:.3f} ms over {nl} dispatches"}
+    if traffic is not None:
+        r["traffic_note"] = ("PMC HBM bytes per dispatch (2*FETCH_SIZE + WRITE_SIZE, "
+                             "gfx950 correction; Infinity-Cache hits included)")
     if kind == "mfma_x3":
         r["peak_note"] = ("fp32 FLOP on the bf16 matrix cores via the exact 3-plane split "
                           "(6 bf16 MFMA products per fp32 product): 2500/6 TFLOP/s; "
@@ -251,19 +266,18 @@ def run_knn(args, ctx):
     sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
     sane &= bool((np.diff(Dh, axis=1) <= 0).all() if metric == vfaiss.METRIC_INNER_PRODUCT
                  else (np.diff(Dh, axis=1) >= 0).all())
-    mean_s = kms / max(1, nl) / 1e3
     flops = 2.0 * n_shard * d * B
     esz = 4 if args.dtype == "f32" else 2
     kname = ctx.lib.timer_kernel()
     gemv = kname in HBM_KERNELS  # the small-batch kernels are HBM-bound
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     if gemv:
-        rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
-                      f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
+        rf = roofline("hbm", n_shard * d * esz * args.steps, kms, nl,
+                      f"{n_shard}*{d}*{esz} B per search (batch {B} over the rank's shard)",
                       kname, traffic, tsrc)
     else:
-        rf = roofline(mfma_kind(kname, esz), flops / mean_s / 1e12, nl, mean_s,
-                      f"2*{n_shard}*{d}*{B} FLOP (one launch = whole batch over the rank's shard)",
+        rf = roofline(mfma_kind(kname, esz), flops * args.steps, kms, nl,
+                      f"2*{n_shard}*{d}*{B} FLOP per search (whole batch over the rank's shard)",
                       kname, traffic, tsrc)
 
     batch1 = None
@@ -323,14 +337,12 @@ def run_selfjoin(args, ctx):
     Ih = I.cpu()
     sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
         (Ih == torch.arange(lo, hi)[:, None]).any())
-    mean_s = kms / max(1, nl) / 1e3
-    flops_total = 2.0 * N * d * nq
+    flops_step = 2.0 * N * d * nq
     kname = ctx.lib.timer_kernel()
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     esz = 4 if args.dtype == "f32" else 2
-    rf = roofline(mfma_kind(kname, esz),
-                  flops_total / (kms / 1e3) / 1e12 if kms > 0 else 0.0, nl, mean_s,
-                  f"2*{N}*{d}*(<=65536 query rows per launch); {nq} query rows per rank per step",
+    rf = roofline(mfma_kind(kname, esz), flops_step * args.steps, kms, nl,
+                  f"2*{N}*{d}*{nq} FLOP per step ({nq} query rows per rank)",
                   kname, traffic, tsrc)
     if ctx.rank == 0:
         res = base_result(args, ctx, args.steps * N / elapsed, elapsed, unit="students/s")
@@ -381,13 +393,12 @@ def run_c5(args, ctx):
 
     elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
     assert index.ntotal == gen.size
-    mean_s = kms / max(1, nl) / 1e3
     n_shard = index.shard.ntotal
     esz = 2 if args.dtype == "bf16" else 4
     kname = ctx.lib.timer_kernel()
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
-    rf = roofline("hbm", n_shard * d * esz / mean_s / 1e9, nl, mean_s,
-                  f"{n_shard}*{d}*{esz} B (one launch = batch {B} over the rank's shard)",
+    rf = roofline("hbm", n_shard * d * esz * args.steps, kms, nl,
+                  f"{n_shard}*{d}*{esz} B per search (batch {B} over the rank's shard)",
                   kname, traffic, tsrc)
     recall = None
     if ctx.world == 1 and args.recall_queries > 0:

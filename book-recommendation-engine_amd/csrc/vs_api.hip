@@ -37,13 +37,13 @@ struct vs_index {
   int64_t rowbytes() const { return ld * esize; }
   char* row(int64_t r) const { return codes + r * rowbytes(); }
   float* norms = nullptr;  // [capacity] squared L2 norms
-  // fp32 indexes: the 3 bf16 planes of every row (hi, mid, lo; exact split) for
-  // the bf16-MFMA fp32-accurate GEMM, derived lazily from `codes`; valid for rows
-  // [0, planes_rows).  [3][capacity][ld].
-  uint16_t* planes = nullptr;
-  int64_t planes_rows = 0;
+  // fp32 indexes: a copy of the rows in the blocked layout the bf16x3 GEMM
+  // streams (vs_gemm_x3.hip), derived lazily from `codes`; valid for rows
+  // [0, blocked_rows).  capacity x ld floats.
+  float* blocked = nullptr;
+  int64_t blocked_rows = 0;
   int engine = VS_ENGINE_AUTO;
-  std::mutex planes_mu;
+  std::mutex blocked_mu;
   std::shared_mutex mu;
 };
 
@@ -101,13 +101,18 @@ struct Scratch {
 // Kernel timer (measurement hook for bench.py; see vs_timer_* in vsearch.h).
 std::mutex g_timer_mu;
 bool g_timer_on = false;
-std::vector<std::pair<hipEvent_t, hipEvent_t>> g_timer_events;
+struct TimedSpan {
+  hipEvent_t a, b;
+  int dispatches;
+};
+std::vector<TimedSpan> g_timer_events;
 
 const char* g_timer_kernel = "";
 
 struct KernelTimer {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;
+  int dispatches = 1;  // kernel launches between the two events
   KernelTimer(hipStream_t s, const char* name) : st(s) {
     {
       std::lock_guard<std::mutex> g(g_timer_mu);
@@ -125,7 +130,7 @@ struct KernelTimer {
     if (!a) return;
     (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_events.emplace_back(a, b);
+    g_timer_events.push_back({a, b, dispatches});
     a = b = nullptr;
   }
 };
@@ -134,37 +139,34 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
 
-void drop_planes(vs_index* idx) {
-  if (idx->planes) (void)hipFree(idx->planes);
-  idx->planes = nullptr;
-  idx->planes_rows = 0;
+void drop_blocked(vs_index* idx) {
+  if (idx->blocked) (void)hipFree(idx->blocked);
+  idx->blocked = nullptr;
+  idx->blocked_rows = 0;
 }
 
-// Makes planes valid for all rows (called under the shared lock; builds are
-// serialised by planes_mu).  Returns false when the planes cannot be allocated
-// (the caller then uses the fp32 MFMA kernel).
-bool ensure_planes(vs_index* idx, hipStream_t st) {
-  std::lock_guard<std::mutex> g(idx->planes_mu);
-  if (!idx->planes) {
-    if (hipMalloc(&idx->planes, (size_t)3 * idx->capacity * idx->ld * sizeof(uint16_t)) !=
-        hipSuccess) {
+// Makes the blocked copy valid for all rows (called under the shared lock;
+// builds are serialised by blocked_mu).  Returns false when it cannot be
+// allocated (the caller then uses the fp32 MFMA kernel).
+bool ensure_blocked(vs_index* idx, hipStream_t st) {
+  std::lock_guard<std::mutex> g(idx->blocked_mu);
+  if (!idx->blocked) {
+    if (hipMalloc(&idx->blocked, (size_t)idx->capacity * idx->ld * sizeof(float)) != hipSuccess) {
       (void)hipGetLastError();
-      idx->planes = nullptr;
+      idx->blocked = nullptr;
       return false;
     }
-    idx->planes_rows = 0;
-    // padding rows must hold zeros, like the fp32 rows
-    if (hipMemsetAsync(idx->planes, 0, (size_t)3 * idx->capacity * idx->ld * sizeof(uint16_t),
-                       st) != hipSuccess)
+    idx->blocked_rows = 0;
+    // padding rows must hold zeros, like the row storage
+    if (hipMemsetAsync(idx->blocked, 0, (size_t)idx->capacity * idx->ld * sizeof(float), st) !=
+        hipSuccess)
       return false;
   }
-  if (idx->planes_rows < idx->ntotal) {
-    // rows up to the capacity slack are zero in codes, so splitting them keeps zeros
-    if (launch_split_planes((const float*)idx->codes, idx->ld, idx->planes_rows,
-                            idx->ntotal - idx->planes_rows, idx->planes,
-                            idx->capacity * idx->ld, 256, st) != hipSuccess)
+  if (idx->blocked_rows < idx->ntotal) {
+    if (launch_block_rows((const float*)idx->codes, idx->ld, idx->blocked_rows,
+                          idx->ntotal - idx->blocked_rows, idx->blocked, st) != hipSuccess)
       return false;
-    idx->planes_rows = idx->ntotal;
+    idx->blocked_rows = idx->ntotal;
   }
   return true;
 }
@@ -213,7 +215,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   }
   // In-flight searches (any stream) may still read the old storage.
   VS_HIP(hipDeviceSynchronize(), "vs: storage growth");
-  drop_planes(idx);  // rebuilt lazily at the new capacity
+  drop_blocked(idx);  // rebuilt lazily at the new capacity
   if (idx->codes) (void)hipFree(idx->codes);
   if (idx->norms) (void)hipFree(idx->norms);
   idx->codes = codes;
@@ -298,32 +300,29 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
 
   // fp32 indexes run the large-batch GEMM on the bf16 matrix cores through the
   // exact 3-plane split (vs_gemm_x3.hip) unless disabled (VS_ENGINE=fp32 /
-  // vs_set_engine) or the planes do not fit in HBM.
+  // vs_set_engine) or the blocked copy of the rows does not fit in HBM.
   int engine = idx->engine != VS_ENGINE_AUTO ? idx->engine : engine_from_env();
   if (engine == VS_ENGINE_AUTO) engine = VS_ENGINE_BF16X3;
-  if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KP <= 32 && ensure_planes(idx, st)) {
+  const int KR = x3_list_len(mode == MODE_IP ? std::min(2 * k - 1, VS_MAX_K) : k);
+  if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KR > 0 && ensure_blocked(idx, st)) {
     X3Args a;
     a.nq_pad = (int)round_up(nq_pad, kX3Q);
     const int nqt3 = a.nq_pad / kX3Q;
-    const int ntiles3 = (ntotal + 255) / 256;
-    // one 4-wave workgroup per CU on 256 CUs
+    const int ntiles3 = (ntotal + kX3Q - 1) / kX3Q;
+    // one 8-wave workgroup per CU on 256 CUs
     a.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles3, (256 + nqt3 - 1) / nqt3));
     part.P = 2 * a.nsplit;
     const size_t n3 = (size_t)a.nq_pad * part.P * KP;
     VS_HIP(scr.alloc((void**)&part.key, n3 * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, n3 * sizeof(int)), "vs: scratch");
-    // query planes (self-join queries are stored rows: split from the fp32 rows
-    // too); rows past nq_pad stay zero
-    uint16_t* qp = nullptr;
-    a.qstride = (int64_t)a.nq_pad * idx->ld;
-    VS_HIP(scr.alloc((void**)&qp, (size_t)3 * a.qstride * sizeof(uint16_t)), "vs: scratch");
-    if (a.nq_pad > nq_pad)
-      VS_HIP(hipMemsetAsync(qp, 0, (size_t)3 * a.qstride * sizeof(uint16_t), st),
-             "vs: query planes");
-    VS_HIP(launch_split_planes(qbuf, idx->ld, 0, nq_pad, qp, a.qstride, 256, st),
-           "vs: query planes");
-    a.XP = idx->planes;
-    a.pstride = idx->capacity * idx->ld;
+    // query planes (self-join queries are stored rows, split the same way);
+    // rows past nq_pad stay zero
+    uint4* qp = nullptr;
+    const size_t qpb = (size_t)3 * a.nq_pad * idx->ld * sizeof(uint16_t);
+    VS_HIP(scr.alloc((void**)&qp, qpb), "vs: scratch");
+    if (a.nq_pad > nq_pad) VS_HIP(hipMemsetAsync(qp, 0, qpb, st), "vs: query planes");
+    VS_HIP(launch_split_queries(qbuf, idx->ld, nq_pad, a.nq_pad, qp, st), "vs: query planes");
+    a.XB = idx->blocked;
     a.xaux = xaux;
     a.QP = qp;
     a.qaux = qaux;
@@ -332,7 +331,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     a.ntotal = ntotal;
     a.self0 = self0;
     KernelTimer tm(st, "gemm_topk_x3");
-    VS_HIP(launch_gemm_topk_x3(KP, mode, a, part, st),
+    VS_HIP(launch_gemm_topk_x3(KR, mode, a, part, st, &tm.dispatches),
            "vs: gemm_topk_x3 launch");
     tm.stop();
     VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
@@ -415,7 +414,7 @@ int vs_destroy(vs_index* idx) {
   {
     DeviceGuard g(idx->device);
     (void)hipDeviceSynchronize();
-    drop_planes(idx);
+    drop_blocked(idx);
     if (idx->codes) (void)hipFree(idx->codes);
     if (idx->norms) (void)hipFree(idx->norms);
   }
@@ -528,7 +527,7 @@ int vs_reset(vs_index* idx) {
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
   VS_HIP(hipDeviceSynchronize(), "vs_reset");
-  drop_planes(idx);
+  drop_blocked(idx);
   if (idx->codes) (void)hipFree(idx->codes);
   if (idx->norms) (void)hipFree(idx->norms);
   idx->codes = nullptr;
@@ -754,7 +753,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
     }
   }
   const int64_t nt = idx->ntotal - nrem;
-  idx->planes_rows = std::min(idx->planes_rows, first);  // rows from `first` on moved
+  idx->blocked_rows = std::min(idx->blocked_rows, first);  // rows from `first` on moved
   VS_HIP(hipMemsetAsync(idx->row(nt), 0, (size_t)nrem * idx->rowbytes(), st),
          "vs_remove_ids: zero tail");
   VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),
@@ -845,8 +844,8 @@ int vs_timer_enable(int on) {
 int vs_timer_reset(void) {
   std::lock_guard<std::mutex> g(g_timer_mu);
   for (auto& p : g_timer_events) {
-    (void)hipEventDestroy(p.first);
-    (void)hipEventDestroy(p.second);
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
   }
   g_timer_events.clear();
   return VS_OK;
@@ -861,14 +860,16 @@ int vs_timer_read(double* total_ms, int64_t* launches) {
   if (!total_ms || !launches) return fail(VS_E_INVALID, "vs_timer_read: null output");
   std::lock_guard<std::mutex> g(g_timer_mu);
   double tot = 0.0;
+  int64_t n = 0;
   for (auto& p : g_timer_events) {
-    VS_HIP(hipEventSynchronize(p.second), "vs_timer_read: synchronise");
+    VS_HIP(hipEventSynchronize(p.b), "vs_timer_read: synchronise");
     float ms = 0.0f;
-    VS_HIP(hipEventElapsedTime(&ms, p.first, p.second), "vs_timer_read: elapsed");
+    VS_HIP(hipEventElapsedTime(&ms, p.a, p.b), "vs_timer_read: elapsed");
     tot += ms;
+    n += p.dispatches;
   }
   *total_ms = tot;
-  *launches = (int64_t)g_timer_events.size();
+  *launches = n;
   return VS_OK;
 }
 

@@ -63,28 +63,35 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,
                               int ntotal, int nblocks, Partials part, hipStream_t st);
-// fp32-accurate GEMM path on bf16 MFMA (3-plane split, vs_gemm_x3.hip).
+// fp32-accurate GEMM path on bf16 MFMA (in-kernel exact 3-plane split,
+// vs_gemm_x3.hip).  Database and query rows in the blocked fp32 layout.
 struct X3Args {
-  const uint16_t* XP = nullptr;  // database planes [3][pstride], K-blocked 256-row tiles
-  int64_t pstride = 0;
-  const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
-  const uint16_t* QP = nullptr;  // query planes [3][qstride], K-blocked 256-row tiles
-  int64_t qstride = 0;
-  const float* qaux = nullptr;   // per-query aux, nqa entries (padding queries read 0)
+  const float* XB = nullptr;    // database rows, blocked (capacity rows)
+  const float* xaux = nullptr;  // per-row norms (L2) or 1/|x| (COS)
+  const uint4* QP = nullptr;    // query planes (launch_split_queries, nq_pad rows)
+  const float* qaux = nullptr;  // per-query aux, nqa entries (padding queries read 0)
   int nqa = 0;
   int64_t ld = 0;
   int ntotal = 0;
-  int nq_pad = 0;                // multiple of kX3Q
+  int nq_pad = 0;               // multiple of kX3Q
   int nsplit = 1;
   int64_t self0 = -1;
 };
-constexpr int kX3Q = 256;  // queries per x3 tile
-// Writes 2*nsplit lists per query (nq_pad queries).  KP <= 32.
-hipError_t launch_gemm_topk_x3(int KP, int mode, const X3Args& a, Partials part, hipStream_t st);
-// Builds the 3 bf16 planes of fp32 rows [r0, r0+n) in the K-blocked layout of
-// tile_rows-row tiles (256 for index and query planes; vs_gemm_x3.hip).
-hipError_t launch_split_planes(const float* X, int64_t ld, int64_t r0, int64_t n, uint16_t* XP,
-                               int64_t pstride, int tile_rows, hipStream_t st);
+constexpr int kX3Q = 256;  // queries (and database rows) per x3 tile
+// Register list length for `need` entries (8, 12, 16, 20 or 24; 0 = too long).
+int x3_list_len(int need);
+// Writes 2*nsplit lists of part.KP entries per query (nq_pad queries): KR register
+// entries (KR <= 24) padded with empty slots.  *ndispatch = kernel launches used.
+hipError_t launch_gemm_topk_x3(int KR, int mode, const X3Args& a, Partials part, hipStream_t st,
+                               int* ndispatch);
+// Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's query planes
+// (3 x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
+hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, uint4* QP,
+                                hipStream_t st);
+// Copies fp32 rows [r0, r0+n) (stride ld, a multiple of 16) into the blocked
+// layout of 256-row tiles the x3 GEMM streams (vs_gemm_x3.hip).
+hipError_t launch_block_rows(const float* X, int64_t ld, int64_t r0, int64_t n, float* XB,
+                             hipStream_t st);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,

@@ -165,12 +165,13 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
  * When enabled, every launch of the dominant search kernel (the fused
  * distance+top-k kernel) is bracketed by HIP events on the launch stream.
  * vs_timer_read synchronises those events and returns the summed kernel time in
- * milliseconds and the launch count since the last reset. */
+ * milliseconds and the number of kernel dispatches inside the timed spans since
+ * the last reset (gemm_topk_x3 cuts one search into several dispatches). */
 int vs_timer_enable(int on);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
-/* Name of the fused search kernel the last search launched ("gemm_topk",
- * "skinny_topk" or "gemv_topk"). */
+/* Name of the fused search kernel the last search launched ("gemm_topk_x3",
+ * "gemm_topk", "skinny_topk" or "gemv_topk"). */
 const char* vs_timer_kernel(void);
 
 #ifdef __cplusplus

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../book-recommendation-engine_amd/csrc"
 build() {  # <suffix> <defines...>
   local sfx=$1; shift
   mkdir -p build$sfx
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c vs_gemm_x3.hip -o build$sfx/vs_gemm_x3.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize "$@" -c vs_gemm_x3.hip -o build$sfx/vs_gemm_x3.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../vsearch/libvsearch$sfx.so \
     build/vs_api.o build/vs_gemm.o build$sfx/vs_gemm_x3.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
 }
