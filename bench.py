@@ -53,9 +53,16 @@ X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 HBM_KERNELS = ("gemv_topk", "skinny_topk")
 
 
+# gemm_topk_x2f (the filter pass of the bf16x2v engine) computes 3 bf16 products
+# per fp32 product: its fp32-equivalent ceiling is the bf16 peak / 3.
+X2F_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3.0
+
+
 def mfma_kind(kname: str, esz: int) -> str:
     if kname == "gemm_topk_x3":
         return "mfma_x3"
+    if kname == "gemm_topk_x2f":
+        return "mfma_x2f"
     return "mfma32" if esz == 4 else "mfma16"
 
 DEFAULTS = {
@@ -223,6 +230,8 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
         peak, unit, bound, scale = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma", 1e12
     elif kind == "mfma_x3":
         peak, unit, bound, scale = round(X3_PEAK_TFLOPS, 3), "TFLOP/s", "mfma", 1e12
+    elif kind == "mfma_x2f":
+        peak, unit, bound, scale = round(X2F_PEAK_TFLOPS, 3), "TFLOP/s", "mfma", 1e12
     else:
         peak, unit, bound, scale = HBM_PEAK_GBS, "GB/s", "hbm", 1e9
     secs = kms / 1e3
@@ -237,6 +246,10 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
     if traffic is not None:
         r["traffic_note"] = ("PMC HBM bytes per dispatch (2*FETCH_SIZE + WRITE_SIZE, "
                              "gfx950 correction; Infinity-Cache hits included)")
+    if kind == "mfma_x2f":
+        r["peak_note"] = ("filter pass of the bf16x2v engine: 3 bf16 MFMA products (hi/mid "
+                          "planes) per fp32 product, 2500/3 TFLOP/s; candidates are then "
+                          "rescored exactly and verified against a rigorous error bound")
     if kind == "mfma_x3":
         r["peak_note"] = ("fp32 FLOP on the bf16 matrix cores via the exact 3-plane split "
                           "(6 bf16 MFMA products per fp32 product): 2500/6 TFLOP/s; "
@@ -260,8 +273,10 @@ def run_knn(args, ctx):
     B, d, k = args.batch, args.d, args.k
     xq = ctx.queries(B, d)
 
+    ctx.lib.filter_stats(reset=True)
     elapsed, kms, nl, (D, I) = ctx.timed(
         lambda i: index.search_device(xq, k, stream=ctx.stream), args.steps, args.warmup)
+    fq, ff = ctx.lib.filter_stats(reset=True)
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
     sane &= bool((np.diff(Dh, axis=1) <= 0).all() if metric == vfaiss.METRIC_INNER_PRODUCT
@@ -269,6 +284,19 @@ def run_knn(args, ctx):
     flops = 2.0 * n_shard * d * B
     esz = 4 if args.dtype == "f32" else 2
     kname = ctx.lib.timer_kernel()
+    exact_check = None
+    if kname == "gemm_topk_x2f":
+        # the same queries through the exact 6-product engine: ids must agree
+        # (the verify step makes the filter engine exact; this re-checks it live)
+        nchk = min(B, 256)
+        index.shard.set_engine("bf16x3")
+        De, Ie = index.search_device(xq[:nchk].contiguous(), k, stream=ctx.stream)
+        index.shard.set_engine("auto")
+        De, Ie = De.cpu().numpy(), Ie.cpu().numpy()
+        rows = int((Ie != Ih[:nchk]).any(axis=1).sum())
+        exact_check = {"queries": nchk, "engine": "bf16x3", "rows_with_id_mismatch": rows,
+                       "max_abs_score_diff": float(np.abs(De - Dh[:nchk]).max())}
+        sane &= rows == 0
     gemv = kname in HBM_KERNELS  # the small-batch kernels are HBM-bound
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     if gemv:
@@ -306,6 +334,9 @@ def run_knn(args, ctx):
             "parallelism": f"row-shard x{ctx.world} + RCCL all-gather top-k merge",
             "kernel": kname}
         res["roofline"] = rf
+        if fq:
+            res["filter_verify"] = {"queries": fq, "fallback_queries": ff,
+                                    "fallback_rate": round(ff / fq, 6), "exact_check": exact_check}
         res["batch1"] = batch1
         res["cpu_baseline"] = cpu
         res["result_sane"] = sane

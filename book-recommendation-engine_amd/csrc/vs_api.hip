@@ -108,6 +108,9 @@ struct TimedSpan {
 std::vector<TimedSpan> g_timer_events;
 
 const char* g_timer_kernel = "";
+// filter-and-verify statistics (vs_filter_stats)
+int64_t g_filter_queries = 0;
+int64_t g_filter_fallbacks = 0;
 
 struct KernelTimer {
   hipEvent_t a = nullptr, b = nullptr;
@@ -176,6 +179,7 @@ int engine_from_env() {
   if (!e) return VS_ENGINE_AUTO;
   if (strcmp(e, "fp32") == 0) return VS_ENGINE_FP32_MFMA;
   if (strcmp(e, "bf16x3") == 0) return VS_ENGINE_BF16X3;
+  if (strcmp(e, "bf16x2v") == 0) return VS_ENGINE_BF16X2_VERIFY;
   return VS_ENGINE_AUTO;
 }
 
@@ -224,11 +228,144 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   return VS_OK;
 }
 
+int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
+             int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
+             hipStream_t st, const float* xaux, int force_engine);
+
+// The filter-and-verify engine (vs_gemm_x3.hip): an NP = 2 pass keeps the KF
+// best approximate candidates of every query, verify_rescore_kernel proves the
+// exact top-`need` is among them (or flags the query), rescores them exactly and
+// the usual merge emits (D, I).  Flagged queries are redone by the exact engine.
+int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq,
+                      int nq_pad, int k, int need, int KF, float min_score, float* D, int64_t* I,
+                      hipStream_t st, const float* xaux) {
+  const int ntotal = (int)idx->ntotal;
+  Scratch scr(st);
+  X3Args a;
+  a.nq_pad = (int)round_up(nq_pad, kX3Q);
+  const int nqt = a.nq_pad / kX3Q;
+  const int ntiles = (ntotal + kX3Q - 1) / kX3Q;
+  a.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
+  Partials part;
+  part.KP = 32;
+  part.P = 2 * a.nsplit;
+  const size_t np_ = (size_t)a.nq_pad * part.P * part.KP;
+  VS_HIP(scr.alloc((void**)&part.key, np_ * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&part.id, np_ * sizeof(int)), "vs: scratch");
+  uint4* qp = nullptr;
+  const size_t qpb = (size_t)2 * a.nq_pad * idx->ld * sizeof(uint16_t);
+  VS_HIP(scr.alloc((void**)&qp, qpb), "vs: scratch");
+  if (a.nq_pad > nq_pad) VS_HIP(hipMemsetAsync(qp, 0, qpb, st), "vs: query planes");
+  VS_HIP(launch_split_queries(qbuf, idx->ld, nq_pad, a.nq_pad, 2, qp, st), "vs: query planes");
+  // |q|^2 (L2 searches stage it in qaux already) and max |x|^2 for the bound
+  const float* qn = qaux;
+  if (mode != MODE_L2) {
+    float* t = nullptr;
+    VS_HIP(scr.alloc((void**)&t, (size_t)nq_pad * sizeof(float)), "vs: scratch");
+    VS_HIP(launch_row_norms(qbuf, 4, idx->ld, 0, nq_pad, t, st), "vs: query norms");
+    qn = t;
+  }
+  unsigned* xmax2 = nullptr;
+  VS_HIP(scr.alloc((void**)&xmax2, sizeof(unsigned)), "vs: scratch");
+  VS_HIP(launch_max_norm(idx->norms, ntotal, xmax2, st), "vs: max norm");
+  a.XB = idx->blocked;
+  a.xaux = xaux;
+  a.QP = qp;
+  a.qaux = qaux;
+  a.nqa = nq_pad;
+  a.ld = idx->ld;
+  a.ntotal = ntotal;
+  a.self0 = -1;
+  {
+    KernelTimer tm(st, "gemm_topk_x2f");
+    VS_HIP(launch_gemm_topk_x3(KF, mode, 2, a, part, st, &tm.dispatches),
+           "vs: gemm_topk_x2f launch");
+    tm.stop();
+  }
+  // approximate top-KF per query (plain lexicographic order: the L2 merge)
+  float* Dk = nullptr;
+  int64_t* Ik = nullptr;
+  VS_HIP(scr.alloc((void**)&Dk, (size_t)nq * KF * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&Ik, (size_t)nq * KF * sizeof(int64_t)), "vs: scratch");
+  VS_HIP(launch_merge_partials(MODE_L2, part, nq, KF, 0, 0.0f, Dk, Ik, KF, st), "vs: merge");
+  Partials vp;
+  vp.KP = 32;
+  vp.P = 1;
+  int* fail_d = nullptr;
+  VS_HIP(scr.alloc((void**)&vp.key, (size_t)nq * vp.KP * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&vp.id, (size_t)nq * vp.KP * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&fail_d, (size_t)nq * sizeof(int)), "vs: scratch");
+  VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
+                               qbuf, qn, idx->ld, x2f_bound_coef(idx->ld), xmax2, vp.key, vp.id,
+                               vp.KP, fail_d, st),
+         "vs: verify");
+  VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st),
+         "vs: merge");
+  // queries the bound could not settle: the exact engine (rare)
+  std::vector<int> fh(nq);
+  VS_HIP(hipMemcpyAsync(fh.data(), fail_d, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st),
+         "vs: verify flags");
+  VS_HIP(hipStreamSynchronize(st), "vs: verify flags");
+  std::vector<int> F;
+  for (int q = 0; q < nq; ++q)
+    if (fh[q]) F.push_back(q);
+  {
+    std::lock_guard<std::mutex> g(g_timer_mu);
+    g_filter_queries += nq;
+    g_filter_fallbacks += (int64_t)F.size();
+  }
+  if (F.empty()) return VS_OK;
+  const int nf = (int)F.size();
+  const int nf_pad = (int)round_up(std::max(nf, kGemvMaxQ), kBQ) + kBQ;  // chunk tails
+  float* q2 = nullptr;
+  float* a2 = nullptr;
+  float* D2 = nullptr;
+  int64_t* I2 = nullptr;
+  VS_HIP(scr.alloc((void**)&q2, (size_t)nf_pad * idx->ld * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&a2, (size_t)nf_pad * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&D2, (size_t)nf * k * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&I2, (size_t)nf * k * sizeof(int64_t)), "vs: scratch");
+  VS_HIP(hipMemsetAsync(q2, 0, (size_t)nf_pad * idx->ld * sizeof(float), st), "vs: fallback");
+  VS_HIP(hipMemsetAsync(a2, 0, (size_t)nf_pad * sizeof(float), st), "vs: fallback");
+  for (int i = 0; i < nf; ++i) {
+    VS_HIP(hipMemcpyAsync(q2 + (int64_t)i * idx->ld, qbuf + (int64_t)F[i] * idx->ld,
+                          (size_t)idx->ld * sizeof(float), hipMemcpyDeviceToDevice, st),
+           "vs: fallback");
+    if (mode == MODE_L2)
+      VS_HIP(hipMemcpyAsync(a2 + i, qaux + F[i], sizeof(float), hipMemcpyDeviceToDevice, st),
+             "vs: fallback");
+  }
+  // a few queries: 16 at a time through the small-batch kernels (one corpus
+  // stream each); more: one exact-engine launch
+  const int step = nf <= 64 ? 16 : nf;
+  for (int f0 = 0; f0 < nf; f0 += step) {
+    const int nc = std::min(step, nf - f0);
+    const int nc_pad = (int)round_up(std::max(nc, kGemvMaxQ), kBQ);
+    int rc = run_topk(idx, mode, q2 + (int64_t)f0 * idx->ld, nullptr, a2 + f0, nc, nc_pad, k, -1,
+                      min_score, D2 + (int64_t)f0 * k, I2 + (int64_t)f0 * k, st, xaux,
+                      VS_ENGINE_BF16X3);
+    if (rc) return rc;
+  }
+  {
+    std::lock_guard<std::mutex> g(g_timer_mu);
+    g_timer_kernel = "gemm_topk_x2f";  // the fallback is part of this engine's search
+  }
+  for (int i = 0; i < nf; ++i) {
+    VS_HIP(hipMemcpyAsync(D + (int64_t)F[i] * k, D2 + (int64_t)i * k, (size_t)k * sizeof(float),
+                          hipMemcpyDeviceToDevice, st),
+           "vs: fallback");
+    VS_HIP(hipMemcpyAsync(I + (int64_t)F[i] * k, I2 + (int64_t)i * k, (size_t)k * sizeof(int64_t),
+                          hipMemcpyDeviceToDevice, st),
+           "vs: fallback");
+  }
+  return VS_OK;
+}
+
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
 // zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
 int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
              int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
-             hipStream_t st, const float* xaux) {
+             hipStream_t st, const float* xaux, int force_engine = VS_ENGINE_AUTO) {
   // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
   // lowest 2k-1 (key, label) entries of every partial list to be exact.
   const int KP = mode == MODE_IP ? kp_for(std::min(2 * k - 1, VS_MAX_K)) : kp_for(k);
@@ -301,9 +438,19 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   // fp32 indexes run the large-batch GEMM on the bf16 matrix cores through the
   // exact 3-plane split (vs_gemm_x3.hip) unless disabled (VS_ENGINE=fp32 /
   // vs_set_engine) or the blocked copy of the rows does not fit in HBM.
-  int engine = idx->engine != VS_ENGINE_AUTO ? idx->engine : engine_from_env();
-  if (engine == VS_ENGINE_AUTO) engine = VS_ENGINE_BF16X3;
-  const int KR = x3_list_len(mode == MODE_IP ? std::min(2 * k - 1, VS_MAX_K) : k);
+  int engine = force_engine != VS_ENGINE_AUTO ? force_engine
+               : idx->engine != VS_ENGINE_AUTO ? idx->engine
+                                               : engine_from_env();
+  // entries of each partial list the final merge needs (faiss's IP tie rule: 2k-1)
+  const int need = mode == MODE_IP ? std::min(2 * k - 1, VS_MAX_K) : k;
+  const int KF = x2f_list_len(need);
+  if (engine == VS_ENGINE_AUTO) engine = KF > 0 ? VS_ENGINE_BF16X2_VERIFY : VS_ENGINE_BF16X3;
+  if (engine == VS_ENGINE_BF16X2_VERIFY && (KF == 0 || self0 >= 0 || mode == MODE_COS))
+    engine = VS_ENGINE_BF16X3;
+  if (idx->esize == 4 && engine == VS_ENGINE_BF16X2_VERIFY && ensure_blocked(idx, st))
+    return run_filter_verify(idx, mode, qbuf, qaux, nq, nq_pad, k, need, KF, min_score, D, I, st,
+                             xaux);
+  const int KR = x3_list_len(need);
   if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KR > 0 && ensure_blocked(idx, st)) {
     X3Args a;
     a.nq_pad = (int)round_up(nq_pad, kX3Q);
@@ -321,7 +468,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     const size_t qpb = (size_t)3 * a.nq_pad * idx->ld * sizeof(uint16_t);
     VS_HIP(scr.alloc((void**)&qp, qpb), "vs: scratch");
     if (a.nq_pad > nq_pad) VS_HIP(hipMemsetAsync(qp, 0, qpb, st), "vs: query planes");
-    VS_HIP(launch_split_queries(qbuf, idx->ld, nq_pad, a.nq_pad, qp, st), "vs: query planes");
+    VS_HIP(launch_split_queries(qbuf, idx->ld, nq_pad, a.nq_pad, 3, qp, st), "vs: query planes");
     a.XB = idx->blocked;
     a.xaux = xaux;
     a.QP = qp;
@@ -331,7 +478,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     a.ntotal = ntotal;
     a.self0 = self0;
     KernelTimer tm(st, "gemm_topk_x3");
-    VS_HIP(launch_gemm_topk_x3(KR, mode, a, part, st, &tm.dispatches),
+    VS_HIP(launch_gemm_topk_x3(KR, mode, 3, a, part, st, &tm.dispatches),
            "vs: gemm_topk_x3 launch");
     tm.stop();
     VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
@@ -563,7 +710,8 @@ int vs_dtype(const vs_index* idx, int* out) {
 
 int vs_set_engine(vs_index* idx, int engine) {
   if (!idx) return fail(VS_E_INVALID, "vs_set_engine: null index");
-  if (engine != VS_ENGINE_AUTO && engine != VS_ENGINE_FP32_MFMA && engine != VS_ENGINE_BF16X3)
+  if (engine != VS_ENGINE_AUTO && engine != VS_ENGINE_FP32_MFMA && engine != VS_ENGINE_BF16X3 &&
+      engine != VS_ENGINE_BF16X2_VERIFY)
     return fail(VS_E_INVALID, "vs_set_engine: unknown engine");
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   idx->engine = engine;
@@ -832,6 +980,15 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
   if (!out) return fail(VS_E_INVALID, "vs_fill_synthetic: null output");
   VS_HIP(launch_fill_synthetic(out, 4, rows, d, d, seed, row0, (hipStream_t)stream),
          "vs_fill_synthetic: launch");
+  return VS_OK;
+}
+
+int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
+  if (!queries || !fallbacks) return fail(VS_E_INVALID, "vs_filter_stats: null output");
+  std::lock_guard<std::mutex> g(g_timer_mu);
+  *queries = g_filter_queries;
+  *fallbacks = g_filter_fallbacks;
+  if (reset) g_filter_queries = g_filter_fallbacks = 0;
   return VS_OK;
 }
 

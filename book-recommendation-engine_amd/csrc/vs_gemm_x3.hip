@@ -44,6 +44,8 @@
 // piece of a contiguous KiB, and holds k = 8i + 4h + e in MFMA slot 4i + e — the
 // same K permutation on both operands, so the dot product is unchanged.
 #include <algorithm>
+#include <climits>
+#include <cmath>
 #include <cstdlib>
 
 #include "vs_device.h"
@@ -62,10 +64,11 @@ constexpr int kT = 256;                   // database rows (and queries) per til
 constexpr int kKB = 16;                   // K elements per stage
 constexpr int kChunkF = kT * kKB;         // floats per (tile, K-block) chunk: 4096
 constexpr int kPlaneB = kT * 32;          // one bf16 plane of one stage: 8 KB
-constexpr int kStageB = 3 * kPlaneB;      // 24 KB
 constexpr int kNBuf = 2;
 constexpr int kSparkB = 8 * 16 * 64 * 4;  // epilogue parking, 4 KB per wave
-constexpr int kLdsB = kNBuf * kStageB + kSparkB;
+// NP planes per operand: 3 = exact split, 2 = hi/mid only (the filter pass)
+template <int NP>
+constexpr int lds_bytes() { return kNBuf * NP * kPlaneB + kSparkB; }
 constexpr int kX3ChunkTiles = 16;         // database tiles per workgroup per launch
 
 // 32-B LDS rows hold 2 chunks of 16 B; chunk c of row r is stored at
@@ -82,23 +85,25 @@ __device__ __forceinline__ uint32_t cvt_pk(float a, float b) {  // v_cvt_pk_bf16
 __device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
 
-// Splits 8 floats (two 16-B pieces) into three planes of 8 bf16 (16 B each).
-__device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, uint4& hi, uint4& mid,
-                                       uint4& lo) {
+// Splits 8 floats (two 16-B pieces) into the first NP planes of 8 bf16 (16 B
+// each): hi, mid, lo.
+template <int NP>
+__device__ __forceinline__ void split_planes(const f32x4& a, const f32x4& b, uint4 (&pl)[NP]) {
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  uint32_t hh[4], mm[4], ll[4];
+  uint32_t w[3][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float x0 = v[2 * i], x1 = v[2 * i + 1];
-    hh[i] = cvt_pk(x0, x1);
-    const float r0 = x0 - bf16_lo(hh[i]), r1 = x1 - bf16_hi(hh[i]);
-    mm[i] = cvt_pk(r0, r1);
-    const float s0 = r0 - bf16_lo(mm[i]), s1 = r1 - bf16_hi(mm[i]);
-    ll[i] = cvt_pk(s0, s1);
+    w[0][i] = cvt_pk(x0, x1);
+    const float r0 = x0 - bf16_lo(w[0][i]), r1 = x1 - bf16_hi(w[0][i]);
+    w[1][i] = cvt_pk(r0, r1);
+    if constexpr (NP == 3) {
+      const float s0 = r0 - bf16_lo(w[1][i]), s1 = r1 - bf16_hi(w[1][i]);
+      w[2][i] = cvt_pk(s0, s1);
+    }
   }
-  hi = make_uint4(hh[0], hh[1], hh[2], hh[3]);
-  mid = make_uint4(mm[0], mm[1], mm[2], mm[3]);
-  lo = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) pl[p] = make_uint4(w[p][0], w[p][1], w[p][2], w[p][3]);
 }
 
 // Publishes this wave's LDS writes and waits for every wave: raw s_barrier (no
@@ -113,13 +118,14 @@ __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_c
 
 }  // namespace
 
-template <int KR, int MODE>
+template <int KR, int MODE, int NP>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x3(
     const float* __restrict__ XB, const float* __restrict__ xaux, const uint4* __restrict__ QP,
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
     int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
     int* __restrict__ pid) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // kLdsB
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // lds_bytes<NP>()
+  constexpr int kStageB = NP * kPlaneB;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -191,64 +197,60 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x3(
         ++lt;
       }
     };
-    auto load_q = [&](int kb, uint4& q0, uint4& q1, uint4& q2) {
+    auto load_q = [&](int kb, uint4 (&q)[NP]) {
       const uint4* p = qsrc + (int64_t)kb * 512;
-      q0 = p[0];
-      q1 = p[qpl];
-      q2 = p[2 * qpl];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) q[j] = p[j * qpl];
     };
     auto write_x = [&](int buf, const f32x4& r0, const f32x4& r1) {
-      uint4 p0, p1, p2;
-      split3(r0, r1, p0, p1, p2);
+      uint4 pl[NP];
+      split_planes<NP>(r0, r1, pl);
       char* base = smem + buf * kStageB + woff;
-      *(uint4*)(base) = p0;
-      *(uint4*)(base + kPlaneB) = p1;
-      *(uint4*)(base + 2 * kPlaneB) = p2;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) *(uint4*)(base + j * kPlaneB) = pl[j];
     };
 
     // One stage: MFMAs over the image of `buf` with query planes qc*, while
     // stage+1's query planes load into qn*, stage+2's database slice into xn*,
     // and stage+1's database slice (xc*) is split into the other image.
-    auto stage = [&](f32x16 (&acc)[8], int buf, int kb_next, const uint4& qc0, const uint4& qc1,
-                     const uint4& qc2, uint4& qn0, uint4& qn1, uint4& qn2, const f32x4& xc0,
-                     const f32x4& xc1, f32x4& xn0, f32x4& xn1) {
+    auto stage = [&](f32x16 (&acc)[8], int buf, int kb_next, const uint4 (&qc)[NP],
+                     uint4 (&qn)[NP], const f32x4& xc0, const f32x4& xc1, f32x4& xn0,
+                     f32x4& xn1) {
       lds_barrier();  // this stage's image is complete; the previous one is free
       if (VS_X3_PROBE != 2) {
-        load_q(kb_next, qn0, qn1, qn2);
+        load_q(kb_next, qn);
         load_x(xn0, xn1);
       }
       const char* cb = smem + buf * kStageB + roff;
-      uint4 x0 = *(const uint4*)(cb), x1 = *(const uint4*)(cb + kPlaneB),
-            x2 = *(const uint4*)(cb + 2 * kPlaneB);
+      uint4 x[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) x[j] = *(const uint4*)(cb + j * kPlaneB);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const char* nb = cb + (i + 1) * 32 * 32;
         f32x16 a = acc[i];
-        // the six products above 2^-24; each fragment register is refilled with
-        // the next row block's fragment right after its last use
-        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x0), as_bf(qc0), a, 0, 0, 0);
-        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x0), as_bf(qc1), a, 0, 0, 0);
-        if (VS_X3_PROBE != 9)
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x0), as_bf(qc2), a, 0, 0, 0);
-        if (i < 7) x0 = *(const uint4*)(nb);
-        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x1), as_bf(qc0), a, 0, 0, 0);
-        if (VS_X3_PROBE != 9)
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x1), as_bf(qc1), a, 0, 0, 0);
-        if (i < 7) x1 = *(const uint4*)(nb + kPlaneB);
-        if (VS_X3_PROBE != 9)
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x2), as_bf(qc0), a, 0, 0, 0);
-        if (i < 7) x2 = *(const uint4*)(nb + 2 * kPlaneB);
+        // the products x_j q_l with j + l < NP (all six above 2^-24 for the exact
+        // split; hh, hm, mh for the filter); each fragment register is refilled
+        // with the next row block's fragment right after its last use
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+#pragma unroll
+          for (int l = 0; l + j < NP; ++l)
+            if (VS_X3_PROBE != 9 || j + l < 2)
+              a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(x[j]), as_bf(qc[l]), a, 0, 0, 0);
+          if (i < 7) x[j] = *(const uint4*)(nb + j * kPlaneB);
+        }
         acc[i] = a;
       }
       write_x(buf ^ 1, xc0, xc1);
     };
 
-    uint4 qa0, qa1, qa2, qb0, qb1, qb2;  // query planes, two stages
-    f32x4 xa0, xa1, xb0, xb1;            // raw database slices, two stages
+    uint4 qpa[NP], qpb[NP];      // query planes, two stages
+    f32x4 xa0, xa1, xb0, xb1;    // raw database slices, two stages
     // prologue: stage 0's image and query planes, stage 1's slice in flight
     f32x4 x00, x01;
     load_x(x00, x01);
-    load_q(0, qa0, qa1, qa2);
+    load_q(0, qpa);
     load_x(xa0, xa1);
     write_x(0, x00, x01);
 
@@ -264,8 +266,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x3(
       // slices alternate between the a and b registers, so no copies are needed
       for (int st = 0; st < nkb; st += 2) {
         const int k1 = st + 1, k2 = st + 2 == nkb ? 0 : st + 2;
-        stage(acc, 0, k1, qa0, qa1, qa2, qb0, qb1, qb2, xa0, xa1, xb0, xb1);
-        stage(acc, 1, k2, qb0, qb1, qb2, qa0, qa1, qa2, xb0, xb1, xa0, xa1);
+        stage(acc, 0, k1, qpa, qpb, xa0, xa1, xb0, xb1);
+        stage(acc, 1, k2, qpb, qpa, xb0, xb1, xa0, xa1);
       }
 
       // Epilogue (one 32-row block at a time): keys, a 16-bit candidate mask
@@ -330,12 +332,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x3(
   }
 }
 
-template <int KR, int MODE>
+template <int KR, int MODE, int NP>
 static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int* ndispatch) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_topk_x3<KR, MODE>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsB);
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_topk_x3<KR, MODE, NP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       lds_bytes<NP>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -350,9 +353,10 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   for (int c = 0; c < nchunk; ++c) {
-    hipLaunchKernelGGL((gemm_topk_x3<KR, MODE>), dim3(nqt * a.nsplit), dim3(512), kLdsB, st,
-                       a.XB, a.xaux, a.QP, a.qaux, a.nqa, (int)(a.ld / kKB), a.ntotal, ntiles,
-                       a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    hipLaunchKernelGGL((gemm_topk_x3<KR, MODE, NP>), dim3(nqt * a.nsplit), dim3(512),
+                       lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, (int)(a.ld / kKB),
+                       a.ntotal, ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key,
+                       part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -360,48 +364,253 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   return hipSuccess;
 }
 
+// Exact split (NP = 3): every list length, IP / L2 / COS.  Filter pass (NP = 2):
+// IP and L2 with the list lengths x2f_list_len returns.
 template <int KR>
-static hipError_t x3_dispatch(int mode, const X3Args& a, Partials part, hipStream_t st,
+static hipError_t x3_dispatch(int mode, int np, const X3Args& a, Partials part, hipStream_t st,
                               int* ndispatch) {
-  switch (mode) {
-    case MODE_IP:
-      return x3_launch<KR, MODE_IP>(a, part, st, ndispatch);
-    case MODE_L2:
-      return x3_launch<KR, MODE_L2>(a, part, st, ndispatch);
-    case MODE_COS:
-      return x3_launch<KR, MODE_COS>(a, part, st, ndispatch);
-    default:
-      return hipErrorInvalidValue;
+  if (np == 3 && KR <= 24) {
+    switch (mode) {
+      case MODE_IP:
+        return x3_launch<KR, MODE_IP, 3>(a, part, st, ndispatch);
+      case MODE_L2:
+        return x3_launch<KR, MODE_L2, 3>(a, part, st, ndispatch);
+      case MODE_COS:
+        return x3_launch<KR, MODE_COS, 3>(a, part, st, ndispatch);
+      default:
+        return hipErrorInvalidValue;
+    }
   }
+  if constexpr (KR == 24 || KR == 32) {
+    if (np == 2) {
+      switch (mode) {
+        case MODE_IP:
+          return x3_launch<KR, MODE_IP, 2>(a, part, st, ndispatch);
+        case MODE_L2:
+          return x3_launch<KR, MODE_L2, 2>(a, part, st, ndispatch);
+        default:
+          break;
+      }
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 // Longer lists do not fit the register file beside the 128 accumulators (KR=32
-// spills ~100 registers into the K loop): those searches take the fp32 engine.
+// spills ~100 registers into the K loop of the exact split): those searches take
+// the fp32 engine.
 int x3_list_len(int need) {
   return need <= 8 ? 8 : need <= 12 ? 12 : need <= 16 ? 16 : need <= 20 ? 20 : need <= 24 ? 24 : 0;
 }
 
-hipError_t launch_gemm_topk_x3(int KR, int mode, const X3Args& a, Partials part, hipStream_t st,
-                               int* ndispatch) {
+// Filter pass list length for `need` exact entries: a margin of at least 8
+// approximate candidates beyond the entries the merge needs (0 = unsupported).
+int x2f_list_len(int need) { return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : 0; }
+
+hipError_t launch_gemm_topk_x3(int KR, int mode, int np, const X3Args& a, Partials part,
+                               hipStream_t st, int* ndispatch) {
   // ld % 32: an even number of K-blocks per tile keeps the LDS image parity of a
   // stage equal to its K-block parity across tiles
   if (a.nq_pad % kT != 0 || a.ld % (2 * kKB) != 0 || KR > part.KP || part.P != 2 * a.nsplit ||
-      a.nsplit < 1)
+      a.nsplit < 1 || (np != 2 && np != 3))
     return hipErrorInvalidValue;
   switch (KR) {
     case 8:
-      return x3_dispatch<8>(mode, a, part, st, ndispatch);
+      return x3_dispatch<8>(mode, np, a, part, st, ndispatch);
     case 12:
-      return x3_dispatch<12>(mode, a, part, st, ndispatch);
+      return x3_dispatch<12>(mode, np, a, part, st, ndispatch);
     case 16:
-      return x3_dispatch<16>(mode, a, part, st, ndispatch);
+      return x3_dispatch<16>(mode, np, a, part, st, ndispatch);
     case 20:
-      return x3_dispatch<20>(mode, a, part, st, ndispatch);
+      return x3_dispatch<20>(mode, np, a, part, st, ndispatch);
     case 24:
-      return x3_dispatch<24>(mode, a, part, st, ndispatch);
+      return x3_dispatch<24>(mode, np, a, part, st, ndispatch);
+    case 32:
+      return x3_dispatch<32>(mode, np, a, part, st, ndispatch);
     default:
       return hipErrorInvalidValue;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Filter-and-verify (engine VS_ENGINE_BF16X2_VERIFY).  The NP = 2 pass scores
+// every row with hh + hm + mh; the dropped terms and the fp32 accumulation are
+// bounded by  |approx_key - exact_key| <= Bkey  (from coef * |x| * |q|, coef =
+// x2f_bound_coef).  Let a = the sorted approximate keys of the KF best
+// candidates of a query and E = their exact keys, sorted; the M-th entry E[M-1]
+// bounds the true M-th best exact key from above (M candidates reach it).  Every
+// row outside the candidate set has approx key >= a[KF-1], so exact key >=
+// a[KF-1] - Bkey; whenever
+//     a[KF-1] - Bkey > E[M-1]
+// those rows are strictly worse than the true M-th entry, and the exact top-M
+// (ties included) is E's first M entries.  verify_rescore_kernel rescores the
+// candidates exactly (fp64 accumulation of the fp32 products, rounded to fp32),
+// sorts them and checks the condition; queries that fail it are flagged for
+// the exact engine.
+
+// Bound coefficient for `ld` K elements: the three dropped product classes of
+// each term (hl, lh, mm: <= 3 * 2^-16 (1 + 2^-8)^2 |x_k q_k|, the rest < 2^-23),
+// plus the accumulation of 3*ld products whose every step may be off by one
+// ulp (u = 2^-23, which also covers truncating adders):
+// gamma = n u / (1 - n u) on sum |products| <= 1.0235 sum |x_k q_k| <= 1.0235 |x||q|.
+double x2f_bound_coef(int64_t ld) {
+  const double u = std::ldexp(1.0, -23);
+  const double n = 3.0 * (double)ld + 1.0;
+  const double gamma = n * u / (1.0 - n * u);
+  const double drop = 3.0 * std::ldexp(1.0, -16) * (1.0 + std::ldexp(1.0, -8)) *
+                          (1.0 + std::ldexp(1.0, -8)) +
+                      std::ldexp(1.0, -23);
+  return (drop + gamma * 1.0235) * (1.0 + 1e-6);
+}
+
+__global__ __launch_bounds__(256) void max_norm_kernel(const float* __restrict__ norms, int64_t n,
+                                                       unsigned* __restrict__ out) {
+  unsigned m = 0;  // non-negative floats (and NaN, above them) order as their bits
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = max(m, __float_as_uint(norms[i]) & 0x7FFFFFFFu);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+hipError_t launch_max_norm(const float* norms, int64_t n, unsigned* out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned), st);
+  if (e != hipSuccess || n <= 0) return e;
+  const int64_t blocks = std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(max_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, norms, n, out);
+  return hipGetLastError();
+}
+
+// One wave per query.  Dk/Ik: the KF best approximate keys (ascending) and local
+// rows of each query; X/xn: fp32 rows (stride ld) and squared norms; Q/qn: query
+// rows and squared norms.  Writes a sorted list of KF exact (key, row) entries,
+// padded to KP, and fail[q].
+template <int MODE>
+__global__ __launch_bounds__(64) void verify_rescore_kernel(
+    int KF, int M, const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
+    const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
+    const float* __restrict__ qn, int64_t ld, double coef, const unsigned* __restrict__ xmax2,
+    float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail) {
+  __shared__ float ek[64];
+  const int lane = threadIdx.x;
+  const int q = blockIdx.x;
+  const float a = lane < KF ? Dk[(int64_t)q * KF + lane] : FLT_MAX;
+  const int id = lane < KF ? (int)Ik[(int64_t)q * KF + lane] : -1;
+  const float aK = __shfl(a, KF - 1);
+  const int idK = __shfl(id, KF - 1);
+
+  // exact keys, one candidate at a time across the wave
+  const float* qrow = Q + (int64_t)q * ld;
+  for (int j = 0; j < KF; ++j) {
+    const int r = __shfl(id, j);
+    if (r < 0) {
+      if (lane == 0) ek[j] = FLT_MAX;
+      continue;
+    }
+    const float* xr = X + (int64_t)r * ld;
+    double acc = 0.0;
+    for (int64_t c = lane * 4; c < ld; c += 256) {
+      const f32x4 xv = *(const f32x4*)(xr + c);
+      const f32x4 qv = *(const f32x4*)(qrow + c);
+      acc = fma((double)xv.x, (double)qv.x, acc);
+      acc = fma((double)xv.y, (double)qv.y, acc);
+      acc = fma((double)xv.z, (double)qv.z, acc);
+      acc = fma((double)xv.w, (double)qv.w, acc);
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      const float ip = (float)acc;
+      ek[j] = MODE == MODE_L2 ? l2_from_ip(qn[q], xn[r], ip) : -ip;
+    }
+  }
+  __syncthreads();
+  // rank sort of (key, row); empty slots last, in lane order among themselves
+  const float k0 = lane < KF ? ek[lane] : FLT_MAX;
+  const int i0 = id < 0 ? INT_MAX : id;
+  int rank = 0;
+  for (int j = 0; j < KF; ++j) {
+    const float kj = __shfl(k0, j);
+    const int ij = __shfl(i0, j);
+    rank += (lex_less(kj, ij, k0, i0) || (kj == k0 && ij == i0 && j < lane)) ? 1 : 0;
+  }
+  float* ok = okey + (int64_t)q * KP;
+  int* oi = oid + (int64_t)q * KP;
+  if (lane < KF) {
+    ok[rank] = k0;
+    oi[rank] = id;  // -1 for empty slots
+  } else if (lane < KP) {
+    ok[lane] = FLT_MAX;
+    oi[lane] = -1;
+  }
+  // the M-th exact key (the lane whose rank is M-1 publishes it)
+  if (lane < KF && rank == M - 1) ek[63] = k0;
+  __syncthreads();
+  const float eM = ek[63];
+  const double qn2 = (double)qn[q];
+  const double xm2 = (double)__uint_as_float(*xmax2);
+  double bkey = coef * sqrt(qn2) * sqrt(xm2);
+  if constexpr (MODE == MODE_L2)  // key = (|q|^2 + |x|^2) - 2 ip, each side rounded
+    bkey = 2.0 * bkey + 8.0 * std::ldexp(1.0, -24) * (qn2 + xm2);
+  // a list that is not full holds every admissible row
+  const bool pass = idK < 0 || ((double)aK - bkey > (double)eM && isfinite(aK) && isfinite(eM) &&
+                                isfinite(bkey));
+  if (lane == 0) fail[q] = pass ? 0 : 1;
+}
+
+hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
+                                 const int64_t* Ik, const float* X, const float* xn,
+                                 const float* Q, const float* qn, int64_t ld, double coef,
+                                 const unsigned* xmax2, float* okey, int* oid, int KP, int* fail,
+                                 hipStream_t st) {
+  if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0) return hipErrorInvalidValue;
+  if (nq <= 0) return hipSuccess;
+  if (mode == MODE_IP)
+    hipLaunchKernelGGL(verify_rescore_kernel<MODE_IP>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
+                       X, xn, Q, qn, ld, coef, xmax2, okey, oid, KP, fail);
+  else if (mode == MODE_L2)
+    hipLaunchKernelGGL(verify_rescore_kernel<MODE_L2>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
+                       X, xn, Q, qn, ld, coef, xmax2, okey, oid, KP, fail);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// Splits fp32 query rows [0, n) (stride ld) into the first NP bf16 planes of the
+// MFMA B fragments: uint4 ((p*nqt + r/256)*nkb + kb)*512 + ((r%256)/32)*64 + lane,
+// lane = h*32 + r%32, holding k = 16kb + {4h..4h+3, 8+4h..8+4h+3} (the K
+// permutation of the blocked database rows).  One thread per (row, kb, h).
+template <int NP>
+__global__ __launch_bounds__(256) void split_queries_kernel(const float* __restrict__ Q,
+                                                            int64_t ld, int64_t n, int nqt,
+                                                            uint4* __restrict__ QP) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nkb = ld / kKB;
+  if (p >= n * nkb * 2) return;
+  const int64_t r = p / (nkb * 2);
+  const int64_t kb = (p / 2) % nkb;
+  const int hh = (int)(p & 1);
+  const float* src = Q + r * ld + kb * kKB + 4 * hh;
+  const f32x4 a = *(const f32x4*)src;
+  const f32x4 c = *(const f32x4*)(src + 8);
+  uint4 v[NP];
+  split_planes<NP>(a, c, v);
+  const int64_t o = ((r / kT) * nkb + kb) * 512 + ((r % kT) / 32) * 64 + hh * 32 + r % 32;
+  const int64_t pl = (int64_t)nqt * nkb * 512;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) QP[o + j * pl] = v[j];
+}
+
+hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, int np,
+                                uint4* QP, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ld % kKB != 0 || nq_pad % kT != 0 || n > nq_pad || (np != 2 && np != 3))
+    return hipErrorInvalidValue;
+  const int64_t items = n * (ld / kKB) * 2;
+  const dim3 grid((unsigned)((items + 255) / 256));
+  if (np == 3)
+    hipLaunchKernelGGL(split_queries_kernel<3>, grid, dim3(256), 0, st, Q, ld, n, nq_pad / kT, QP);
+  else
+    hipLaunchKernelGGL(split_queries_kernel<2>, grid, dim3(256), 0, st, Q, ld, n, nq_pad / kT, QP);
+  return hipGetLastError();
 }
 
 // Copies fp32 rows [r0, r0+n) (row-major, stride ld) into the blocked layout
@@ -420,41 +629,6 @@ __global__ __launch_bounds__(256) void block_rows_kernel(const float* __restrict
   const int64_t o =
       (t * (ld / kKB) + bk) * kChunkF + (((i * 8 + rr / 32) * 2 + hh) * 32 + rr % 32) * 4;
   *(f32x4*)(XB + o) = v;
-}
-
-// Splits fp32 query rows [0, n) (stride ld) into the three bf16 planes of the
-// MFMA B fragments: uint4 ((p*nqt + r/256)*nkb + kb)*512 + ((r%256)/32)*64 + lane,
-// lane = h*32 + r%32, holding k = 16kb + {4h..4h+3, 8+4h..8+4h+3} (the K
-// permutation of the blocked database rows).  One thread per (row, kb, h).
-__global__ __launch_bounds__(256) void split_queries_kernel(const float* __restrict__ Q,
-                                                            int64_t ld, int64_t n, int nqt,
-                                                            uint4* __restrict__ QP) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nkb = ld / kKB;
-  if (p >= n * nkb * 2) return;
-  const int64_t r = p / (nkb * 2);
-  const int64_t kb = (p / 2) % nkb;
-  const int hh = (int)(p & 1);
-  const float* src = Q + r * ld + kb * kKB + 4 * hh;
-  const f32x4 a = *(const f32x4*)src;
-  const f32x4 c = *(const f32x4*)(src + 8);
-  uint4 p0, p1, p2;
-  split3(a, c, p0, p1, p2);
-  const int64_t o = ((r / kT) * nkb + kb) * 512 + ((r % kT) / 32) * 64 + hh * 32 + r % 32;
-  const int64_t pl = (int64_t)nqt * nkb * 512;
-  QP[o] = p0;
-  QP[o + pl] = p1;
-  QP[o + 2 * pl] = p2;
-}
-
-hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, uint4* QP,
-                                hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  if (ld % kKB != 0 || nq_pad % kT != 0 || n > nq_pad) return hipErrorInvalidValue;
-  const int64_t items = n * (ld / kKB) * 2;
-  hipLaunchKernelGGL(split_queries_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st,
-                     Q, ld, n, nq_pad / kT, QP);
-  return hipGetLastError();
 }
 
 hipError_t launch_block_rows(const float* X, int64_t ld, int64_t r0, int64_t n, float* XB,

@@ -80,14 +80,30 @@ struct X3Args {
 constexpr int kX3Q = 256;  // queries (and database rows) per x3 tile
 // Register list length for `need` entries (8, 12, 16, 20 or 24; 0 = too long).
 int x3_list_len(int need);
+// Filter pass (NP = 2) list length for `need` exact entries (24 or 32; 0 = too long).
+int x2f_list_len(int need);
 // Writes 2*nsplit lists of part.KP entries per query (nq_pad queries): KR register
-// entries (KR <= 24) padded with empty slots.  *ndispatch = kernel launches used.
-hipError_t launch_gemm_topk_x3(int KR, int mode, const X3Args& a, Partials part, hipStream_t st,
-                               int* ndispatch);
-// Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's query planes
-// (3 x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
-hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, uint4* QP,
-                                hipStream_t st);
+// entries padded with empty slots.  np = 3: exact split (KR <= 24, IP/L2/COS);
+// np = 2: filter pass (KR 24 or 32, IP/L2).  *ndispatch = kernel launches used.
+hipError_t launch_gemm_topk_x3(int KR, int mode, int np, const X3Args& a, Partials part,
+                               hipStream_t st, int* ndispatch);
+// |approx - exact| <= coef * |x| * |q| for the filter pass over ld K elements.
+double x2f_bound_coef(int64_t ld);
+// *out = bits of max(norms[0..n)) (norms >= 0; NaN propagates as the maximum).
+hipError_t launch_max_norm(const float* norms, int64_t n, unsigned* out, hipStream_t st);
+// Checks and rescores the filter candidates (see vs_gemm_x3.hip): Dk/Ik hold the
+// KF best approximate keys of each query (ascending, local rows); writes sorted
+// exact lists of KP entries (okey/oid) and fail[q] = 1 where the exact engine
+// must redo query q.
+hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
+                                 const int64_t* Ik, const float* X, const float* xn,
+                                 const float* Q, const float* qn, int64_t ld, double coef,
+                                 const unsigned* xmax2, float* okey, int* oid, int KP, int* fail,
+                                 hipStream_t st);
+// Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's np query planes
+// (np x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
+hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, int np,
+                                uint4* QP, hipStream_t st);
 // Copies fp32 rows [r0, r0+n) (stride ld, a multiple of 16) into the blocked
 // layout of 256-row tiles the x3 GEMM streams (vs_gemm_x3.hip).
 hipError_t launch_block_rows(const float* X, int64_t ld, int64_t r0, int64_t n, float* XB,

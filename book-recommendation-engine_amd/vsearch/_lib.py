@@ -25,6 +25,7 @@ MAX_K = 64
 ENGINE_AUTO = 0
 ENGINE_FP32_MFMA = 1
 ENGINE_BF16X3 = 2
+ENGINE_BF16X2_VERIFY = 3
 
 E_INVALID = -1
 E_HIP = -2
@@ -71,6 +72,7 @@ SIGNATURES = {
     "vs_timer_reset": (_c_int, []),
     "vs_timer_read": (_c_int, [ctypes.POINTER(ctypes.c_double), _i64p]),
     "vs_timer_kernel": (ctypes.c_char_p, []),
+    "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
 }
 
 _lock = threading.Lock()
@@ -172,3 +174,12 @@ def timer_read():
     n = _c_i64(0)
     check(load().vs_timer_read(ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+def filter_stats(reset: bool = False):
+    """(queries searched by the filter-and-verify engine, queries the exact
+    engine redid) since the last reset."""
+    q = ctypes.c_int64(0)
+    f = ctypes.c_int64(0)
+    check(load().vs_filter_stats(ctypes.byref(q), ctypes.byref(f), 1 if reset else 0))
+    return q.value, f.value

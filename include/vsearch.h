@@ -100,16 +100,24 @@ int vs_metric(const vs_index* idx, int* out);
 int vs_dtype(const vs_index* idx, int* out);
 
 /* Arithmetic engine of the large-batch path of fp32 indexes:
- *   VS_ENGINE_AUTO       library default (currently BF16X3; env VS_ENGINE=fp32|bf16x3)
+ *   VS_ENGINE_AUTO       library default: BF16X2_VERIFY where it applies (IP/L2
+ *                        searches needing <= 24 list entries), else BF16X3;
+ *                        env VS_ENGINE=fp32|bf16x3|bf16x2v overrides
  *   VS_ENGINE_FP32_MFMA  v_mfma_f32_32x32x2_f32 on the fp32 rows
  *   VS_ENGINE_BF16X3     v_mfma_f32_32x32x16_bf16 on an exact 3-plane bf16 split of
  *                        every fp32 value (hi+mid+lo == v), 6 products per term
  *                        (dropped terms < 2^-24 |x q|): fp32-accurate, 2.7x the
- *                        fp32 matrix rate; costs 6 extra bytes per stored element
+ *                        fp32 matrix rate; keeps a blocked fp32 copy of the rows
+ *   VS_ENGINE_BF16X2_VERIFY  filter and verify: a 3-product pass (hi/mid planes)
+ *                        keeps 24-32 candidates per query, a rigorous error bound
+ *                        proves the exact top-k is among them, and the candidates
+ *                        are rescored exactly; queries the bound cannot settle are
+ *                        redone by BF16X3 — results identical to an exact engine
  * bf16 indexes ignore it. */
 #define VS_ENGINE_AUTO 0
 #define VS_ENGINE_FP32_MFMA 1
 #define VS_ENGINE_BF16X3 2
+#define VS_ENGINE_BF16X2_VERIFY 3
 int vs_set_engine(vs_index* idx, int engine);
 
 /* Rows [0,ntotal) get labels id_base + row.  Used by the row-sharded multi-GPU
@@ -168,10 +176,13 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
  * milliseconds and the number of kernel dispatches inside the timed spans since
  * the last reset (gemm_topk_x3 cuts one search into several dispatches). */
 int vs_timer_enable(int on);
+/* Queries searched by the filter-and-verify engine and how many of them the
+ * exact engine had to redo, since the last reset (reset != 0 clears them). */
+int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
-/* Name of the fused search kernel the last search launched ("gemm_topk_x3",
- * "gemm_topk", "skinny_topk" or "gemv_topk"). */
+/* Name of the fused search kernel the last search launched ("gemm_topk_x2f",
+ * "gemm_topk_x3", "gemm_topk", "skinny_topk" or "gemv_topk"). */
 const char* vs_timer_kernel(void);
 
 #ifdef __cplusplus

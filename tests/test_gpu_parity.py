@@ -364,10 +364,10 @@ def test_small_batch_ragged_rows(vf, metric):
             _check(vf, xb, _rand(nq, 64, 33), 8, metric)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("engine", ["fp32", "bf16x3", "bf16x2v"])
 @pytest.mark.parametrize("metric", [L2, IP])
 def test_large_batch_engines(vf, engine, metric):
-    """Both large-batch engines of fp32 indexes meet the fp32 tolerance."""
+    """Every large-batch engine of fp32 indexes meets the fp32 tolerance."""
     xb = _rand(9000, 1536, 40) * 0.05
     xq = _rand(300, 1536, 41) * 0.05
     index = vf.IndexFlat(1536, metric)
@@ -380,12 +380,13 @@ def test_large_batch_engines(vf, engine, metric):
         assert not bad, (engine, k, bad[:5])
 
 
-def test_bf16x3_planes_follow_mutations(vf):
-    """The lazily built bf16 planes track add / remove_ids / reset."""
+@pytest.mark.parametrize("engine", ["bf16x3", "bf16x2v"])
+def test_blocked_rows_follow_mutations(vf, engine):
+    """The lazily built blocked copy of the rows tracks add / remove_ids / reset."""
     xb = _rand(3000, 96, 42)
     xq = _rand(150, 96, 43)
     index = vf.IndexFlatIP(96)
-    index.set_engine("bf16x3")
+    index.set_engine(engine)
     index.add(xb[:2000])
     D, I = index.search(xq, 10)  # builds planes for 2000 rows
     index.add(xb[2000:])  # planes now stale for the tail
@@ -465,3 +466,63 @@ def test_bf16x3_selfjoin_offsets(vf):
         assert abs(float(Sr[1000 + q, j]) - float(S[q, j])) < 1e-5
     S2, I2 = index.selfjoin(12, q0=5, nq=300, exclude_self=False)
     assert (I2[:, 0] == np.arange(5, 305)).mean() > 0.99  # a row is its own best match
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_bf16x2v_matches_exact_engine(vf, metric):
+    """The filter-and-verify engine returns the exact lists: oracle parity (ids
+    equal except documented ties) and the exact engine's ids on (nearly) every
+    row — the two round their fp32 scores differently, so an exact near-tie may
+    order differently."""
+    xb = _rand(200000, 256, 60)
+    xq = _rand(600, 256, 61)
+    index = vf.IndexFlat(256, metric)
+    index.add(xb)
+    for k in (1, 4, 10, 12, 16):
+        if metric == IP and 2 * k - 1 + 8 > 32:
+            continue
+        index.set_engine("bf16x3")
+        De, Ie = index.search(xq, k)
+        index.set_engine("bf16x2v")
+        D, I = index.search(xq, k)
+        Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        assert not bad, (k, bad[:5])
+        assert (I == Ie).all(axis=1).mean() > 0.99
+        np.testing.assert_allclose(D, De, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_bf16x2v_ragged_shapes(vf, metric):
+    for n, d, nq in ((5000, 100, 1000), (257, 1536, 129), (70001, 32, 256), (40, 64, 300)):
+        xb = _rand(n, d, 62)
+        xq = _rand(nq, d, 63)
+        index = vf.IndexFlat(d, metric)
+        index.set_engine("bf16x2v")
+        index.add(xb)
+        for k in (5, 10):
+            D, I = index.search(xq, k)
+            Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+            assert not bad, (n, d, nq, k, bad[:5])
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_bf16x2v_falls_back_on_ties(vf, metric):
+    """Duplicated rows tie exactly, so the bound cannot separate the candidates:
+    those queries go to the exact engine, and the results keep oracle parity."""
+    from vsearch import _lib
+
+    base = _rand(300, 64, 64)
+    xb = np.concatenate([np.repeat(base[:20], 40, axis=0), base[20:]])  # 800 dup + 280
+    xq = np.concatenate([base[:20] + 0.001 * _rand(20, 64, 65), _rand(300, 64, 66)])
+    index = vf.IndexFlat(64, metric)
+    index.set_engine("bf16x2v")
+    index.add(xb)
+    _lib.filter_stats(reset=True)
+    D, I = index.search(xq, 10)
+    nq, nfb = _lib.filter_stats(reset=True)
+    assert nq == xq.shape[0] and nfb >= 20
+    Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
+    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+    assert not bad, bad[:5]
