@@ -119,7 +119,7 @@ __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_c
 }  // namespace
 
 template <int KR, int MODE, int NP>
-__global__ __launch_bounds__(512, 1) void gemm_topk_x3(
+__device__ __forceinline__ void topk_body(
     const float* __restrict__ XB, const float* __restrict__ xaux, const uint4* __restrict__ QP,
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
     int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
@@ -332,11 +332,38 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x3(
   }
 }
 
+// The exact engine (three planes, six products) and the filter pass of bf16x2v
+// (two planes, three products), named apart so that profiles tell them apart.
+template <int KR, int MODE>
+__global__ __launch_bounds__(512, 1) void gemm_topk_x3(
+    const float* __restrict__ XB, const float* __restrict__ xaux, const uint4* __restrict__ QP,
+    const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
+    int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
+    int* __restrict__ pid) {
+  topk_body<KR, MODE, 3>(XB, xaux, QP, qaux, nqa, nkb, ntotal, ntiles, nsplit, nqt, self0, chunk,
+                         nchunk, KP, pkey, pid);
+}
+template <int KR, int MODE>
+__global__ __launch_bounds__(512, 1) void gemm_topk_x2f(
+    const float* __restrict__ XB, const float* __restrict__ xaux, const uint4* __restrict__ QP,
+    const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
+    int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
+    int* __restrict__ pid) {
+  topk_body<KR, MODE, 2>(XB, xaux, QP, qaux, nqa, nkb, ntotal, ntiles, nsplit, nqt, self0, chunk,
+                         nchunk, KP, pkey, pid);
+}
+
+template <int KR, int MODE, int NP>
+static const void* x3_kernel() {
+  if constexpr (NP == 3) return (const void*)gemm_topk_x3<KR, MODE>;
+  else return (const void*)gemm_topk_x2f<KR, MODE>;
+}
+
 template <int KR, int MODE, int NP>
 static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int* ndispatch) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_topk_x3<KR, MODE, NP>,
+    hipError_t e = hipFuncSetAttribute(x3_kernel<KR, MODE, NP>(),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds_bytes<NP>());
     if (e != hipSuccess) return e;
@@ -353,10 +380,15 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   for (int c = 0; c < nchunk; ++c) {
-    hipLaunchKernelGGL((gemm_topk_x3<KR, MODE, NP>), dim3(nqt * a.nsplit), dim3(512),
-                       lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, (int)(a.ld / kKB),
-                       a.ntotal, ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key,
-                       part.id);
+    const int nkb = (int)(a.ld / kKB);
+    if constexpr (NP == 3)
+      hipLaunchKernelGGL((gemm_topk_x3<KR, MODE>), dim3(nqt * a.nsplit), dim3(512),
+                         lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
+                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    else
+      hipLaunchKernelGGL((gemm_topk_x2f<KR, MODE>), dim3(nqt * a.nsplit), dim3(512),
+                         lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
+                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
