@@ -42,6 +42,11 @@ struct vs_index {
   // [0, blocked_rows).  capacity x ld floats.
   float* blocked = nullptr;
   int64_t blocked_rows = 0;
+  // fp32 indexes, filter pass from planes (VS_X2F_SRC=planes): the hi/mid bf16
+  // planes of the rows in the order of the filter kernel's LDS images
+  // (split_rows_kernel); valid for rows [0, planes_rows).  capacity x ld x 2 bf16.
+  uint4* planes = nullptr;
+  int64_t planes_rows = 0;
   int engine = VS_ENGINE_AUTO;
   std::mutex blocked_mu;
   std::shared_mutex mu;
@@ -142,10 +147,48 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
 
-void drop_blocked(vs_index* idx) {
+// Default source of the filter pass (x2f_source): blocked fp32 rows.
+constexpr int kX2fDefaultSource = 0;
+
+void drop_blocked(vs_index* idx) {  // both derived copies of the rows
   if (idx->blocked) (void)hipFree(idx->blocked);
   idx->blocked = nullptr;
   idx->blocked_rows = 0;
+  if (idx->planes) (void)hipFree(idx->planes);
+  idx->planes = nullptr;
+  idx->planes_rows = 0;
+}
+
+// Makes the hi/mid planes valid for all rows (as ensure_blocked).
+bool ensure_planes(vs_index* idx, hipStream_t st) {
+  std::lock_guard<std::mutex> g(idx->blocked_mu);
+  const size_t bytes = (size_t)idx->capacity * idx->ld * 2 * sizeof(uint16_t);
+  if (!idx->planes) {
+    if (hipMalloc(&idx->planes, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      idx->planes = nullptr;
+      return false;
+    }
+    idx->planes_rows = 0;
+    if (hipMemsetAsync(idx->planes, 0, bytes, st) != hipSuccess) return false;
+  }
+  if (idx->planes_rows < idx->ntotal) {
+    if (launch_split_rows((const float*)idx->codes, idx->ld, idx->planes_rows,
+                          idx->ntotal - idx->planes_rows, 2, idx->planes, st) != hipSuccess)
+      return false;
+    idx->planes_rows = idx->ntotal;
+  }
+  return true;
+}
+
+// Source of the filter pass's database operand: 1 = pre-split planes by
+// LDS-DMA, 0 = blocked fp32 rows split in the kernel.  VS_X2F_SRC=planes|blocked
+// overrides (read per search, so tests and A/B runs can switch it).
+int x2f_source() {
+  const char* e = getenv("VS_X2F_SRC");
+  if (e && strcmp(e, "planes") == 0) return 1;
+  if (e && strcmp(e, "blocked") == 0) return 0;
+  return kX2fDefaultSource;
 }
 
 // Makes the blocked copy valid for all rows (called under the shared lock;
@@ -238,7 +281,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
 // the usual merge emits (D, I).  Flagged queries are redone by the exact engine.
 int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq,
                       int nq_pad, int k, int need, int KF, float min_score, float* D, int64_t* I,
-                      hipStream_t st, const float* xaux) {
+                      hipStream_t st, const float* xaux, int xd) {
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
   X3Args a;
@@ -246,8 +289,9 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   const int nqt = a.nq_pad / kX3Q;
   const int ntiles = (ntotal + kX3Q - 1) / kX3Q;
   a.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
+  const int L = x2f_lane_len();  // lane list length (<= KF)
   Partials part;
-  part.KP = 32;
+  part.KP = kp_for(KF);  // lists padded past L, so the merge can emit KF
   part.P = 2 * a.nsplit;
   const size_t np_ = (size_t)a.nq_pad * part.P * part.KP;
   VS_HIP(scr.alloc((void**)&part.key, np_ * sizeof(float)), "vs: scratch");
@@ -268,7 +312,7 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   unsigned* xmax2 = nullptr;
   VS_HIP(scr.alloc((void**)&xmax2, sizeof(unsigned)), "vs: scratch");
   VS_HIP(launch_max_norm(idx->norms, ntotal, xmax2, st), "vs: max norm");
-  a.XB = idx->blocked;
+  a.XB = xd ? (const float*)idx->planes : idx->blocked;
   a.xaux = xaux;
   a.QP = qp;
   a.qaux = qaux;
@@ -278,7 +322,7 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   a.self0 = -1;
   {
     KernelTimer tm(st, "gemm_topk_x2f");
-    VS_HIP(launch_gemm_topk_x3(KF, mode, 2, a, part, st, &tm.dispatches),
+    VS_HIP(launch_gemm_topk_x3(L, mode, 2, xd, a, part, st, &tm.dispatches),
            "vs: gemm_topk_x2f launch");
     tm.stop();
   }
@@ -296,8 +340,8 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   VS_HIP(scr.alloc((void**)&vp.id, (size_t)nq * vp.KP * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&fail_d, (size_t)nq * sizeof(int)), "vs: scratch");
   VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
-                               qbuf, qn, idx->ld, x2f_bound_coef(idx->ld), xmax2, vp.key, vp.id,
-                               vp.KP, fail_d, st),
+                               qbuf, qn, idx->ld, x2f_bound_coef(idx->ld), xmax2, part, L,
+                               vp.key, vp.id, vp.KP, fail_d, st),
          "vs: verify");
   VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st),
          "vs: merge");
@@ -447,9 +491,12 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   if (engine == VS_ENGINE_AUTO) engine = KF > 0 ? VS_ENGINE_BF16X2_VERIFY : VS_ENGINE_BF16X3;
   if (engine == VS_ENGINE_BF16X2_VERIFY && (KF == 0 || self0 >= 0 || mode == MODE_COS))
     engine = VS_ENGINE_BF16X3;
-  if (idx->esize == 4 && engine == VS_ENGINE_BF16X2_VERIFY && ensure_blocked(idx, st))
-    return run_filter_verify(idx, mode, qbuf, qaux, nq, nq_pad, k, need, KF, min_score, D, I, st,
-                             xaux);
+  if (idx->esize == 4 && engine == VS_ENGINE_BF16X2_VERIFY) {
+    const int xd = x2f_source();
+    if (xd ? ensure_planes(idx, st) : ensure_blocked(idx, st))
+      return run_filter_verify(idx, mode, qbuf, qaux, nq, nq_pad, k, need, KF, min_score, D, I,
+                               st, xaux, xd);
+  }
   const int KR = x3_list_len(need);
   if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KR > 0 && ensure_blocked(idx, st)) {
     X3Args a;
@@ -478,7 +525,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     a.ntotal = ntotal;
     a.self0 = self0;
     KernelTimer tm(st, "gemm_topk_x3");
-    VS_HIP(launch_gemm_topk_x3(KR, mode, 3, a, part, st, &tm.dispatches),
+    VS_HIP(launch_gemm_topk_x3(KR, mode, 3, 0, a, part, st, &tm.dispatches),
            "vs: gemm_topk_x3 launch");
     tm.stop();
     VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
@@ -902,6 +949,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
   }
   const int64_t nt = idx->ntotal - nrem;
   idx->blocked_rows = std::min(idx->blocked_rows, first);  // rows from `first` on moved
+  idx->planes_rows = std::min(idx->planes_rows, first);
   VS_HIP(hipMemsetAsync(idx->row(nt), 0, (size_t)nrem * idx->rowbytes(), st),
          "vs_remove_ids: zero tail");
   VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),

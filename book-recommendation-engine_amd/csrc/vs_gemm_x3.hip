@@ -10,13 +10,19 @@
 // 2^-24 of |x_k q_k| — the size of the rounding error of one fp32 product.  The
 // result is an fp32-accurate dot product at 6/16 of the fp32 MFMA cost (the bf16
 // MFMA rate is 16x the fp32 one).  Scores are checked against the fp64 oracle
-// with the same tolerance as the plain fp32 kernel.
+// with the same tolerance as the plain fp32 kernel.  The same kernel body with
+// two planes (hi, mid: products hh, hm, mh) is the filter pass of the
+// filter-and-verify engine (gemm_topk_x2f; bound and verification further down).
 //
-// The split happens INSIDE the kernel, from fp32 data: pre-split planes are 6 B
-// per element against 4 B of fp32, and the staging instructions, not the matrix
-// cores, bound the first version of this engine, which streamed planes through
-// LDS-DMA (profiles/r01_x3_probes.txt: no staging loads 359 ms, all of them
-// 536 ms, every load an L2 hit 511 ms).
+// The exact engine splits INSIDE the kernel, from fp32 data: three pre-split
+// planes are 6 B per element against 4 B of fp32, and the staging instructions,
+// not the matrix cores, bound the first version of this engine, which streamed
+// planes through LDS-DMA (profiles/r01_x3_probes.txt: no staging loads 359 ms,
+// all of them 536 ms, every load an L2 hit 511 ms).  The filter pass can do
+// either (template XD): split in-kernel from the blocked fp32 rows (XD = 0), or
+// stream two pre-split planes — still 4 B per element — by LDS-DMA straight into
+// the stage's LDS image, with no split VALU and no ds_write (XD = 1,
+// split_rows_kernel builds them).
 //
 // Tile: 256 database rows x 256 queries per workgroup of 8 waves (two per SIMD,
 // one workgroup per CU).  Wave w owns queries [32w, 32w+32) against all 256 rows:
@@ -116,9 +122,33 @@ __device__ __forceinline__ void lds_barrier() {
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 
+// LDS-DMA of 16 B per lane into the wave-uniform LDS byte address `lds`; M0 is
+// written and restored inside the statement.  hipcc does not count it: the caller
+// retires it with its own vmcnt.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+// A 16-B register load hipcc does not count either; its destination is read only
+// after a wait statement that names it "+v" (cdna_hip_programming.md §5.7).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return __builtin_bit_cast(uint4, v);
+}
+// Ties a 16-B register value to the wait statement (a native vector, so the
+// operand is a VGPR quad rather than an indirect struct).
+#define VS_TIE16(q) "+v"(*reinterpret_cast<u32x4*>(&(q)))
+
 }  // namespace
 
-template <int KR, int MODE, int NP>
+template <int KR, int MODE, int NP, int XD>
 __device__ __forceinline__ void topk_body(
     const float* __restrict__ XB, const float* __restrict__ xaux, const uint4* __restrict__ QP,
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
@@ -210,17 +240,8 @@ __device__ __forceinline__ void topk_body(
       for (int j = 0; j < NP; ++j) *(uint4*)(base + j * kPlaneB) = pl[j];
     };
 
-    // One stage: MFMAs over the image of `buf` with query planes qc*, while
-    // stage+1's query planes load into qn*, stage+2's database slice into xn*,
-    // and stage+1's database slice (xc*) is split into the other image.
-    auto stage = [&](f32x16 (&acc)[8], int buf, int kb_next, const uint4 (&qc)[NP],
-                     uint4 (&qn)[NP], const f32x4& xc0, const f32x4& xc1, f32x4& xn0,
-                     f32x4& xn1) {
-      lds_barrier();  // this stage's image is complete; the previous one is free
-      if (VS_X3_PROBE != 2) {
-        load_q(kb_next, qn);
-        load_x(xn0, xn1);
-      }
+    // The MFMAs of one stage over the image of `buf` with query planes qc.
+    auto mma = [&](f32x16 (&acc)[8], int buf, const uint4 (&qc)[NP]) {
       const char* cb = smem + buf * kStageB + roff;
       uint4 x[NP];
 #pragma unroll
@@ -242,17 +263,82 @@ __device__ __forceinline__ void topk_body(
         }
         acc[i] = a;
       }
+    };
+
+    // One stage, XD = 0: MFMAs over the image of `buf` with query planes qc,
+    // while stage+1's query planes load into qn, stage+2's database slice into
+    // xn*, and stage+1's database slice (xc*) is split into the other image.
+    auto stage = [&](f32x16 (&acc)[8], int buf, int kb_next, const uint4 (&qc)[NP],
+                     uint4 (&qn)[NP], const f32x4& xc0, const f32x4& xc1, f32x4& xn0,
+                     f32x4& xn1) {
+      lds_barrier();  // this stage's image is complete; the previous one is free
+      if (VS_X3_PROBE != 2) {
+        load_q(kb_next, qn);
+        load_x(xn0, xn1);
+      }
+      mma(acc, buf, qc);
       write_x(buf ^ 1, xc0, xc1);
     };
 
-    uint4 qpa[NP], qpb[NP];      // query planes, two stages
-    f32x4 xa0, xa1, xb0, xb1;    // raw database slices, two stages
-    // prologue: stage 0's image and query planes, stage 1's slice in flight
-    f32x4 x00, x01;
-    load_x(x00, x01);
-    load_q(0, qpa);
-    load_x(xa0, xa1);
-    write_x(0, x00, x01);
+    // XD = 1.  Piece v (0 .. 8*NP-1) of a stage's image = plane v/8, rows
+    // 32*(v%8) .. +31 (1 KiB); wave w moves pieces NP*w .. NP*w + NP-1.  Lane l
+    // lands at bytes [16l, 16l+16) of its piece: row 32*(v%8) + l/2, 16-B slot
+    // l&1, which must hold chunk (l&1) ^ ((row >> 3) & 1) — the swizzle goes on
+    // the SOURCE address (the LDS side of LDS-DMA is lane-linear).  Query planes
+    // come by asm loads too; every load of a stage is retired by one vmcnt(0) at
+    // its end (counted and uncounted loads in one loop mis-wait).
+    const char* xpb = (const char*)XB;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
+    const int prow = lane >> 1;
+    const uint32_t psrc = (uint32_t)(prow * 2 + ((lane & 1) ^ ((prow >> 3) & 1))) * 16u;
+    auto dma_x = [&](int buf) {  // the stage at the cursor into image `buf`
+      const char* cbase = xpb + ((int64_t)min(lt, t1 - 1) * nkb + lst) * kStageB + psrc;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const int v = w * NP + j;
+        glds16(cbase + v * 1024,
+               __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(buf * kStageB + v * 1024)));
+      }
+      if (++lst == nkb) {
+        lst = 0;
+        ++lt;
+      }
+    };
+    auto load_q_asm = [&](int kb, uint4 (&q)[NP]) {
+      const uint4* p = qsrc + (int64_t)kb * 512;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) q[j] = gload16(p + j * qpl);
+    };
+    auto wait_all = [&](uint4 (&q)[NP]) {  // this wave's DMA and query loads landed
+      if constexpr (NP == 2)
+        asm volatile("s_waitcnt vmcnt(0)" : VS_TIE16(q[0]), VS_TIE16(q[1])::"memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" : VS_TIE16(q[0]), VS_TIE16(q[1]), VS_TIE16(q[2])::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto stage_dma = [&](f32x16 (&acc)[8], int buf, int kb_next, const uint4 (&qc)[NP],
+                         uint4 (&qn)[NP]) {
+      lds_barrier();  // this stage's image is complete; the previous one is free
+      load_q_asm(kb_next, qn);
+      dma_x(buf ^ 1);
+      mma(acc, buf, qc);
+      wait_all(qn);
+    };
+
+    uint4 qpa[NP], qpb[NP];    // query planes, two stages
+    f32x4 xa0, xa1, xb0, xb1;  // raw database slices, two stages (XD = 0)
+    if constexpr (XD == 0) {
+      // prologue: stage 0's image and query planes, stage 1's slice in flight
+      f32x4 x00, x01;
+      load_x(x00, x01);
+      load_q(0, qpa);
+      load_x(xa0, xa1);
+      write_x(0, x00, x01);
+    } else {
+      dma_x(0);
+      load_q_asm(0, qpa);
+      wait_all(qpa);
+    }
 
     float* spark = (float*)(smem + kNBuf * kStageB) + w * 16 * 64;
     for (int t = t0; t < t1; ++t) {
@@ -266,8 +352,13 @@ __device__ __forceinline__ void topk_body(
       // slices alternate between the a and b registers, so no copies are needed
       for (int st = 0; st < nkb; st += 2) {
         const int k1 = st + 1, k2 = st + 2 == nkb ? 0 : st + 2;
-        stage(acc, 0, k1, qpa, qpb, xa0, xa1, xb0, xb1);
-        stage(acc, 1, k2, qpb, qpa, xb0, xb1, xa0, xa1);
+        if constexpr (XD == 0) {
+          stage(acc, 0, k1, qpa, qpb, xa0, xa1, xb0, xb1);
+          stage(acc, 1, k2, qpb, qpa, xb0, xb1, xa0, xa1);
+        } else {
+          stage_dma(acc, 0, k1, qpa, qpb);
+          stage_dma(acc, 1, k2, qpb, qpa);
+        }
       }
 
       // Epilogue (one 32-row block at a time): keys, a 16-bit candidate mask
@@ -340,30 +431,32 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x3(
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
     int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
     int* __restrict__ pid) {
-  topk_body<KR, MODE, 3>(XB, xaux, QP, qaux, nqa, nkb, ntotal, ntiles, nsplit, nqt, self0, chunk,
-                         nchunk, KP, pkey, pid);
+  topk_body<KR, MODE, 3, 0>(XB, xaux, QP, qaux, nqa, nkb, ntotal, ntiles, nsplit, nqt, self0,
+                            chunk, nchunk, KP, pkey, pid);
 }
-template <int KR, int MODE>
+// XD: database operand from the blocked fp32 rows (0) or from pre-split planes
+// by LDS-DMA (1).
+template <int KR, int MODE, int XD>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x2f(
     const float* __restrict__ XB, const float* __restrict__ xaux, const uint4* __restrict__ QP,
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
     int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
     int* __restrict__ pid) {
-  topk_body<KR, MODE, 2>(XB, xaux, QP, qaux, nqa, nkb, ntotal, ntiles, nsplit, nqt, self0, chunk,
-                         nchunk, KP, pkey, pid);
+  topk_body<KR, MODE, 2, XD>(XB, xaux, QP, qaux, nqa, nkb, ntotal, ntiles, nsplit, nqt, self0,
+                             chunk, nchunk, KP, pkey, pid);
 }
 
-template <int KR, int MODE, int NP>
+template <int KR, int MODE, int NP, int XD>
 static const void* x3_kernel() {
   if constexpr (NP == 3) return (const void*)gemm_topk_x3<KR, MODE>;
-  else return (const void*)gemm_topk_x2f<KR, MODE>;
+  else return (const void*)gemm_topk_x2f<KR, MODE, XD>;
 }
 
-template <int KR, int MODE, int NP>
+template <int KR, int MODE, int NP, int XD>
 static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int* ndispatch) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(x3_kernel<KR, MODE, NP>(),
+    hipError_t e = hipFuncSetAttribute(x3_kernel<KR, MODE, NP, XD>(),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds_bytes<NP>());
     if (e != hipSuccess) return e;
@@ -386,7 +479,7 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
                          lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
                          ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     else
-      hipLaunchKernelGGL((gemm_topk_x2f<KR, MODE>), dim3(nqt * a.nsplit), dim3(512),
+      hipLaunchKernelGGL((gemm_topk_x2f<KR, MODE, XD>), dim3(nqt * a.nsplit), dim3(512),
                          lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
                          ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     hipError_t e = hipGetLastError();
@@ -396,34 +489,31 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   return hipSuccess;
 }
 
-// Exact split (NP = 3): every list length, IP / L2 / COS.  Filter pass (NP = 2):
-// IP and L2 with the list lengths x2f_list_len returns.
+// Exact split (NP = 3, XD = 0): every list length, IP / L2 / COS.  Filter pass
+// (NP = 2): IP and L2 with the list lengths x2f_list_len returns, from blocked
+// fp32 rows (XD = 0) or pre-split planes (XD = 1).
 template <int KR>
-static hipError_t x3_dispatch(int mode, int np, const X3Args& a, Partials part, hipStream_t st,
-                              int* ndispatch) {
-  if (np == 3 && KR <= 24) {
+static hipError_t x3_dispatch(int mode, int np, int xd, const X3Args& a, Partials part,
+                              hipStream_t st, int* ndispatch) {
+  if (np == 3 && xd == 0 && KR <= 24) {
     switch (mode) {
       case MODE_IP:
-        return x3_launch<KR, MODE_IP, 3>(a, part, st, ndispatch);
+        return x3_launch<KR, MODE_IP, 3, 0>(a, part, st, ndispatch);
       case MODE_L2:
-        return x3_launch<KR, MODE_L2, 3>(a, part, st, ndispatch);
+        return x3_launch<KR, MODE_L2, 3, 0>(a, part, st, ndispatch);
       case MODE_COS:
-        return x3_launch<KR, MODE_COS, 3>(a, part, st, ndispatch);
+        return x3_launch<KR, MODE_COS, 3, 0>(a, part, st, ndispatch);
       default:
         return hipErrorInvalidValue;
     }
   }
-  if constexpr (KR == 24 || KR == 32) {
-    if (np == 2) {
-      switch (mode) {
-        case MODE_IP:
-          return x3_launch<KR, MODE_IP, 2>(a, part, st, ndispatch);
-        case MODE_L2:
-          return x3_launch<KR, MODE_L2, 2>(a, part, st, ndispatch);
-        default:
-          break;
-      }
-    }
+  if constexpr (KR == 16 || KR == 32) {
+    if (np == 2 && mode == MODE_IP)
+      return xd ? x3_launch<KR, MODE_IP, 2, 1>(a, part, st, ndispatch)
+                : x3_launch<KR, MODE_IP, 2, 0>(a, part, st, ndispatch);
+    if (np == 2 && mode == MODE_L2)
+      return xd ? x3_launch<KR, MODE_L2, 2, 1>(a, part, st, ndispatch)
+                : x3_launch<KR, MODE_L2, 2, 0>(a, part, st, ndispatch);
   }
   return hipErrorInvalidValue;
 }
@@ -435,30 +525,41 @@ int x3_list_len(int need) {
   return need <= 8 ? 8 : need <= 12 ? 12 : need <= 16 ? 16 : need <= 20 ? 20 : need <= 24 ? 24 : 0;
 }
 
-// Filter pass list length for `need` exact entries: a margin of at least 8
-// approximate candidates beyond the entries the merge needs (0 = unsupported).
+// Filter pass: number of merged approximate candidates for `need` exact entries,
+// a margin of at least 8 beyond the entries the merge needs (0 = unsupported).
 int x2f_list_len(int need) { return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : 0; }
 
-hipError_t launch_gemm_topk_x3(int KR, int mode, int np, const X3Args& a, Partials part,
+// Per-lane list length of the filter pass.  A lane list does not have to hold
+// all KF candidates: a full list's last entry bounds every row the lane dropped,
+// and the verification takes the smallest such floor into its condition (see
+// below).  16 entries keep the kernel's 256 registers free of spills (32 spill);
+// on uncorrelated data each lane list sees 1/P of the rows, so its 16th entry
+// sits near rank 16·P overall, far behind the KF-th.  VS_X2F_L=32 overrides.
+int x2f_lane_len() {
+  const char* e = getenv("VS_X2F_L");
+  return e && atoi(e) == 32 ? 32 : 16;
+}
+
+hipError_t launch_gemm_topk_x3(int KR, int mode, int np, int xd, const X3Args& a, Partials part,
                                hipStream_t st, int* ndispatch) {
   // ld % 32: an even number of K-blocks per tile keeps the LDS image parity of a
   // stage equal to its K-block parity across tiles
   if (a.nq_pad % kT != 0 || a.ld % (2 * kKB) != 0 || KR > part.KP || part.P != 2 * a.nsplit ||
-      a.nsplit < 1 || (np != 2 && np != 3))
+      a.nsplit < 1 || (np != 2 && np != 3) || (xd != 0 && xd != 1))
     return hipErrorInvalidValue;
   switch (KR) {
     case 8:
-      return x3_dispatch<8>(mode, np, a, part, st, ndispatch);
+      return x3_dispatch<8>(mode, np, xd, a, part, st, ndispatch);
     case 12:
-      return x3_dispatch<12>(mode, np, a, part, st, ndispatch);
+      return x3_dispatch<12>(mode, np, xd, a, part, st, ndispatch);
     case 16:
-      return x3_dispatch<16>(mode, np, a, part, st, ndispatch);
+      return x3_dispatch<16>(mode, np, xd, a, part, st, ndispatch);
     case 20:
-      return x3_dispatch<20>(mode, np, a, part, st, ndispatch);
+      return x3_dispatch<20>(mode, np, xd, a, part, st, ndispatch);
     case 24:
-      return x3_dispatch<24>(mode, np, a, part, st, ndispatch);
+      return x3_dispatch<24>(mode, np, xd, a, part, st, ndispatch);
     case 32:
-      return x3_dispatch<32>(mode, np, a, part, st, ndispatch);
+      return x3_dispatch<32>(mode, np, xd, a, part, st, ndispatch);
     default:
       return hipErrorInvalidValue;
   }
@@ -521,6 +622,7 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     int KF, int M, const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
     const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
     const float* __restrict__ qn, int64_t ld, double coef, const unsigned* __restrict__ xmax2,
+    const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail) {
   __shared__ float ek[64];
   const int lane = threadIdx.x;
@@ -529,6 +631,20 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
   const int id = lane < KF ? (int)Ik[(int64_t)q * KF + lane] : -1;
   const float aK = __shfl(a, KF - 1);
   const int idK = __shfl(id, KF - 1);
+  // T: the KF-th merged key (if the merge found KF) and the last key of every
+  // full lane list; `bounded` = false when neither exists (the candidates are
+  // every admissible row)
+  bool bounded = idK >= 0;
+  float T = idK >= 0 ? aK : FLT_MAX;
+  for (int j = lane; j < P; j += 64) {
+    const int64_t o = ((int64_t)q * P + j) * LKP + L - 1;
+    if (lid[o] >= 0) {
+      bounded = true;
+      T = fminf(T, lkey[o]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) T = fminf(T, __shfl_xor(T, o));
+  bounded = __any(bounded);
 
   // exact keys, one candidate at a time across the wave
   const float* qrow = Q + (int64_t)q * ld;
@@ -582,25 +698,28 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
   double bkey = coef * sqrt(qn2) * sqrt(xm2);
   if constexpr (MODE == MODE_L2)  // key = (|q|^2 + |x|^2) - 2 ip, each side rounded
     bkey = 2.0 * bkey + 8.0 * std::ldexp(1.0, -24) * (qn2 + xm2);
-  // a list that is not full holds every admissible row
-  const bool pass = idK < 0 || ((double)aK - bkey > (double)eM && isfinite(aK) && isfinite(eM) &&
-                                isfinite(bkey));
+  const bool pass = !bounded || ((double)T - bkey > (double)eM && isfinite(T) && isfinite(eM) &&
+                                  isfinite(bkey));
   if (lane == 0) fail[q] = pass ? 0 : 1;
 }
 
 hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
                                  const int64_t* Ik, const float* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, double coef,
-                                 const unsigned* xmax2, float* okey, int* oid, int KP, int* fail,
-                                 hipStream_t st) {
-  if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0) return hipErrorInvalidValue;
+                                 const unsigned* xmax2, Partials lists, int L, float* okey,
+                                 int* oid, int KP, int* fail, hipStream_t st) {
+  if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
+      L > lists.KP)
+    return hipErrorInvalidValue;
   if (nq <= 0) return hipSuccess;
   if (mode == MODE_IP)
     hipLaunchKernelGGL(verify_rescore_kernel<MODE_IP>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
-                       X, xn, Q, qn, ld, coef, xmax2, okey, oid, KP, fail);
+                       X, xn, Q, qn, ld, coef, xmax2, lists.key, lists.id, lists.P, lists.KP, L,
+                       okey, oid, KP, fail);
   else if (mode == MODE_L2)
     hipLaunchKernelGGL(verify_rescore_kernel<MODE_L2>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
-                       X, xn, Q, qn, ld, coef, xmax2, okey, oid, KP, fail);
+                       X, xn, Q, qn, ld, coef, xmax2, lists.key, lists.id, lists.P, lists.KP, L,
+                       okey, oid, KP, fail);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -642,6 +761,44 @@ hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pa
     hipLaunchKernelGGL(split_queries_kernel<3>, grid, dim3(256), 0, st, Q, ld, n, nq_pad / kT, QP);
   else
     hipLaunchKernelGGL(split_queries_kernel<2>, grid, dim3(256), 0, st, Q, ld, n, nq_pad / kT, QP);
+  return hipGetLastError();
+}
+
+// Splits fp32 database rows [r0, r0+n) into NP bf16 planes laid out as the LDS
+// images of the stages (XD = 1): chunk (t, kb) holds NP planes of 8 KB, and 16-B
+// chunk h (k = 16kb + {4h..4h+3, 8+4h..8+4h+3}, the K permutation) of plane j,
+// row r%256 is uint4 ((t*nkb + kb)*NP + j)*512 + (r%256)*2 + h (unswizzled; the
+// kernel swizzles on the source address).  One thread per (row, kb, h).
+template <int NP>
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ X, int64_t ld,
+                                                         int64_t r0, int64_t n,
+                                                         uint4* __restrict__ XP) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nkb = ld / kKB;
+  if (p >= n * nkb * 2) return;
+  const int64_t r = r0 + p / (nkb * 2);
+  const int64_t kb = (p / 2) % nkb;
+  const int hh = (int)(p & 1);
+  const float* src = X + r * ld + kb * kKB + 4 * hh;
+  const f32x4 a = *(const f32x4*)src;
+  const f32x4 c = *(const f32x4*)(src + 8);
+  uint4 v[NP];
+  split_planes<NP>(a, c, v);
+  const int64_t base = ((r / kT) * nkb + kb) * NP * 512 + (r % kT) * 2 + hh;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) XP[base + j * 512] = v[j];
+}
+
+hipError_t launch_split_rows(const float* X, int64_t ld, int64_t r0, int64_t n, int np,
+                             uint4* XP, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ld % kKB != 0 || (np != 2 && np != 3)) return hipErrorInvalidValue;
+  const int64_t items = n * (ld / kKB) * 2;
+  const dim3 grid((unsigned)((items + 255) / 256));
+  if (np == 3)
+    hipLaunchKernelGGL(split_rows_kernel<3>, grid, dim3(256), 0, st, X, ld, r0, n, XP);
+  else
+    hipLaunchKernelGGL(split_rows_kernel<2>, grid, dim3(256), 0, st, X, ld, r0, n, XP);
   return hipGetLastError();
 }
 

@@ -82,24 +82,28 @@ constexpr int kX3Q = 256;  // queries (and database rows) per x3 tile
 int x3_list_len(int need);
 // Filter pass (NP = 2) list length for `need` exact entries (24 or 32; 0 = too long).
 int x2f_list_len(int need);
+int x2f_lane_len();
 // Writes 2*nsplit lists of part.KP entries per query (nq_pad queries): KR register
 // entries padded with empty slots.  np = 3: exact split (KR <= 24, IP/L2/COS);
-// np = 2: filter pass (KR 24 or 32, IP/L2).  *ndispatch = kernel launches used.
-hipError_t launch_gemm_topk_x3(int KR, int mode, int np, const X3Args& a, Partials part,
+// np = 2: filter pass (KR 24 or 32, IP/L2).  xd = 0: a.XB holds the blocked fp32
+// rows (launch_block_rows); xd = 1 (np = 2 only): the pre-split planes
+// (launch_split_rows).  *ndispatch = kernel launches used.
+hipError_t launch_gemm_topk_x3(int KR, int mode, int np, int xd, const X3Args& a, Partials part,
                                hipStream_t st, int* ndispatch);
 // |approx - exact| <= coef * |x| * |q| for the filter pass over ld K elements.
 double x2f_bound_coef(int64_t ld);
 // *out = bits of max(norms[0..n)) (norms >= 0; NaN propagates as the maximum).
 hipError_t launch_max_norm(const float* norms, int64_t n, unsigned* out, hipStream_t st);
 // Checks and rescores the filter candidates (see vs_gemm_x3.hip): Dk/Ik hold the
-// KF best approximate keys of each query (ascending, local rows); writes sorted
+// KF best approximate keys of each query (ascending, local rows), `lists` the
+// filter pass's lane lists (L entries each) for their floors; writes sorted
 // exact lists of KP entries (okey/oid) and fail[q] = 1 where the exact engine
 // must redo query q.
 hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
                                  const int64_t* Ik, const float* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, double coef,
-                                 const unsigned* xmax2, float* okey, int* oid, int KP, int* fail,
-                                 hipStream_t st);
+                                 const unsigned* xmax2, Partials lists, int L, float* okey,
+                                 int* oid, int KP, int* fail, hipStream_t st);
 // Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's np query planes
 // (np x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
 hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, int np,
@@ -108,6 +112,10 @@ hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pa
 // layout of 256-row tiles the x3 GEMM streams (vs_gemm_x3.hip).
 hipError_t launch_block_rows(const float* X, int64_t ld, int64_t r0, int64_t n, float* XB,
                              hipStream_t st);
+// Splits fp32 rows [r0, r0+n) into the np bf16 planes of the x2f LDS images
+// (capacity x ld x np bf16 in total; vs_gemm_x3.hip, split_rows_kernel).
+hipError_t launch_split_rows(const float* X, int64_t ld, int64_t r0, int64_t n, int np,
+                             uint4* XP, hipStream_t st);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
