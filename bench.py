@@ -103,12 +103,13 @@ def pmc_traffic(workload: str, kernel_prefix: str):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{workload}.json")))
     if not files:
         return None, None
-    with open(files[-1], encoding="utf-8") as f:
-        summ = json.load(f)
-    for name, rec in summ.get("kernels", {}).items():
-        if name.startswith(kernel_prefix):
-            return rec.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
-    return None, os.path.relpath(files[-1], ROOT)
+    for path in reversed(files):  # newest tag first; the first summary naming the kernel wins
+        with open(path, encoding="utf-8") as f:
+            summ = json.load(f)
+        for name, rec in summ.get("kernels", {}).items():
+            if name.startswith(kernel_prefix):
+                return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(shard, args, xq_host):
