@@ -197,6 +197,8 @@ class FAISS:
         self.distance_strategy = DistanceStrategy(distance_strategy)
         self.override_relevance_score_fn = relevance_score_fn
         self._normalize_L2 = normalize_L2
+        self._keymap_field: Optional[str] = None  # metadata field indexed by _key_index
+        self._keymap: Dict[Any, List[str]] = {}
         if (self.distance_strategy != DistanceStrategy.EUCLIDEAN_DISTANCE
                 and self._normalize_L2):
             warnings.warn(
@@ -242,6 +244,11 @@ class FAISS:
         self.docstore.add({id_: doc for id_, doc in zip(ids, documents)})
         starting_len = len(self.index_to_docstore_id)
         self.index_to_docstore_id.update({starting_len + j: id_ for j, id_ in enumerate(ids)})
+        if self._keymap_field is not None:
+            for doc in documents:
+                key = doc.metadata.get(self._keymap_field)
+                if key is not None:
+                    self._keymap.setdefault(key, []).append(doc.id)
         return ids
 
     def add_texts(self, texts: Iterable[str], metadatas: Optional[List[dict]] = None,
@@ -265,6 +272,62 @@ class FAISS:
                 kwargs["ids"] = [i if i else str(uuid.uuid4()) for i in ids]
         return self.add_texts(texts, metadatas, **kwargs)
 
+    def _key_index(self, field: str) -> Dict[Any, List[str]]:
+        """metadata[field] -> docstore ids holding it.  Built by one scan on first use
+        for `field`, then maintained by every add / delete (O(changed rows))."""
+        if self._keymap_field != field:
+            keymap: Dict[Any, List[str]] = {}
+            for i in sorted(self.index_to_docstore_id):
+                _id = self.index_to_docstore_id[i]
+                doc = self.docstore.search(_id)
+                if isinstance(doc, Document) and doc.metadata.get(field) is not None:
+                    keymap.setdefault(doc.metadata[field], []).append(_id)
+            self._keymap_field, self._keymap = field, keymap
+        return self._keymap
+
+    def ids_for_key(self, value: Any, field: str = "book_id") -> List[str]:
+        """Docstore ids whose metadata[field] == value, in label order."""
+        return list(self._key_index(field).get(value, ()))
+
+    def upsert_embeddings(self, texts: Sequence[str], embeddings: Sequence[List[float]],
+                          metadatas: Sequence[dict], key: str = "book_id",
+                          ids: Optional[List[str]] = None) -> List[str]:
+        """Delete-then-add.  The reference appends a second row when a
+        book is re-embedded (incremental_workers/book_vector/main.py:148,
+        ingestion_service/pipeline.py:363), so searches return the stale copy too.
+        Here every existing row whose metadata[key] matches an incoming row is
+        removed first (one remove_ids compaction on the device), and within the
+        batch the last row for a key wins.  Rows without the key are plain appends."""
+        texts, embeddings, metadatas = list(texts), list(embeddings), list(metadatas)
+        _len_check_if_sized(texts, metadatas, "texts", "metadatas")
+        _len_check_if_sized(texts, embeddings, "texts", "embeddings")
+        if ids is not None:
+            _len_check_if_sized(texts, ids, "texts", "ids")
+        last = {m.get(key): j for j, m in enumerate(metadatas) if m.get(key) is not None}
+        keep = [j for j, m in enumerate(metadatas)
+                if m.get(key) is None or last[m.get(key)] == j]
+        keymap = self._key_index(key)
+        stale = [sid for j in keep if metadatas[j].get(key) is not None
+                 for sid in keymap.get(metadatas[j][key], ())]
+        if ids is not None:
+            clash = set(ids[j] for j in keep).intersection(self.index_to_docstore_id.values())
+            clash.difference_update(stale)
+            if clash:
+                raise ValueError(f"Tried to add ids that already exist: {clash}")
+        if stale:
+            self.delete(stale)
+        return self.__add([texts[j] for j in keep], [embeddings[j] for j in keep],
+                          metadatas=[metadatas[j] for j in keep],
+                          ids=None if ids is None else [ids[j] for j in keep])
+
+    def upsert_texts(self, texts: Iterable[str], metadatas: List[dict], key: str = "book_id",
+                     ids: Optional[List[str]] = None, **kwargs: Any) -> List[str]:
+        """`add_texts` with delete-then-add on metadata[key]; embeds before mutating,
+        so an embedding failure leaves the store unchanged."""
+        texts = list(texts)
+        embeddings = self._embed_documents(texts)
+        return self.upsert_embeddings(texts, embeddings, metadatas, key=key, ids=ids)
+
     def delete(self, ids: Optional[List[str]] = None, **kwargs: Any) -> Optional[bool]:
         if ids is None:
             raise ValueError("No ids provided to delete.")
@@ -276,6 +339,15 @@ class FAISS:
         reversed_index = {id_: idx for idx, id_ in self.index_to_docstore_id.items()}
         index_to_delete = {reversed_index[id_] for id_ in ids}
         self.index.remove_ids(np.fromiter(index_to_delete, dtype=np.int64))
+        if self._keymap_field is not None:
+            for id_ in ids:
+                doc = self.docstore.search(id_)
+                key = doc.metadata.get(self._keymap_field) if isinstance(doc, Document) else None
+                lst = self._keymap.get(key)
+                if lst is not None and id_ in lst:
+                    lst.remove(id_)
+                    if not lst:
+                        del self._keymap[key]
         self.docstore.delete(ids)
         remaining_ids = [id_ for i, id_ in sorted(self.index_to_docstore_id.items())
                          if i not in index_to_delete]

@@ -116,3 +116,52 @@ def test_sharded_single_rank_nccl():
         np.testing.assert_array_equal(Id.cpu().numpy(), I)
     finally:
         dist.destroy_process_group()
+
+
+def test_upsert_on_gpu(golden):
+    """§8 f4 delete-then-add on the HIP index: a re-embedded book keeps one row."""
+    from vsearch import langchain as vlc
+    from vsearch.synth import SynthEmbeddings
+
+    inputs, _ = golden
+    emb = SynthEmbeddings()
+    texts, metas = inputs["book_texts"][:60], inputs["book_metadata"][:60]
+    store = vlc.FAISS.from_texts(texts, emb, metadatas=metas)
+    new = texts[7] + " (revised edition)"
+    store.upsert_texts([new], metadatas=[metas[7]])
+    assert store.index.ntotal == 60
+    assert len(store.ids_for_key(metas[7]["book_id"])) == 1
+    hit = store.similarity_search(new, k=1)[0]
+    assert hit.page_content == new and hit.metadata["book_id"] == metas[7]["book_id"]
+    want = np.stack([emb.embed_query(t) for t in texts[:7] + texts[8:] + [new]])
+    np.testing.assert_array_equal(store.index.reconstruct_n(0, 60), want.astype(np.float32))
+
+
+def test_service_on_gpu(catalog_store, golden):
+    """§8 f2 resident service: concurrent remote searches, coalesced into shared
+    engine calls on the HIP index, return what the in-process store returns."""
+    import threading
+
+    from vsearch.service import IndexService, RemoteFAISS
+
+    inputs, _ = golden
+    kws = inputs["keywords"][:32]
+    want = {kw: [(d.id, float(s)) for d, s in catalog_store.similarity_search_with_score(kw, k=5)]
+            for kw in kws}
+    got = {}
+    with IndexService(catalog_store) as svc:
+        barrier = threading.Barrier(8, timeout=60)
+
+        def worker(qs):
+            with RemoteFAISS(svc.address) as cli:
+                barrier.wait()
+                for kw in qs:
+                    got[kw] = [(d.id, float(s)) for d, s in cli.similarity_search_with_score(kw, k=5)]
+
+        ts = [threading.Thread(target=worker, args=(kws[i::8],)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(90)
+        assert svc.stats["search_rows"] == 32
+    assert got == want

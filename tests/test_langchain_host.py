@@ -223,3 +223,52 @@ def test_synthetic_rows_generator():
     z = sm(1234 ^ (i * 7 + j))
     assert x[1, 4] == np.float32((z >> 40) * 2.0 ** -23 - 1.0)
     np.testing.assert_array_equal(synthetic_rows(0, 10, 7, 1234)[5:8], x)
+
+
+def test_upsert_replaces_reembedded_rows(patched_indexes):
+    """a re-embedded book replaces its row instead of appending a
+    duplicate (the reference appends: book_vector/main.py:148)."""
+    emb = SynthEmbeddings(32)
+    texts = [f"book {i}" for i in range(6)]
+    metas = [{"book_id": f"B{i}"} for i in range(6)]
+    store = vlc.FAISS.from_texts(texts, emb, metadatas=metas,
+                                 distance_strategy=vlc.DistanceStrategy.MAX_INNER_PRODUCT)
+    assert store.ids_for_key("B2") == [store.index_to_docstore_id[2]]
+    # plain add_texts keeps the reference's append-duplicates behaviour
+    store.add_texts(["book 2 v2"], metadatas=[{"book_id": "B2"}])
+    assert store.index.ntotal == 7 and len(store.ids_for_key("B2")) == 2
+    # upsert: both B2 rows go, one new row; B4 appears twice in the batch, last wins
+    new_ids = store.upsert_texts(["book 2 v3", "book 4 v2", "book 4 v3", "fresh"],
+                                 metadatas=[{"book_id": "B2"}, {"book_id": "B4"},
+                                            {"book_id": "B4"}, {"book_id": "B9"}])
+    assert len(new_ids) == 3
+    assert store.index.ntotal == 6 - 2 + 3
+    assert sorted(store.index_to_docstore_id) == list(range(store.index.ntotal))
+    books = [store.docstore.search(store.index_to_docstore_id[i]).metadata["book_id"]
+             for i in range(store.index.ntotal)]
+    assert sorted(books) == ["B0", "B1", "B2", "B3", "B4", "B5", "B9"]
+    assert books.count("B2") == 1 and books.count("B4") == 1
+    # the index rows are the new embeddings, in label order
+    want = np.array(emb.embed_documents(["book 0", "book 1", "book 3", "book 5", "book 2 v3",
+                                         "book 4 v3", "fresh"]), dtype=np.float32)
+    np.testing.assert_array_equal(store.index.reconstruct_n(0, store.index.ntotal), want)
+    hit = store.similarity_search("book 4 v3", k=1)[0]
+    assert hit.metadata["book_id"] == "B4" and hit.page_content == "book 4 v3"
+    assert store.similarity_search("book 4 v2", k=1)[0].page_content != "book 4 v2"
+    # the key map follows deletes
+    store.delete(store.ids_for_key("B0"))
+    assert store.ids_for_key("B0") == [] and store.index.ntotal == 6
+
+
+def test_upsert_validates_before_mutating(patched_indexes):
+    emb = SynthEmbeddings(16)
+    store = vlc.FAISS.from_texts(["a", "b"], emb, metadatas=[{"book_id": 1}, {"book_id": 2}],
+                                 ids=["ia", "ib"])
+    with pytest.raises(ValueError):
+        store.upsert_texts(["c"], metadatas=[{"book_id": 3}], ids=["ia"])  # id clash
+    with pytest.raises(ValueError):
+        store.upsert_texts(["c", "d"], metadatas=[{"book_id": 3}])  # length mismatch
+    assert store.index.ntotal == 2
+    # re-using the replaced row's own id is allowed (it is deleted first)
+    store.upsert_texts(["a2"], metadatas=[{"book_id": 1}], ids=["ia"])
+    assert store.index.ntotal == 2 and store.docstore.search("ia").page_content == "a2"
