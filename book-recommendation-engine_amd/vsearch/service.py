@@ -12,8 +12,10 @@ HBM and serves the same vector-store calls to any number of clients:
 * Concurrent searches are **coalesced**: requests that arrive while the engine
   is busy are stacked into one (B x d) batch and run as ONE ``index.search``
   (the skinny / GEMM engines instead of B separate GEMV scans), then split back.
-  Results are identical to per-request searches: each query row's top-k does
-  not depend on the other rows of the batch.
+  Each row's answer is what faiss returns for that row inside a batch of the
+  stacked size: the same exact top-k; only the score's last bits can differ
+  from a lone search, as faiss's own nq < 20 / nq >= 20 branches do (L2 direct
+  sum vs norm expansion), within the fp32 tolerance.
 * Writers (``add_texts`` / ``upsert_texts`` / ``delete`` / ``save_local``) take the
   store exclusively; readers share it (readers-writer lock), the same ordering
   faiss gives (concurrent ``search`` allowed, ``add`` exclusive).

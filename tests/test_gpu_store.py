@@ -164,4 +164,9 @@ def test_service_on_gpu(catalog_store, golden):
         for t in ts:
             t.join(90)
         assert svc.stats["search_rows"] == 32
-    assert got == want
+    # a stacked batch may take faiss's other branch (nq >= 20: norm expansion,
+    # SURVEY.md §8 a7), so scores agree to the fp32 tolerance, ids exactly
+    for kw in kws:
+        assert [i for i, _ in got[kw]] == [i for i, _ in want[kw]]
+        np.testing.assert_allclose([s for _, s in got[kw]], [s for _, s in want[kw]],
+                                   rtol=1e-5, atol=1e-5)
