@@ -9,16 +9,19 @@ OUT=gpurun_out/ab_${TAG}
 mkdir -p "$OUT"
 VARIANTS=("$@")
 [ ${#VARIANTS[@]} -eq 0 ] && VARIANTS=("VS_X2F_SRC=blocked" "VS_X2F_SRC=planes")
+name() { local n=${1##*/}; n=${n//[=,.]/_}; echo "$n"; }  # log name of a variant
 if [ -z "${AB_SKIP_TESTS:-}" ]; then
   for v in "${VARIANTS[@]}"; do
+    n=$(name "$v")
     env ${v//,/ } timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
-      -m gpu tests/test_gpu_parity.py -k "bf16x2v or blocked_rows" > "$OUT/test_${v//[=,]/_}.log" 2>&1 \
-      || { echo "tests failed for $v"; tail -30 "$OUT/test_${v//[=,]/_}.log"; exit 1; }
-    tail -2 "$OUT/test_${v//[=,]/_}.log"
+      -m gpu tests/test_gpu_parity.py -k "${AB_TESTS:-bf16x2v or blocked_rows}" > "$OUT/test_$n.log" 2>&1 \
+      || { echo "tests failed for $v"; tail -30 "$OUT/test_$n.log"; exit 1; }
+    tail -2 "$OUT/test_$n.log"
   done
 fi
 for v in "${VARIANTS[@]}"; do
+  n=$(name "$v")
   env ${v//,/ } timeout -k 10 300 python3 -u bench.py --steps 5 --warmup 1 --batch1-steps 0 \
-    --no-cpu-baseline > "$OUT/bench_${v//[=,]/_}.log" 2>&1 || { echo "bench failed for $v"; tail -20 "$OUT/bench_${v//[=,]/_}.log"; exit 1; }
-  echo "$v: $(grep -o '"value": [0-9.]*' "$OUT/bench_${v//[=,]/_}.log" | head -1) $(grep -o '"frac": [0-9.]*' "$OUT/bench_${v//[=,]/_}.log" | head -1) $(grep -o '"fallback_queries": [0-9]*' "$OUT/bench_${v//[=,]/_}.log") $(grep -o '"rows_with_id_mismatch": [0-9]*' "$OUT/bench_${v//[=,]/_}.log")"
+    --no-cpu-baseline > "$OUT/bench_$n.log" 2>&1 || { echo "bench failed for $v"; tail -20 "$OUT/bench_$n.log"; exit 1; }
+  echo "$v: $(grep -o '"value": [0-9.]*' "$OUT/bench_$n.log" | head -1) $(grep -o '"frac": [0-9.]*' "$OUT/bench_$n.log" | head -1) $(grep -o '"fallback_queries": [0-9]*' "$OUT/bench_$n.log") $(grep -o '"rows_with_id_mismatch": [0-9]*' "$OUT/bench_$n.log")"
 done
