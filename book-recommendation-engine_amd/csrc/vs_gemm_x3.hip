@@ -61,6 +61,9 @@
 #ifndef VS_X3_PROBE
 #define VS_X3_PROBE 0
 #endif
+#ifndef VS_X2F_PRIO
+#define VS_X2F_PRIO 1
+#endif
 
 namespace vs {
 
@@ -70,17 +73,26 @@ constexpr int kT = 256;                   // database rows (and queries) per til
 constexpr int kKB = 16;                   // K elements per stage
 constexpr int kChunkF = kT * kKB;         // floats per (tile, K-block) chunk: 4096
 constexpr int kPlaneB = kT * 32;          // one bf16 plane of one stage: 8 KB
-constexpr int kNBuf = 2;
 constexpr int kSparkB = 8 * 16 * 64 * 4;  // epilogue parking, 4 KB per wave
+constexpr int kNBuf = 2;                  // LDS images (stages in flight)
 // NP planes per operand: 3 = exact split, 2 = hi/mid only (the filter pass)
-template <int NP>
+template <int NP, int XD>
 constexpr int lds_bytes() { return kNBuf * NP * kPlaneB + kSparkB; }
 constexpr int kX3ChunkTiles = 16;         // database tiles per workgroup per launch
 
 // 32-B LDS rows hold 2 chunks of 16 B; chunk c of row r is stored at
-// c ^ ((r >> 3) & 1), which spreads each 16-lane ds_read_b128 group of the
-// 32-row fragment reads over 16 distinct 16-B slots.
-__device__ __forceinline__ int swz32(int r, int c) { return c ^ ((r >> 3) & 1); }
+// c ^ (((r >> 3) ^ (r >> 2)) & 1).  Reads: each 16-lane ds_read_b128 group of the
+// 32-row fragment reads (rows {0-3,12-15,20-27} / {4-11,16-19,28-31}, 256-B bank
+// period) lands on 16 distinct 16-B slots; writes: each 8-lane ds_write_b128
+// group (rows 8j..8j+7, 128-B bank period) covers 8 distinct slots, so neither
+// conflicts.  (VS_X2F_SWZ=0 selects the older c ^ ((r >> 3) & 1): conflict-free
+// reads, 2-way conflicted writes.)
+#ifndef VS_X2F_SWZ
+#define VS_X2F_SWZ 1
+#endif
+__device__ __forceinline__ int swz32(int r, int c) {
+  return VS_X2F_SWZ ? c ^ (((r >> 3) ^ (r >> 2)) & 1) : c ^ ((r >> 3) & 1);
+}
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -154,7 +166,7 @@ __device__ __forceinline__ void topk_body(
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
     int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
     int* __restrict__ pid) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // lds_bytes<NP>()
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // lds_bytes<NP, XD>()
   constexpr int kStageB = NP * kPlaneB;
 
   const int tid = threadIdx.x;
@@ -290,7 +302,7 @@ __device__ __forceinline__ void topk_body(
     const char* xpb = (const char*)XB;
     const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
     const int prow = lane >> 1;
-    const uint32_t psrc = (uint32_t)(prow * 2 + ((lane & 1) ^ ((prow >> 3) & 1))) * 16u;
+    const uint32_t psrc = (uint32_t)(prow * 2 + swz32(prow, lane & 1)) * 16u;
     auto dma_x = [&](int buf) {  // the stage at the cursor into image `buf`
       const char* cbase = xpb + ((int64_t)min(lt, t1 - 1) * nkb + lst) * kStageB + psrc;
 #pragma unroll
@@ -340,39 +352,25 @@ __device__ __forceinline__ void topk_body(
       wait_all(qpa);
     }
 
+    // waves 4-7 share their SIMDs with waves 0-3 and lose every VALU
+    // arbitration on age; one static priority for that half (MI355X_MICROARCH.md,
+    // "Two waves per SIMD" item 4)
+    if (VS_X2F_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
     float* spark = (float*)(smem + kNBuf * kStageB) + w * 16 * 64;
-    for (int t = t0; t < t1; ++t) {
-      f32x16 acc[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
 
-      // two stages per iteration (nkb is even): the query planes and database
-      // slices alternate between the a and b registers, so no copies are needed
-      for (int st = 0; st < nkb; st += 2) {
-        const int k1 = st + 1, k2 = st + 2 == nkb ? 0 : st + 2;
-        if constexpr (XD == 0) {
-          stage(acc, 0, k1, qpa, qpb, xa0, xa1, xb0, xb1);
-          stage(acc, 1, k2, qpb, qpa, xb0, xb1, xa0, xa1);
-        } else {
-          stage_dma(acc, 0, k1, qpa, qpb);
-          stage_dma(acc, 1, k2, qpb, qpa);
-        }
-      }
-
-      // Epilogue (one 32-row block at a time): keys, a 16-bit candidate mask
-      // against the lane's current worst entry, and insertion of the flagged
-      // values only (after the first tiles almost nothing passes).
-      const int r0 = t * kT;
+    // Epilogue of tile t (one 32-row block at a time): keys, a 16-bit candidate
+    // mask against the lane's current worst entry, and insertion of the flagged
+    // values only (after the first tiles almost nothing passes).
+    auto epilogue = [&](const f32x16 (&acc)[8], int t) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
+        const int r0 = t * kT + 32 * i;
         f32x4 xa[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
-            xa[jj] = *(const f32x4*)(xaux + r0 + 32 * i + 8 * jj + 4 * h);
+            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
         }
         const float tk = lk[KR - 1];
         const int ti = li[KR - 1];
@@ -380,7 +378,7 @@ __device__ __forceinline__ void topk_body(
         f32x16 v16 = acc[i];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const int rb = r0 + 32 * i + 8 * jj + 4 * h;
+          const int rb = r0 + 8 * jj + 4 * h;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int row = rb + e;
@@ -404,11 +402,32 @@ __device__ __forceinline__ void topk_body(
           do {
             const int bi = __builtin_ctz(m);
             m &= m - 1;
-            const int row = r0 + 32 * i + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+            const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
             list_insert<KR, int>(lk, li, spark[bi * 64 + lane], row);
           } while (m);
         }
       }
+    };
+
+    for (int t = t0; t < t1; ++t) {
+      f32x16 acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+      // two stages per iteration (nkb is even): the query planes and database
+      // slices alternate between the a and b registers, so no copies are needed
+      for (int st = 0; st < nkb; st += 2) {
+        const int k1 = st + 1, k2 = st + 2 == nkb ? 0 : st + 2;
+        if constexpr (XD == 0) {
+          stage(acc, 0, k1, qpa, qpb, xa0, xa1, xb0, xb1);
+          stage(acc, 1, k2, qpb, qpa, xb0, xb1, xa0, xa1);
+        } else {
+          stage_dma(acc, 0, k1, qpa, qpb);
+          stage_dma(acc, 1, k2, qpb, qpa);
+        }
+      }
+      epilogue(acc, t);
     }
   }
 
@@ -458,7 +477,7 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(x3_kernel<KR, MODE, NP, XD>(),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       lds_bytes<NP>());
+                                       lds_bytes<NP, XD>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -472,15 +491,16 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
+  constexpr int lds = lds_bytes<NP, XD>();
   for (int c = 0; c < nchunk; ++c) {
     const int nkb = (int)(a.ld / kKB);
     if constexpr (NP == 3)
       hipLaunchKernelGGL((gemm_topk_x3<KR, MODE>), dim3(nqt * a.nsplit), dim3(512),
-                         lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
+                         lds, st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
                          ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     else
       hipLaunchKernelGGL((gemm_topk_x2f<KR, MODE, XD>), dim3(nqt * a.nsplit), dim3(512),
-                         lds_bytes<NP>(), st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
+                         lds, st, a.XB, a.xaux, a.QP, a.qaux, a.nqa, nkb, a.ntotal,
                          ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -507,7 +527,7 @@ static hipError_t x3_dispatch(int mode, int np, int xd, const X3Args& a, Partial
         return hipErrorInvalidValue;
     }
   }
-  if constexpr (KR == 16 || KR == 32) {
+  if constexpr (KR == 12 || KR == 16 || KR == 32) {
     if (np == 2 && mode == MODE_IP)
       return xd ? x3_launch<KR, MODE_IP, 2, 1>(a, part, st, ndispatch)
                 : x3_launch<KR, MODE_IP, 2, 0>(a, part, st, ndispatch);
@@ -534,10 +554,11 @@ int x2f_list_len(int need) { return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : 
 // and the verification takes the smallest such floor into its condition (see
 // below).  16 entries keep the kernel's 256 registers free of spills (32 spill);
 // on uncorrelated data each lane list sees 1/P of the rows, so its 16th entry
-// sits near rank 16·P overall, far behind the KF-th.  VS_X2F_L=32 overrides.
+// sits near rank 16·P overall, far behind the KF-th.  VS_X2F_L=12 / 32 override.
 int x2f_lane_len() {
   const char* e = getenv("VS_X2F_L");
-  return e && atoi(e) == 32 ? 32 : 16;
+  const int v = e ? atoi(e) : 0;
+  return v == 12 || v == 32 ? v : 16;
 }
 
 hipError_t launch_gemm_topk_x3(int KR, int mode, int np, int xd, const X3Args& a, Partials part,
