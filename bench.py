@@ -299,7 +299,9 @@ def run_knn(args, ctx):
                        "max_abs_score_diff": float(np.abs(De - Dh[:nchk]).max())}
         sane &= rows == 0
     gemv = kname in HBM_KERNELS  # the small-batch kernels are HBM-bound
-    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
+    # PMC summaries are single-GPU profiles: per-dispatch bytes of a 1/N shard differ
+    traffic, tsrc = (pmc_traffic(args.workload, "void vs::" + kname + "<") if ctx.world == 1
+                     else (None, None))
     if gemv:
         rf = roofline("hbm", n_shard * d * esz * args.steps, kms, nl,
                       f"{n_shard}*{d}*{esz} B per search (batch {B} over the rank's shard)",
