@@ -76,7 +76,7 @@ constexpr int kPlaneB = kT * 32;          // one bf16 plane of one stage: 8 KB
 constexpr int kSparkB = 8 * 16 * 64 * 4;  // epilogue parking, 4 KB per wave
 constexpr int kNBuf = 2;                  // LDS images (stages in flight)
 // NP planes per operand: 3 = exact split, 2 = hi/mid only (the filter pass)
-template <int NP, int XD>
+template <int NP>
 constexpr int lds_bytes() { return kNBuf * NP * kPlaneB + kSparkB; }
 constexpr int kX3ChunkTiles = 16;         // database tiles per workgroup per launch
 
@@ -166,8 +166,8 @@ __device__ __forceinline__ void topk_body(
     const float* __restrict__ qaux, int nqa, int nkb, int ntotal, int ntiles, int nsplit, int nqt,
     int64_t self0, int chunk, int nchunk, int KP, float* __restrict__ pkey,
     int* __restrict__ pid) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // lds_bytes<NP, XD>()
-  constexpr int kStageB = NP * kPlaneB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // lds_bytes<NP>()
+  constexpr int kStageB = NP * kPlaneB;  // one LDS image: NP planes of one K-block
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -473,11 +473,11 @@ static const void* x3_kernel() {
 
 template <int KR, int MODE, int NP, int XD>
 static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int* ndispatch) {
+  constexpr int lds = lds_bytes<NP>();
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(x3_kernel<KR, MODE, NP, XD>(),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       lds_bytes<NP, XD>());
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -491,7 +491,6 @@ static hipError_t x3_launch(const X3Args& a, Partials part, hipStream_t st, int*
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
-  constexpr int lds = lds_bytes<NP, XD>();
   for (int c = 0; c < nchunk; ++c) {
     const int nkb = (int)(a.ld / kKB);
     if constexpr (NP == 3)

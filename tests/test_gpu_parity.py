@@ -380,6 +380,24 @@ def test_large_batch_engines(vf, engine, metric):
         assert not bad, (engine, k, bad[:5])
 
 
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("d", [64, 128, 192, 96, 160])
+def test_bf16x2v_stage_shapes(vf, metric, d):
+    """The filter pass takes two K-blocks per stage when ld % 64 == 0 (d = 64, 128,
+    192: one, two, three stage pairs per tile) and one otherwise (96, 160);
+    several tiles, a ragged last tile and a ragged query tile."""
+    xb = _rand(1800, d, 46)
+    xq = _rand(300, d, 47)
+    index = vf.IndexFlat(d, metric)
+    index.set_engine("bf16x2v")
+    index.add(xb)
+    for k in (1, 10):
+        D, I = index.search(xq, k)
+        Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        assert not bad, (d, k, bad[:5])
+
+
 @pytest.mark.parametrize("engine", ["bf16x3", "bf16x2v"])
 def test_blocked_rows_follow_mutations(vf, engine):
     """The lazily built blocked copy of the rows tracks add / remove_ids / reset."""
