@@ -84,6 +84,10 @@ def parse():
     p.add_argument("--batch", type=int, default=None)
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--metric", choices=["ip", "l2"], default=None)
+    p.add_argument("--data", choices=["uniform", "clustered"], default="uniform",
+                   help="c2/c3 corpus: counter-based uniform rows (default) or unit-norm "
+                        "clustered rows like text embeddings (1024 centroids, noise 0.5; "
+                        "one GPU only) to measure the filter engine's fallback rate")
     p.add_argument("--batch1-steps", type=int, default=20)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
@@ -260,6 +264,27 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
     return r
 
 
+class ClusteredRows:
+    """Unit-norm rows like text embeddings: row i = normalize(c[i % 1024] + 0.5 * n_i),
+    centroids c and noise n_i standard normal / sqrt(d) (the clustered
+    variant).  Deterministic per 1M-row chunk; queries use another noise seed."""
+
+    def __init__(self, torch, d, seed, noise_seed=None, ncent=1024, sigma=0.5):
+        self.torch, self.d, self.sigma = torch, d, sigma
+        self.noise_seed = seed + 1 if noise_seed is None else noise_seed
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        c = torch.randn((ncent, d), generator=g, device="cuda")
+        self.cent = c / c.norm(dim=1, keepdim=True)
+
+    def rows(self, r0, n):
+        torch = self.torch
+        g = torch.Generator(device="cuda").manual_seed(self.noise_seed * 1_000_003 + r0)
+        idx = torch.arange(r0, r0 + n, device="cuda") % self.cent.shape[0]
+        x = self.cent[idx] + self.sigma * torch.randn((n, self.d), generator=g,
+                                                      device="cuda") / self.d ** 0.5
+        return (x / x.norm(dim=1, keepdim=True)).contiguous()
+
+
 def run_knn(args, ctx):
     import numpy as np
 
@@ -269,10 +294,22 @@ def run_knn(args, ctx):
     torch = ctx.torch
     metric = vfaiss.METRIC_INNER_PRODUCT if args.metric == "ip" else vfaiss.METRIC_L2
     index = ShardedIndexFlat(args.d, metric, device=ctx.local, dtype=args.dtype)
-    index.add_synthetic(args.ntotal, seed=1234)
-    n_shard = index.shard.ntotal
     B, d, k = args.batch, args.d, args.k
-    xq = ctx.queries(B, d)
+    if args.data == "clustered":
+        if ctx.world != 1:
+            raise SystemExit("--data clustered runs on one GPU")
+        gen = ClusteredRows(torch, d, seed=1234)
+        for r0 in range(0, args.ntotal, 1 << 20):
+            x = gen.rows(r0, min(1 << 20, args.ntotal - r0))
+            index.shard.add_device(x.data_ptr(), x.shape[0], stream=ctx.stream)
+            torch.cuda.synchronize()
+            del x
+        index._sync_counts()
+        xq = ClusteredRows(torch, d, seed=1234, noise_seed=5678).rows(0, B)
+    else:
+        index.add_synthetic(args.ntotal, seed=1234)
+        xq = ctx.queries(B, d)
+    n_shard = index.shard.ntotal
 
     ctx.lib.filter_stats(reset=True)
     elapsed, kms, nl, (D, I) = ctx.timed(
@@ -330,6 +367,9 @@ def run_knn(args, ctx):
         if not args.no_cpu_baseline and ctx.world == 1 and args.dtype == "f32":
             cpu = cpu_baseline(index.shard, args, xq.cpu().numpy())
         res = base_result(args, ctx, args.steps * B / elapsed, elapsed)
+        if args.data == "clustered":
+            res["data"] = ("synthetic: unit-norm clustered rows (1024 centroids + 0.5 noise, "
+                           "torch generator seed 1234; queries noise seed 5678)")
         res["config"] = {
             "workload": f"{args.workload.upper()}: {args.ntotal}x{d} {args.dtype} exact flat "
                         f"{'inner-product' if args.metric == 'ip' else 'L2'}, batch {B}, top-{k}",
@@ -468,6 +508,9 @@ def run_c5(args, ctx):
     mt = ctx.max_over_ranks(mut_time)
     if ctx.rank == 0:
         res = base_result(args, ctx, args.steps * B / elapsed, elapsed)
+        if args.data == "clustered":
+            res["data"] = ("synthetic: unit-norm clustered rows (1024 centroids + 0.5 noise, "
+                           "torch generator seed 1234; queries noise seed 5678)")
         res["config"] = {"workload": f"C5: {N}x{d} {args.dtype}-stored flat "
                                      f"{'IP' if args.metric == 'ip' else 'L2'}, batch {B}, "
                                      f"top-{k}, 1% remove + 1% append every 10 batches",

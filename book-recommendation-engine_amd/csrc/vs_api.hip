@@ -48,11 +48,18 @@ struct vs_index {
   uint4* planes = nullptr;
   int64_t planes_rows = 0;
   int engine = VS_ENGINE_AUTO;
+  // filter-and-verify fallback rate (moving average over large searches) and a
+  // probe counter: see the adaptive choice in run_topk
+  double x2v_fallback = 0.0;
+  int64_t x2v_probe = 0;
+  std::mutex x2v_mu;
   std::mutex blocked_mu;
   std::shared_mutex mu;
 };
 
 namespace {
+
+constexpr double kX2vMaxFallback = 0.4;  // filter-and-verify: adaptive switch point
 
 thread_local std::string g_err;
 
@@ -358,6 +365,11 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
     g_filter_queries += nq;
     g_filter_fallbacks += (int64_t)F.size();
   }
+  {
+    std::lock_guard<std::mutex> g(idx->x2v_mu);
+    const double w = std::min(1.0, nq / 1024.0) * 0.5;  // small batches move it less
+    idx->x2v_fallback = (1.0 - w) * idx->x2v_fallback + w * ((double)F.size() / nq);
+  }
   if (F.empty()) return VS_OK;
   const int nf = (int)F.size();
   const int nf_pad = (int)round_up(std::max(nf, kGemvMaxQ), kBQ) + kBQ;  // chunk tails
@@ -488,9 +500,19 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   // entries of each partial list the final merge needs (faiss's IP tie rule: 2k-1)
   const int need = mode == MODE_IP ? std::min(2 * k - 1, VS_MAX_K) : k;
   const int KF = x2f_list_len(need);
+  const bool library_choice = engine == VS_ENGINE_AUTO;
   if (engine == VS_ENGINE_AUTO) engine = KF > 0 ? VS_ENGINE_BF16X2_VERIFY : VS_ENGINE_BF16X3;
   if (engine == VS_ENGINE_BF16X2_VERIFY && (KF == 0 || self0 >= 0 || mode == MODE_COS))
     engine = VS_ENGINE_BF16X3;
+  // Adaptive: a query falls back when its top scores crowd inside the filter's
+  // error bound.  The filter pass costs ~0.53 of the exact engine, so once the
+  // recent fallback rate passes 0.4 (break-even ~0.47) the exact engine runs
+  // directly; every 16th search still takes the filter path to re-measure.
+  if (library_choice && engine == VS_ENGINE_BF16X2_VERIFY) {
+    std::lock_guard<std::mutex> g(idx->x2v_mu);
+    if (idx->x2v_fallback > kX2vMaxFallback && idx->x2v_probe++ % 16 != 0)
+      engine = VS_ENGINE_BF16X3;
+  }
   if (idx->esize == 4 && engine == VS_ENGINE_BF16X2_VERIFY) {
     const int xd = x2f_source();
     if (xd ? ensure_planes(idx, st) : ensure_blocked(idx, st))

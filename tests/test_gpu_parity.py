@@ -544,3 +544,27 @@ def test_bf16x2v_falls_back_on_ties(vf, metric):
     Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
     bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
     assert not bad, bad[:5]
+
+
+def test_auto_engine_adapts_to_fallback_rate(vf):
+    """Auto engine choice: when most queries of the recent filter passes fall back
+    (every query near a 40-fold duplicated row), large searches go straight to the
+    exact engine, with one filter pass every 16 searches to re-measure; results
+    keep oracle parity throughout."""
+    from vsearch import _lib
+
+    base = _rand(300, 64, 70)
+    xb = np.repeat(base, 40, axis=0)  # every row tied 40 times
+    xq = base[:256] + 0.001 * _rand(256, 64, 71)
+    index = vf.IndexFlatIP(64)  # engine left on auto
+    index.add(xb)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    filtered = []
+    for _ in range(17):
+        _lib.filter_stats(reset=True)
+        D, I = index.search(xq, 10)
+        filtered.append(_lib.filter_stats(reset=True)[0])
+        bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+        assert not bad, bad[:5]
+    assert filtered[0] == 256  # first search: filter pass, (nearly) all fall back
+    assert sum(1 for f in filtered[1:] if f) <= 2  # then the exact engine, re-probes only
