@@ -555,7 +555,7 @@ def test_auto_engine_adapts_to_fallback_rate(vf):
 
     base = _rand(300, 64, 70)
     xb = np.repeat(base, 40, axis=0)  # every row tied 40 times
-    xq = base[:256] + 0.001 * _rand(256, 64, 71)
+    xq = np.repeat(base, 4, axis=0)[:1024] + 0.001 * _rand(1024, 64, 71)
     index = vf.IndexFlatIP(64)  # engine left on auto
     index.add(xb)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
@@ -566,5 +566,5 @@ def test_auto_engine_adapts_to_fallback_rate(vf):
         filtered.append(_lib.filter_stats(reset=True)[0])
         bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
         assert not bad, bad[:5]
-    assert filtered[0] == 256  # first search: filter pass, (nearly) all fall back
+    assert filtered[0] == 1024  # first search: filter pass, (nearly) all fall back
     assert sum(1 for f in filtered[1:] if f) <= 2  # then the exact engine, re-probes only
