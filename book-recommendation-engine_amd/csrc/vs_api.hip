@@ -288,15 +288,19 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
 // the usual merge emits (D, I).  Flagged queries are redone by the exact engine.
 int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq,
                       int nq_pad, int k, int need, int KF, float min_score, float* D, int64_t* I,
-                      hipStream_t st, const float* xaux, int xd) {
+                      hipStream_t st, const float* xaux, int xd, int64_t self0) {
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
   X3Args a;
   a.nq_pad = (int)round_up(nq_pad, kX3Q);
   const int nqt = a.nq_pad / kX3Q;
   const int ntiles = (ntotal + kX3Q - 1) / kX3Q;
-  a.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
   const int L = x2f_lane_len();  // lane list length (<= KF)
+  // enough lists that their 2*nsplit*L entries cover 2*KF candidates (KF = 64:
+  // four database splits even when the query tiles alone fill the chip)
+  a.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, (KF + L - 1) / L),
+                                    std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
+  a.nsplit = std::max(a.nsplit, 1);
   Partials part;
   part.KP = kp_for(KF);  // lists padded past L, so the merge can emit KF
   part.P = 2 * a.nsplit;
@@ -326,7 +330,7 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   a.nqa = nq_pad;
   a.ld = idx->ld;
   a.ntotal = ntotal;
-  a.self0 = -1;
+  a.self0 = self0;  // self-join: query q is row self0 + q, never its own candidate
   {
     KernelTimer tm(st, "gemm_topk_x2f");
     VS_HIP(launch_gemm_topk_x3(L, mode, 2, xd, a, part, st, &tm.dispatches),
@@ -340,15 +344,18 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   VS_HIP(scr.alloc((void**)&Ik, (size_t)nq * KF * sizeof(int64_t)), "vs: scratch");
   VS_HIP(launch_merge_partials(MODE_L2, part, nq, KF, 0, 0.0f, Dk, Ik, KF, st), "vs: merge");
   Partials vp;
-  vp.KP = 32;
+  vp.KP = kp_for(KF);
   vp.P = 1;
   int* fail_d = nullptr;
   VS_HIP(scr.alloc((void**)&vp.key, (size_t)nq * vp.KP * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&vp.id, (size_t)nq * vp.KP * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&fail_d, (size_t)nq * sizeof(int)), "vs: scratch");
+  // cosine (self-join): qaux / xaux are the inverse norms the keys are scaled by
+  const double coef = mode == MODE_COS ? x2f_cos_key_bound(idx->ld) : x2f_bound_coef(idx->ld);
   VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
-                               qbuf, qn, idx->ld, x2f_bound_coef(idx->ld), xmax2, part, L,
-                               vp.key, vp.id, vp.KP, fail_d, st),
+                               qbuf, qn, idx->ld, coef, xmax2, part, L, vp.key, vp.id, vp.KP,
+                               fail_d, st, mode == MODE_COS ? qaux : nullptr,
+                               mode == MODE_COS ? xaux : nullptr),
          "vs: verify");
   VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st),
          "vs: merge");
@@ -372,6 +379,9 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   }
   if (F.empty()) return VS_OK;
   const int nf = (int)F.size();
+  // self-joins: the flagged queries are not consecutive rows, so they are redone
+  // as plain searches for k + 1 and their own row is dropped afterwards
+  const int kf = self0 >= 0 ? k + 1 : k;
   const int nf_pad = (int)round_up(std::max(nf, kGemvMaxQ), kBQ) + kBQ;  // chunk tails
   float* q2 = nullptr;
   float* a2 = nullptr;
@@ -379,15 +389,15 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   int64_t* I2 = nullptr;
   VS_HIP(scr.alloc((void**)&q2, (size_t)nf_pad * idx->ld * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&a2, (size_t)nf_pad * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&D2, (size_t)nf * k * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&I2, (size_t)nf * k * sizeof(int64_t)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&D2, (size_t)nf * kf * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&I2, (size_t)nf * kf * sizeof(int64_t)), "vs: scratch");
   VS_HIP(hipMemsetAsync(q2, 0, (size_t)nf_pad * idx->ld * sizeof(float), st), "vs: fallback");
   VS_HIP(hipMemsetAsync(a2, 0, (size_t)nf_pad * sizeof(float), st), "vs: fallback");
   for (int i = 0; i < nf; ++i) {
     VS_HIP(hipMemcpyAsync(q2 + (int64_t)i * idx->ld, qbuf + (int64_t)F[i] * idx->ld,
                           (size_t)idx->ld * sizeof(float), hipMemcpyDeviceToDevice, st),
            "vs: fallback");
-    if (mode == MODE_L2)
+    if (mode == MODE_L2 || mode == MODE_COS)  // |q|^2, or 1/|q| for cosine
       VS_HIP(hipMemcpyAsync(a2 + i, qaux + F[i], sizeof(float), hipMemcpyDeviceToDevice, st),
              "vs: fallback");
   }
@@ -397,14 +407,42 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   for (int f0 = 0; f0 < nf; f0 += step) {
     const int nc = std::min(step, nf - f0);
     const int nc_pad = (int)round_up(std::max(nc, kGemvMaxQ), kBQ);
-    int rc = run_topk(idx, mode, q2 + (int64_t)f0 * idx->ld, nullptr, a2 + f0, nc, nc_pad, k, -1,
-                      min_score, D2 + (int64_t)f0 * k, I2 + (int64_t)f0 * k, st, xaux,
+    int rc = run_topk(idx, mode, q2 + (int64_t)f0 * idx->ld, nullptr, a2 + f0, nc, nc_pad, kf, -1,
+                      min_score, D2 + (int64_t)f0 * kf, I2 + (int64_t)f0 * kf, st, xaux,
                       VS_ENGINE_BF16X3);
     if (rc) return rc;
   }
   {
     std::lock_guard<std::mutex> g(g_timer_mu);
     g_timer_kernel = "gemm_topk_x2f";  // the fallback is part of this engine's search
+  }
+  if (self0 >= 0) {  // drop each query's own row (first occurrence), keep k entries
+    std::vector<float> dh((size_t)nf * kf), dk((size_t)nf * k);
+    std::vector<int64_t> ih((size_t)nf * kf), ik((size_t)nf * k);
+    VS_HIP(hipMemcpyAsync(dh.data(), D2, dh.size() * sizeof(float), hipMemcpyDeviceToHost, st),
+           "vs: fallback");
+    VS_HIP(hipMemcpyAsync(ih.data(), I2, ih.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st),
+           "vs: fallback");
+    VS_HIP(hipStreamSynchronize(st), "vs: fallback");
+    for (int i = 0; i < nf; ++i) {
+      const int64_t self = idx->id_base + self0 + F[i];
+      int o = 0;
+      bool dropped = false;
+      for (int j = 0; j < kf && o < k; ++j) {
+        if (!dropped && ih[(size_t)i * kf + j] == self) {
+          dropped = true;
+          continue;
+        }
+        dk[(size_t)i * k + o] = dh[(size_t)i * kf + j];
+        ik[(size_t)i * k + o] = ih[(size_t)i * kf + j];
+        ++o;
+      }
+    }
+    VS_HIP(hipMemcpyAsync(D2, dk.data(), dk.size() * sizeof(float), hipMemcpyHostToDevice, st),
+           "vs: fallback");
+    VS_HIP(hipMemcpyAsync(I2, ik.data(), ik.size() * sizeof(int64_t), hipMemcpyHostToDevice, st),
+           "vs: fallback");
+    VS_HIP(hipStreamSynchronize(st), "vs: fallback");  // dk / ik leave scope
   }
   for (int i = 0; i < nf; ++i) {
     VS_HIP(hipMemcpyAsync(D + (int64_t)F[i] * k, D2 + (int64_t)i * k, (size_t)k * sizeof(float),
@@ -502,7 +540,9 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
   const int KF = x2f_list_len(need);
   const bool library_choice = engine == VS_ENGINE_AUTO;
   if (engine == VS_ENGINE_AUTO) engine = KF > 0 ? VS_ENGINE_BF16X2_VERIFY : VS_ENGINE_BF16X3;
-  if (engine == VS_ENGINE_BF16X2_VERIFY && (KF == 0 || self0 >= 0 || mode == MODE_COS))
+  // the filter pass: IP / L2 searches, and cosine self-joins from blocked rows
+  if (engine == VS_ENGINE_BF16X2_VERIFY &&
+      (KF == 0 || (mode == MODE_COS && (self0 < 0 || x2f_source() != 0))))
     engine = VS_ENGINE_BF16X3;
   // Adaptive: a query falls back when its top scores crowd inside the filter's
   // error bound.  The filter pass costs ~0.53 of the exact engine, so once the
@@ -517,7 +557,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     const int xd = x2f_source();
     if (xd ? ensure_planes(idx, st) : ensure_blocked(idx, st))
       return run_filter_verify(idx, mode, qbuf, qaux, nq, nq_pad, k, need, KF, min_score, D, I,
-                               st, xaux, xd);
+                               st, xaux, xd, self0);
   }
   const int KR = x3_list_len(need);
   if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KR > 0 && ensure_blocked(idx, st)) {

@@ -533,6 +533,8 @@ static hipError_t x3_dispatch(int mode, int np, int xd, const X3Args& a, Partial
     if (np == 2 && mode == MODE_L2)
       return xd ? x3_launch<KR, MODE_L2, 2, 1>(a, part, st, ndispatch)
                 : x3_launch<KR, MODE_L2, 2, 0>(a, part, st, ndispatch);
+    if (np == 2 && mode == MODE_COS && xd == 0 && KR == 16)
+      return x3_launch<KR, MODE_COS, 2, 0>(a, part, st, ndispatch);
   }
   return hipErrorInvalidValue;
 }
@@ -546,7 +548,9 @@ int x3_list_len(int need) {
 
 // Filter pass: number of merged approximate candidates for `need` exact entries,
 // a margin of at least 8 beyond the entries the merge needs (0 = unsupported).
-int x2f_list_len(int need) { return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : 0; }
+int x2f_list_len(int need) {
+  return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : need + 8 <= 64 ? 64 : 0;
+}
 
 // Per-lane list length of the filter pass.  A lane list does not have to hold
 // all KF candidates: a full list's last entry bounds every row the lane dropped,
@@ -616,6 +620,17 @@ double x2f_bound_coef(int64_t ld) {
   return (drop + gamma * 1.0235) * (1.0 + 1e-6);
 }
 
+// Cosine keys -(s * qinv * xinv), qinv/xinv = 1/sqrt of the stored squared norms
+// (those norms carry up to gamma(ld) relative error, so |q| * qinv <= 1 + 1.1 gamma):
+// |key_a - key_e| <= coef |q||x| qinv xinv (1 + u) + two roundings of |key| <~ 1,
+// i.e. <= (coef + 2^-22)(1 + 3 gamma(ld)), independent of the rows.
+double x2f_cos_key_bound(int64_t ld) {
+  const double u = std::ldexp(1.0, -23);
+  const double n = (double)ld;
+  const double gamma = n * u / (1.0 - n * u);
+  return (x2f_bound_coef(ld) + std::ldexp(1.0, -22)) * (1.0 + 3.0 * gamma) * (1.0 + 1e-6);
+}
+
 __global__ __launch_bounds__(256) void max_norm_kernel(const float* __restrict__ norms, int64_t n,
                                                        unsigned* __restrict__ out) {
   unsigned m = 0;  // non-negative floats (and NaN, above them) order as their bits
@@ -643,7 +658,8 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
     const float* __restrict__ qn, int64_t ld, double coef, const unsigned* __restrict__ xmax2,
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
-    float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail) {
+    float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
+    const float* __restrict__ qinv, const float* __restrict__ xinv) {
   __shared__ float ek[64];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
@@ -687,7 +703,10 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
       const float ip = (float)acc;
-      ek[j] = MODE == MODE_L2 ? l2_from_ip(qn[q], xn[r], ip) : -ip;
+      // the filter epilogue's key formulas (topk_body), on the exact dot product
+      ek[j] = MODE == MODE_L2    ? l2_from_ip(qn[q], xn[r], ip)
+              : MODE == MODE_COS ? -(ip * (qinv[q] * xinv[r]))
+                                 : -ip;
     }
   }
   __syncthreads();
@@ -718,6 +737,8 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
   double bkey = coef * sqrt(qn2) * sqrt(xm2);
   if constexpr (MODE == MODE_L2)  // key = (|q|^2 + |x|^2) - 2 ip, each side rounded
     bkey = 2.0 * bkey + 8.0 * std::ldexp(1.0, -24) * (qn2 + xm2);
+  if constexpr (MODE == MODE_COS)  // scale-free: the host passes the whole key bound
+    bkey = coef;
   const bool pass = !bounded || ((double)T - bkey > (double)eM && isfinite(T) && isfinite(eM) &&
                                   isfinite(bkey));
   if (lane == 0) fail[q] = pass ? 0 : 1;
@@ -727,7 +748,8 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  const int64_t* Ik, const float* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, double coef,
                                  const unsigned* xmax2, Partials lists, int L, float* okey,
-                                 int* oid, int KP, int* fail, hipStream_t st) {
+                                 int* oid, int KP, int* fail, hipStream_t st, const float* qinv,
+                                 const float* xinv) {
   if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
       L > lists.KP)
     return hipErrorInvalidValue;
@@ -735,11 +757,15 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
   if (mode == MODE_IP)
     hipLaunchKernelGGL(verify_rescore_kernel<MODE_IP>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
                        X, xn, Q, qn, ld, coef, xmax2, lists.key, lists.id, lists.P, lists.KP, L,
-                       okey, oid, KP, fail);
+                       okey, oid, KP, fail, qinv, xinv);
   else if (mode == MODE_L2)
     hipLaunchKernelGGL(verify_rescore_kernel<MODE_L2>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
                        X, xn, Q, qn, ld, coef, xmax2, lists.key, lists.id, lists.P, lists.KP, L,
-                       okey, oid, KP, fail);
+                       okey, oid, KP, fail, qinv, xinv);
+  else if (mode == MODE_COS && qinv && xinv)
+    hipLaunchKernelGGL(verify_rescore_kernel<MODE_COS>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik,
+                       X, xn, Q, qn, ld, coef, xmax2, lists.key, lists.id, lists.P, lists.KP, L,
+                       okey, oid, KP, fail, qinv, xinv);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

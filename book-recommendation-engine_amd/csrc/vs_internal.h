@@ -92,6 +92,7 @@ hipError_t launch_gemm_topk_x3(int KR, int mode, int np, int xd, const X3Args& a
                                hipStream_t st, int* ndispatch);
 // |approx - exact| <= coef * |x| * |q| for the filter pass over ld K elements.
 double x2f_bound_coef(int64_t ld);
+double x2f_cos_key_bound(int64_t ld);
 // *out = bits of max(norms[0..n)) (norms >= 0; NaN propagates as the maximum).
 hipError_t launch_max_norm(const float* norms, int64_t n, unsigned* out, hipStream_t st);
 // Checks and rescores the filter candidates (see vs_gemm_x3.hip): Dk/Ik hold the
@@ -103,7 +104,8 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  const int64_t* Ik, const float* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, double coef,
                                  const unsigned* xmax2, Partials lists, int L, float* okey,
-                                 int* oid, int KP, int* fail, hipStream_t st);
+                                 int* oid, int KP, int* fail, hipStream_t st,
+                                 const float* qinv = nullptr, const float* xinv = nullptr);
 // Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's np query planes
 // (np x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
 hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, int np,

@@ -174,6 +174,33 @@ def test_selfjoin_random(vf, k):
     np.testing.assert_allclose(S[ok], Sr[ok], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("k", [10, 50])
+def test_selfjoin_filter_fallback_drops_self(vf, k):
+    """Cosine self-join through the filter engine with 40-fold duplicated rows: the
+    tied candidates cannot be separated by the bound, those students are redone
+    as plain searches for k + 1 and lose their own row; parity with the oracle."""
+    from vsearch import _lib
+
+    base = _rand(30, 96, 72)
+    x = np.concatenate([np.repeat(base, 40, axis=0), _rand(600, 96, 73)])
+    index = vf.IndexFlatIP(96)
+    index.set_engine("bf16x2v")
+    index.add(x)
+    _lib.filter_stats(reset=True)
+    S, I = index.selfjoin(k)
+    nq, nfb = _lib.filter_stats(reset=True)
+    assert nq == x.shape[0]
+    if k == 10:  # 39 exact ties at similarity 1: every duplicated row falls back
+        assert nfb >= 1000
+    Sr, Ir = flat.pgvector_cosine_topk(x, k)
+    assert not (I == np.arange(x.shape[0])[:, None]).any()
+    diff = I != Ir
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5, (q, j)
+    ok = ~diff & (I >= 0)
+    np.testing.assert_allclose(S[ok], Sr[ok], rtol=1e-5, atol=1e-6)
+
+
 def test_selfjoin_threshold_and_subrange(vf):
     rng = np.random.default_rng(15)
     base = rng.standard_normal((40, 32)).astype(np.float32)
@@ -424,7 +451,7 @@ def test_blocked_rows_follow_mutations(vf, engine):
     assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("engine", ["fp32", "bf16x3", "bf16x2v"])
 def test_selfjoin_engines(vf, engine):
     x = _rand(2000, 256, 44)
     index = vf.IndexFlatIP(256)
