@@ -407,12 +407,28 @@ def run_selfjoin(args, ctx):
         index.selfjoin_device(k, lo, nq, D.data_ptr(), I.data_ptr(), stream=ctx.stream)
         return None
 
+    ctx.lib.filter_stats(reset=True)
     elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
+    fq, ff = ctx.lib.filter_stats(reset=True)
     Ih = I.cpu()
     sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
         (Ih == torch.arange(lo, hi)[:, None]).any())
     flops_step = 2.0 * N * d * nq
     kname = ctx.lib.timer_kernel()
+    exact_check = None
+    if kname == "gemm_topk_x2f":
+        # the first 256 students again through the fp32 MFMA engine: ids must agree
+        nchk = min(nq, 256)
+        De = torch.empty((nchk, k), dtype=torch.float32, device="cuda")
+        Ie = torch.empty((nchk, k), dtype=torch.int64, device="cuda")
+        index.set_engine("fp32")
+        index.selfjoin_device(k, lo, nchk, De.data_ptr(), Ie.data_ptr(), stream=ctx.stream)
+        index.set_engine("auto")
+        torch.cuda.synchronize()
+        rows = int((Ie.cpu() != Ih[:nchk]).any(dim=1).sum())
+        exact_check = {"students": nchk, "engine": "fp32", "rows_with_id_mismatch": rows,
+                       "max_abs_sim_diff": float((De - D[:nchk]).abs().max())}
+        sane &= rows == 0
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     esz = 4 if args.dtype == "f32" else 2
     rf = roofline(mfma_kind(kname, esz), flops_step * args.steps, kms, nl,
@@ -424,6 +440,10 @@ def run_selfjoin(args, ctx):
                          "ntotal": N, "d": d, "k": k,
                          "parallelism": f"replicated corpus, query rows split x{ctx.world}"}
         res["roofline"] = rf
+        if fq:
+            res["filter_verify"] = {"students": fq, "fallback_students": ff,
+                                    "fallback_rate": round(ff / fq, 6),
+                                    "exact_check": exact_check}
         res["result_sane"] = sane
         res["cpu_baseline"] = None
         return res
