@@ -425,10 +425,16 @@ def run_selfjoin(args, ctx):
         index.selfjoin_device(k, lo, nchk, De.data_ptr(), Ie.data_ptr(), stream=ctx.stream)
         index.set_engine("auto")
         torch.cuda.synchronize()
-        rows = int((Ie.cpu() != Ih[:nchk]).any(dim=1).sum())
+        diff = Ie.cpu() != Ih[:nchk]
+        rows = int(diff.any(dim=1).sum())
+        # a label may differ only where the two similarities tie within fp32 error
+        # (the fp32 engine's own rounding; DESIGN.md §4.1 tolerance)
+        dsim = (De - D[:nchk]).abs().cpu()
+        beyond = int((diff & (dsim > 1e-5)).any(dim=1).sum())
         exact_check = {"students": nchk, "engine": "fp32", "rows_with_id_mismatch": rows,
-                       "max_abs_sim_diff": float((De - D[:nchk]).abs().max())}
-        sane &= rows == 0
+                       "rows_beyond_tie_tolerance": beyond,
+                       "max_abs_sim_diff": float(dsim.max())}
+        sane &= beyond == 0
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     esz = 4 if args.dtype == "f32" else 2
     rf = roofline(mfma_kind(kname, esz), flops_step * args.steps, kms, nl,
