@@ -288,7 +288,8 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
 // the usual merge emits (D, I).  Flagged queries are redone by the exact engine.
 int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq,
                       int nq_pad, int k, int need, int KF, float min_score, float* D, int64_t* I,
-                      hipStream_t st, const float* xaux, int xd, int64_t self0) {
+                      hipStream_t st, const float* xaux, int xd, int64_t self0,
+                      int level = 0) {
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
   X3Args a;
@@ -367,18 +368,24 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   std::vector<int> F;
   for (int q = 0; q < nq; ++q)
     if (fh[q]) F.push_back(q);
+  const int nf = (int)F.size();
+  // More than 32 flagged queries (and room for more candidates): a second filter
+  // pass over just those, keeping 64 candidates, settles most of them for about
+  // 1/16 of a full pass per 256 queries; what it cannot settle goes to the exact
+  // engine.  The stats count queries that reach the exact engine.
+  const bool second = level == 0 && self0 < 0 && KF < 64 && x2f_list_len(need) > 0 &&
+                      need + 8 <= 64 && nf > 32;
   {
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_filter_queries += nq;
-    g_filter_fallbacks += (int64_t)F.size();
+    if (level == 0) g_filter_queries += nq;
+    if (!second) g_filter_fallbacks += nf;
   }
-  {
+  if (level == 0) {
     std::lock_guard<std::mutex> g(idx->x2v_mu);
     const double w = std::min(1.0, nq / 1024.0) * 0.5;  // small batches move it less
-    idx->x2v_fallback = (1.0 - w) * idx->x2v_fallback + w * ((double)F.size() / nq);
+    idx->x2v_fallback = (1.0 - w) * idx->x2v_fallback + w * ((double)nf / nq);
   }
   if (F.empty()) return VS_OK;
-  const int nf = (int)F.size();
   // self-joins: the flagged queries are not consecutive rows, so they are redone
   // as plain searches for k + 1 and their own row is dropped afterwards
   const int kf = self0 >= 0 ? k + 1 : k;
@@ -401,10 +408,15 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
       VS_HIP(hipMemcpyAsync(a2 + i, qaux + F[i], sizeof(float), hipMemcpyDeviceToDevice, st),
              "vs: fallback");
   }
+  if (second) {
+    int rc = run_filter_verify(idx, mode, q2, a2, nf, nf_pad, k, need, 64, min_score, D2, I2, st,
+                               xaux, xd, -1, 1);
+    if (rc) return rc;
+  }
   // a few queries: 16 at a time through the small-batch kernels (one corpus
   // stream each); more: one exact-engine launch
   const int step = nf <= 64 ? 16 : nf;
-  for (int f0 = 0; f0 < nf; f0 += step) {
+  for (int f0 = 0; f0 < (second ? 0 : nf); f0 += step) {
     const int nc = std::min(step, nf - f0);
     const int nc_pad = (int)round_up(std::max(nc, kGemvMaxQ), kBQ);
     int rc = run_topk(idx, mode, q2 + (int64_t)f0 * idx->ld, nullptr, a2 + f0, nc, nc_pad, kf, -1,

@@ -595,3 +595,28 @@ def test_auto_engine_adapts_to_fallback_rate(vf):
         assert not bad, bad[:5]
     assert filtered[0] == 1024  # first search: filter pass, (nearly) all fall back
     assert sum(1 for f in filtered[1:] if f) <= 2  # then the exact engine, re-probes only
+
+
+def test_bf16x2v_second_pass_settles_near_duplicates(vf):
+    """24 near-copies of every base row: with 24 candidates the bound cannot
+    separate a query's copies, with 64 it can (the next rows are far below), so
+    the second filter pass settles every flagged query and none reaches the exact
+    engine; results keep oracle parity."""
+    from vsearch import _lib
+
+    base = _rand(40, 64, 74)
+    xb = np.repeat(base, 24, axis=0) + 1e-4 * _rand(960, 64, 75)
+    xb = np.concatenate([xb, _rand(2000, 64, 76)])
+    xq = base + 1e-4 * _rand(40, 64, 77)
+    xq = np.concatenate([xq, _rand(216, 64, 78)])
+    index = vf.IndexFlatIP(64)
+    index.set_engine("bf16x2v")
+    index.add(xb)
+    _lib.filter_stats(reset=True)
+    D, I = index.search(xq, 10)
+    nq, n_exact = _lib.filter_stats(reset=True)
+    assert nq == xq.shape[0]
+    assert n_exact == 0
+    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+    assert not bad, bad[:5]
