@@ -604,11 +604,11 @@ def test_bf16x2v_second_pass_settles_near_duplicates(vf):
     engine; results keep oracle parity."""
     from vsearch import _lib
 
-    base = _rand(40, 64, 74)
-    xb = np.repeat(base, 24, axis=0) + 1e-4 * _rand(960, 64, 75)
+    base = _rand(60, 64, 74)
+    xb = np.repeat(base, 24, axis=0) + 1e-4 * _rand(1440, 64, 75)
     xb = np.concatenate([xb, _rand(2000, 64, 76)])
-    xq = base + 1e-4 * _rand(40, 64, 77)
-    xq = np.concatenate([xq, _rand(216, 64, 78)])
+    xq = base + 1e-4 * _rand(60, 64, 77)
+    xq = np.concatenate([xq, _rand(196, 64, 78)])
     index = vf.IndexFlatIP(64)
     index.set_engine("bf16x2v")
     index.add(xb)
