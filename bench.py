@@ -314,6 +314,7 @@ def run_knn(args, ctx):
     ctx.lib.filter_stats(reset=True)
     elapsed, kms, nl, (D, I) = ctx.timed(
         lambda i: index.search_device(xq, k, stream=ctx.stream), args.steps, args.warmup)
+    fw = ctx.lib.filter_wide_stats()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
@@ -378,7 +379,7 @@ def run_knn(args, ctx):
             "kernel": kname}
         res["roofline"] = rf
         if fq:
-            res["filter_verify"] = {"queries": fq, "fallback_queries": ff,
+            res["filter_verify"] = {"queries": fq, "wide_checked": fw, "fallback_queries": ff,
                                     "fallback_rate": round(ff / fq, 6), "exact_check": exact_check}
         res["batch1"] = batch1
         res["cpu_baseline"] = cpu
@@ -409,6 +410,7 @@ def run_selfjoin(args, ctx):
 
     ctx.lib.filter_stats(reset=True)
     elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
+    fw = ctx.lib.filter_wide_stats()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Ih = I.cpu()
     sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
@@ -447,7 +449,7 @@ def run_selfjoin(args, ctx):
                          "parallelism": f"replicated corpus, query rows split x{ctx.world}"}
         res["roofline"] = rf
         if fq:
-            res["filter_verify"] = {"students": fq, "fallback_students": ff,
+            res["filter_verify"] = {"students": fq, "wide_checked": fw, "fallback_students": ff,
                                     "fallback_rate": round(ff / fq, 6),
                                     "exact_check": exact_check}
         res["result_sane"] = sane

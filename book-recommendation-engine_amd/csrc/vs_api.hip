@@ -123,6 +123,16 @@ const char* g_timer_kernel = "";
 // filter-and-verify statistics (vs_filter_stats)
 int64_t g_filter_queries = 0;
 int64_t g_filter_fallbacks = 0;
+int64_t g_filter_wide = 0;  // flagged queries given to launch_verify_wide
+
+// The wide verification of flagged queries (VS_X2F_WIDE=0 turns it off, for A/B).
+bool x2f_wide_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("VS_X2F_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 struct KernelTimer {
   hipEvent_t a = nullptr, b = nullptr;
@@ -297,9 +307,10 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   const int nqt = a.nq_pad / kX3Q;
   const int ntiles = (ntotal + kX3Q - 1) / kX3Q;
   const int L = x2f_lane_len();  // lane list length (<= KF)
-  // enough lists that their 2*nsplit*L entries cover 2*KF candidates (KF = 64:
-  // four database splits even when the query tiles alone fill the chip)
-  a.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, (KF + L - 1) / L),
+  // enough lists that their 2*nsplit*L entries cover 4*KF candidates (KF = 64:
+  // eight database splits even when the query tiles alone fill the chip), so the
+  // list floors sit well behind the KF-th candidate for the wide check
+  a.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, (2 * KF + L - 1) / L),
                                     std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
   a.nsplit = std::max(a.nsplit, 1);
   Partials part;
@@ -358,9 +369,8 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
                                fail_d, st, mode == MODE_COS ? qaux : nullptr,
                                mode == MODE_COS ? xaux : nullptr),
          "vs: verify");
-  VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st),
-         "vs: merge");
-  // queries the bound could not settle: the exact engine (rare)
+  // queries the bound could not settle on KF candidates: rescore every lane-list
+  // entry below the list floors (launch_verify_wide), then the rest go on below
   std::vector<int> fh(nq);
   VS_HIP(hipMemcpyAsync(fh.data(), fail_d, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st),
          "vs: verify flags");
@@ -368,6 +378,29 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   std::vector<int> F;
   for (int q = 0; q < nq; ++q)
     if (fh[q]) F.push_back(q);
+  if (!F.empty() && x2f_wide_enabled()) {
+    int* qlist = nullptr;
+    VS_HIP(scr.alloc((void**)&qlist, F.size() * sizeof(int)), "vs: scratch");
+    VS_HIP(hipMemcpyAsync(qlist, F.data(), F.size() * sizeof(int), hipMemcpyHostToDevice, st),
+           "vs: verify list");
+    VS_HIP(launch_verify_wide(mode, (int)F.size(), qlist, KF, need, (const float*)idx->codes,
+                              idx->norms, qbuf, qn, idx->ld, coef, xmax2, part, L, vp.key, vp.id,
+                              vp.KP, fail_d, st, mode == MODE_COS ? qaux : nullptr,
+                              mode == MODE_COS ? xaux : nullptr),
+           "vs: verify wide");
+    VS_HIP(hipMemcpyAsync(fh.data(), fail_d, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st),
+           "vs: verify flags");
+    VS_HIP(hipStreamSynchronize(st), "vs: verify flags");  // qlist's copy is done too
+    {
+      std::lock_guard<std::mutex> g(g_timer_mu);
+      g_filter_wide += (int64_t)F.size();
+    }
+    F.clear();
+    for (int q = 0; q < nq; ++q)
+      if (fh[q]) F.push_back(q);
+  }
+  VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st),
+         "vs: merge");
   const int nf = (int)F.size();
   // More than 32 flagged queries (and room for more candidates): a second filter
   // pass over just those, keeping 64 candidates, settles most of them for about
@@ -1110,7 +1143,14 @@ int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
   std::lock_guard<std::mutex> g(g_timer_mu);
   *queries = g_filter_queries;
   *fallbacks = g_filter_fallbacks;
-  if (reset) g_filter_queries = g_filter_fallbacks = 0;
+  if (reset) g_filter_queries = g_filter_fallbacks = g_filter_wide = 0;
+  return VS_OK;
+}
+
+int vs_filter_wide_stats(int64_t* wide) {
+  if (!wide) return fail(VS_E_INVALID, "vs_filter_wide_stats: null output");
+  std::lock_guard<std::mutex> g(g_timer_mu);
+  *wide = g_filter_wide;
   return VS_OK;
 }
 

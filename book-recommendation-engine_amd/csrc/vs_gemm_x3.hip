@@ -771,6 +771,147 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
   return hipGetLastError();
 }
 
+// Wide verification of a flagged query (one 256-thread workgroup each).  The
+// condition above only needs a threshold T such that every row outside the
+// rescored set has approximate key >= T: the smallest last entry of the full lane
+// lists is one (a full list dropped only rows lexicographically after its last
+// entry), and then the set may be *all* list entries below T, not just the KF
+// merged ones.  Each of the P lists sees 1/P of the rows, so its 16th entry sits
+// near overall rank 16·P and T, their minimum, a few hundred rows deep (C3: P =
+// 32), far behind the KF-th; queries whose best keys crowd within
+// the bound (near-duplicates, clustered embeddings) are settled here without a
+// second pass over the corpus.  More than kWideCap entries below T, fewer than M,
+// or a non-finite key: the query stays flagged.
+template <int MODE>
+__global__ __launch_bounds__(256) void verify_wide_kernel(
+    const int* __restrict__ qlist, int KF, int M, const float* __restrict__ X,
+    const float* __restrict__ xn, const float* __restrict__ Q, const float* __restrict__ qn,
+    int64_t ld, double coef, const unsigned* __restrict__ xmax2, const float* __restrict__ lkey,
+    const int* __restrict__ lid, int P, int LKP, int L, float* __restrict__ okey,
+    int* __restrict__ oid, int KP, int* __restrict__ fail, const float* __restrict__ qinv,
+    const float* __restrict__ xinv) {
+  __shared__ float ck[kWideCap];
+  __shared__ int cid[kWideCap];
+  __shared__ float wT[4];
+  __shared__ int wB[4];
+  __shared__ int cnt, bad;
+  __shared__ float eMs;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q = qlist[blockIdx.x];
+  const int64_t lbase = (int64_t)q * P * LKP;
+  float T = FLT_MAX;
+  bool bounded = false;
+  for (int j = tid; j < P; j += 256) {
+    const int64_t o = lbase + (int64_t)j * LKP + L - 1;
+    if (lid[o] >= 0) {
+      bounded = true;
+      T = fminf(T, lkey[o]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) T = fminf(T, __shfl_xor(T, o));
+  bounded = __any(bounded);
+  if (lane == 0) {
+    wT[wv] = T;
+    wB[wv] = bounded ? 1 : 0;
+  }
+  if (tid == 0) {
+    cnt = 0;
+    bad = 0;
+    eMs = FLT_MAX;
+  }
+  __syncthreads();
+  T = fminf(fminf(wT[0], wT[1]), fminf(wT[2], wT[3]));
+  bounded = (wB[0] | wB[1] | wB[2] | wB[3]) != 0;
+  // gather every entry below T (all entries when no list is full)
+  for (int j = tid; j < P * L; j += 256) {
+    const int64_t o = lbase + (int64_t)(j / L) * LKP + j % L;
+    const int r = lid[o];
+    if (r >= 0 && (!bounded || lkey[o] < T)) {
+      const int s = atomicAdd(&cnt, 1);
+      if (s < kWideCap) cid[s] = r;
+    }
+  }
+  __syncthreads();
+  const int n = cnt;
+  if (n > kWideCap || n < M || !isfinite(T)) return;  // uniform: stays flagged
+  // exact keys, one candidate per wave at a time (fp64 accumulation, as above)
+  const float* qrow = Q + (int64_t)q * ld;
+  for (int j = wv; j < n; j += 4) {
+    const int r = cid[j];
+    const float* xr = X + (int64_t)r * ld;
+    double acc = 0.0;
+    for (int64_t c = lane * 4; c < ld; c += 256) {
+      const f32x4 xv = *(const f32x4*)(xr + c);
+      const f32x4 qv = *(const f32x4*)(qrow + c);
+      acc = fma((double)xv.x, (double)qv.x, acc);
+      acc = fma((double)xv.y, (double)qv.y, acc);
+      acc = fma((double)xv.z, (double)qv.z, acc);
+      acc = fma((double)xv.w, (double)qv.w, acc);
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      const float ip = (float)acc;
+      const float key = MODE == MODE_L2    ? l2_from_ip(qn[q], xn[r], ip)
+                        : MODE == MODE_COS ? -(ip * (qinv[q] * xinv[r]))
+                                           : -ip;
+      ck[j] = key;
+      if (!isfinite(key)) bad = 1;
+    }
+  }
+  __syncthreads();
+  if (bad) return;  // uniform
+  // rank of each (key, row) among the n (rows are distinct: the lists are disjoint)
+  float* ok = okey + (int64_t)q * KP;
+  int* oi = oid + (int64_t)q * KP;
+  for (int j = tid; j < n; j += 256) {
+    const float kj = ck[j];
+    const int ij = cid[j];
+    int rank = 0;
+    for (int t = 0; t < n; ++t) rank += lex_less(ck[t], cid[t], kj, ij) ? 1 : 0;
+    if (rank < KF) {
+      ok[rank] = kj;
+      oi[rank] = ij;
+    }
+    if (rank == M - 1) eMs = kj;
+  }
+  for (int j = min(n, KF) + tid; j < KP; j += 256) {
+    ok[j] = FLT_MAX;
+    oi[j] = -1;
+  }
+  __syncthreads();
+  const float eM = eMs;
+  const double qn2 = (double)qn[q];
+  const double xm2 = (double)__uint_as_float(*xmax2);
+  double bkey = coef * sqrt(qn2) * sqrt(xm2);
+  if constexpr (MODE == MODE_L2) bkey = 2.0 * bkey + 8.0 * std::ldexp(1.0, -24) * (qn2 + xm2);
+  if constexpr (MODE == MODE_COS) bkey = coef;
+  const bool pass = !bounded || ((double)T - bkey > (double)eM && isfinite(eM) && isfinite(bkey));
+  if (tid == 0 && pass) fail[q] = 0;
+}
+
+hipError_t launch_verify_wide(int mode, int nf, const int* qlist, int KF, int M, const float* X,
+                              const float* xn, const float* Q, const float* qn, int64_t ld,
+                              double coef, const unsigned* xmax2, Partials lists, int L,
+                              float* okey, int* oid, int KP, int* fail, hipStream_t st,
+                              const float* qinv, const float* xinv) {
+  if (KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
+  if (nf <= 0) return hipSuccess;
+#define VS_WIDE(MD)                                                                            \
+  hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(nf), dim3(256), 0, st, qlist, KF, M, X, xn, Q, \
+                     qn, ld, coef, xmax2, lists.key, lists.id, lists.P, lists.KP, L, okey, oid,  \
+                     KP, fail, qinv, xinv)
+  if (mode == MODE_IP)
+    VS_WIDE(MODE_IP);
+  else if (mode == MODE_L2)
+    VS_WIDE(MODE_L2);
+  else if (mode == MODE_COS && qinv && xinv)
+    VS_WIDE(MODE_COS);
+  else
+    return hipErrorInvalidValue;
+#undef VS_WIDE
+  return hipGetLastError();
+}
+
 // Splits fp32 query rows [0, n) (stride ld) into the first NP bf16 planes of the
 // MFMA B fragments: uint4 ((p*nqt + r/256)*nkb + kb)*512 + ((r%256)/32)*64 + lane,
 // lane = h*32 + r%32, holding k = 16kb + {4h..4h+3, 8+4h..8+4h+3} (the K

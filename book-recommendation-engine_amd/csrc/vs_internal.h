@@ -106,6 +106,16 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  const unsigned* xmax2, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st,
                                  const float* qinv = nullptr, const float* xinv = nullptr);
+// Second verification of the nf queries qlist[] flagged by verify_rescore: every
+// lane-list entry below the smallest full-list floor is rescored exactly (up to
+// kWideCap per query) and the condition re-checked on that wider set; passing
+// queries get their sorted exact list in okey/oid and fail[q] = 0.
+constexpr int kWideCap = 1024;
+hipError_t launch_verify_wide(int mode, int nf, const int* qlist, int KF, int M, const float* X,
+                              const float* xn, const float* Q, const float* qn, int64_t ld,
+                              double coef, const unsigned* xmax2, Partials lists, int L,
+                              float* okey, int* oid, int KP, int* fail, hipStream_t st,
+                              const float* qinv = nullptr, const float* xinv = nullptr);
 // Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's np query planes
 // (np x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
 hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, int np,

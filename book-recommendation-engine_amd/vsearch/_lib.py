@@ -73,6 +73,7 @@ SIGNATURES = {
     "vs_timer_read": (_c_int, [ctypes.POINTER(ctypes.c_double), _i64p]),
     "vs_timer_kernel": (ctypes.c_char_p, []),
     "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
+    "vs_filter_wide_stats": (_c_int, [_i64p]),
 }
 
 _lock = threading.Lock()
@@ -183,3 +184,11 @@ def filter_stats(reset: bool = False):
     f = ctypes.c_int64(0)
     check(load().vs_filter_stats(ctypes.byref(q), ctypes.byref(f), 1 if reset else 0))
     return q.value, f.value
+
+
+def filter_wide_stats() -> int:
+    """Flagged queries re-checked by the wide verification since the last
+    filter_stats reset (read it before that reset)."""
+    w = ctypes.c_int64(0)
+    check(load().vs_filter_wide_stats(ctypes.byref(w)))
+    return w.value

@@ -179,6 +179,10 @@ int vs_timer_enable(int on);
 /* Queries searched by the filter-and-verify engine and how many of them the
  * exact engine had to redo, since the last reset (reset != 0 clears them). */
 int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset);
+/* Of those queries, how many the first check flagged and the wide check (every
+ * lane-list entry below the list floors rescored) examined again, since the last
+ * vs_filter_stats reset.  Diagnostic only: no reference interface. */
+int vs_filter_wide_stats(int64_t* wide);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
 /* Name of the fused search kernel the last search launched ("gemm_topk_x2f",

@@ -620,3 +620,31 @@ def test_bf16x2v_second_pass_settles_near_duplicates(vf):
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
     bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
     assert not bad, bad[:5]
+
+
+def test_bf16x2v_wide_check_settles_scattered_near_duplicates(vf):
+    """40 near-copies of each base row, scattered over the corpus: the KF merged
+    candidates are all copies, so the first check flags those queries; every lane
+    list holds only one or two copies, so the wide check (all list entries below
+    the list floors rescored) settles them without a second pass or the exact
+    engine; results keep oracle parity."""
+    from vsearch import _lib
+
+    base = _rand(60, 64, 80)
+    xb = np.concatenate([np.repeat(base, 40, axis=0) + 1e-4 * _rand(2400, 64, 81),
+                         _rand(4000, 64, 82)])
+    xb = xb[np.random.default_rng(83).permutation(xb.shape[0])]
+    xq = np.concatenate([base + 1e-4 * _rand(60, 64, 84), _rand(196, 64, 85)])
+    for metric in (IP, L2):
+        index = vf.IndexFlat(64, metric)
+        index.set_engine("bf16x2v")
+        index.add(xb)
+        _lib.filter_stats(reset=True)
+        D, I = index.search(xq, 10)
+        wide = _lib.filter_wide_stats()
+        nq, n_exact = _lib.filter_stats(reset=True)
+        assert nq == xq.shape[0]
+        assert wide >= 60 and n_exact == 0, (metric, wide, n_exact)
+        Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        assert not bad, bad[:5]
