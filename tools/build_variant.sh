@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/../book-recommendation-engine_amd/csrc"
 sfx=$1; shift
 mkdir -p build_$sfx
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-memory-clause "$@" \
   -c vs_gemm_x3.hip -o build_$sfx/vs_gemm_x3.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../vsearch/libvsearch_$sfx.so \
   build/vs_api.o build/vs_gemm.o build_$sfx/vs_gemm_x3.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
