@@ -3,6 +3,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
                     [--ntotal N] [--batch B] [--k K] [--metric ip|l2] [--no-cpu-baseline]
 
+Ranks: under torchrun (WORLD_SIZE set) this process is one rank.  Started
+directly with --gpus N > 1, it is a launcher: it starts N fresh rank processes
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, 127.0.0.1
+rendezvous), never touches HIP itself, and exits with their status.  Rank 0
+prints the JSON line with n_gpus = the world size RCCL saw and the head-count
+of an all-gather over every rank.
+
 Workloads (BASELINE.json configs; the default is the one the metric is quoted on):
   c3  10M x 1536 fp32, batch 4096, top-10 IP.  One step = one exact search of the
       batch over the whole corpus, row-sharded over the N ranks (one process per
@@ -73,7 +80,7 @@ DEFAULTS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None)
@@ -93,7 +100,12 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=1024)
     p.add_argument("--recall-queries", type=int, default=1000)
-    a = p.parse_args()
+    p.add_argument("--cpu-batch1-rows", type=int, default=1_000_000)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher/collective rehearsal on CPU (gloo, no GPU, no kernel): "
+                        "each step all-gathers a (batch, k) list like the sharded search; "
+                        "the line carries dry_run=true and is not a measurement")
+    a = p.parse_args(argv)
     for key, val in DEFAULTS[a.workload].items():
         if getattr(a, key, None) is None:
             setattr(a, key, val)
@@ -132,7 +144,7 @@ def cpu_baseline(shard, args, xq_host):
     dt = time.perf_counter() - t0
     threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     qps_full = xq.shape[0] / dt * n / args.ntotal
-    return {
+    res = {
         "value": round(qps_full, 3),
         "unit": "queries/s",
         "cores": int(threads),
@@ -141,7 +153,77 @@ def cpu_baseline(shard, args, xq_host):
                   f"{dt:.2f} s; extrapolated x{n}/{args.ntotal} rows (flat scan is linear in N)",
         "impl": "oracle/flat.py knn_faiss_fp32: faiss BLAS branch restated "
                 "(numpy sgemm blocks + top-k), faiss-cpu not installable offline",
+        "cpu_model": cpu_model(),
+        "host_cpus_affinity": len(os.sched_getaffinity(0)),
     }
+    # the reference's live shape: one query (mcp_book_server.py:142 -> faiss
+    # sequential branch, nq < 20: one thread scans every row with a size-k heap)
+    if args.cpu_batch1_rows > 0:
+        from oracle import cfaiss
+
+        n1 = min(args.cpu_batch1_rows, n)
+        q1 = xq[:1]
+        cfaiss.knn_seq(xb[:1000], q1, args.k, metric)  # load / warm
+        t0 = time.perf_counter()
+        cfaiss.knn_seq(xb[:n1], q1, args.k, metric)
+        dt1 = time.perf_counter() - t0
+        ms_full = dt1 * 1e3 * args.ntotal / n1
+        res["batch1"] = {
+            "ms_per_query": round(ms_full, 3), "qps": round(1e3 / ms_full, 4), "cores": 1,
+            "kind": "port",
+            "sample": f"1 query x {n1} rows, {dt1:.3f} s; extrapolated x{args.ntotal}/{n1} rows",
+            "impl": "oracle/faiss_flat.c oracle_knn_seq: faiss's sequential branch (fp32 "
+                    "scalar sums + heap) on one thread, as faiss runs nq=1",
+        }
+    return res
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo", encoding="utf-8") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def launch_ranks(argv, n: int) -> int:
+    """Start n rank processes of this script and wait for them (the driver's
+    `bench.py --gpus N` form).  The parent imports nothing that touches HIP, so
+    each rank initialises its own GPU in a fresh process."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port)})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait()
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # one rank failed: the others would wait forever
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc if rc >= 0 else 1
 
 
 class Ctx:
@@ -153,25 +235,44 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dry = bool(args.dry_run)
         if self.world != args.gpus:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={self.world}; using WORLD_SIZE",
                   file=sys.stderr)
-        torch.cuda.set_device(self.local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", rank=self.rank, world_size=self.world,
-                                device_id=torch.device("cuda", self.local))
-        from vsearch import _lib
+        if self.dry:
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dev = torch.device("cpu")
+            self.lib = None
+            self.stream = 0
+        else:
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", rank=self.rank, world_size=self.world,
+                                    device_id=torch.device("cuda", self.local))
+            from vsearch import _lib
 
-        self.lib = _lib
-        self.stream = torch.cuda.current_stream().cuda_stream
+            self.dev = torch.device("cuda", self.local)
+            self.lib = _lib
+            self.stream = torch.cuda.current_stream().cuda_stream
+        # head-count over the collective itself: every rank reports (rank, device)
+        me = torch.tensor([1, self.rank, -1 if self.dry else self.local], dtype=torch.int64,
+                          device=self.dev)
+        allv = [torch.zeros_like(me) for _ in range(self.world)]
+        dist.all_gather(allv, me)
+        self.ranks_seen = int(sum(int(v[0]) for v in allv))
+        self.devices = [int(v[2]) for v in allv]
+
+    def synchronize(self):
+        if not self.dry:
+            self.torch.cuda.synchronize()
 
     def sync_all(self):
         self.dist.barrier()
-        self.torch.cuda.synchronize()
+        self.synchronize()
 
     def max_over_ranks(self, x: float) -> float:
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -188,18 +289,21 @@ class Ctx:
         last = None
         for _ in range(warmup):
             last = fn(-1)
-        self.torch.cuda.synchronize()
-        self.lib.timer_reset()
-        self.lib.timer_enable(True)
+        self.synchronize()
+        if self.lib:
+            self.lib.timer_reset()
+            self.lib.timer_enable(True)
         self.sync_all()
         t0 = time.perf_counter()
         for i in range(steps):
             last = fn(i)
-        self.torch.cuda.synchronize()
+        self.synchronize()
         self.dist.barrier()
         t1 = time.perf_counter()
-        self.lib.timer_enable(False)
-        kms, nl = self.lib.timer_read()
+        kms, nl = 0.0, 0
+        if self.lib:
+            self.lib.timer_enable(False)
+            kms, nl = self.lib.timer_read()
         return self.max_over_ranks(t1 - t0), kms, nl, last
 
 
@@ -212,6 +316,8 @@ def base_result(args, ctx, value, elapsed, unit="queries/s"):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ranks_seen": ctx.ranks_seen,
+        "devices": ctx.devices,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -390,7 +496,10 @@ def run_knn(args, ctx):
 
 def run_selfjoin(args, ctx):
     """C4: graph_refresher self-join (cosine top-k excluding self); the corpus is
-    replicated on every rank and the query rows are split (no collective)."""
+    replicated on every rank and the query rows are split.  Each step ends with
+    the writer's input on rank 0: every rank's (similarity, label) rows are
+    gathered there over RCCL (graph_refresher/main.py:386-389 inserts them from
+    one process), padded to the largest block."""
     from vsearch import faiss as vfaiss
     from vsearch.sharded import shard_bounds
 
@@ -401,11 +510,18 @@ def run_selfjoin(args, ctx):
     index.add_synthetic(N, seed=1234)
     lo, hi = shard_bounds(N, ctx.world, ctx.rank)
     nq = hi - lo
-    D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
-    I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    nmax = -(-N // ctx.world)  # largest block
+    Dp = torch.full((nmax, k), -3.0e38, dtype=torch.float32, device="cuda")
+    Ip = torch.full((nmax, k), -1, dtype=torch.int64, device="cuda")
+    D, I = Dp[:nq], Ip[:nq]
+    gD = [torch.empty_like(Dp) for _ in range(ctx.world)] if ctx.rank == 0 else None
+    gI = [torch.empty_like(Ip) for _ in range(ctx.world)] if ctx.rank == 0 else None
 
     def step(i):
         index.selfjoin_device(k, lo, nq, D.data_ptr(), I.data_ptr(), stream=ctx.stream)
+        if ctx.world > 1:  # the rows go to the one writer process
+            ctx.dist.gather(Dp, gD, dst=0)
+            ctx.dist.gather(Ip, gI, dst=0)
         return None
 
     ctx.lib.filter_stats(reset=True)
@@ -443,10 +559,24 @@ def run_selfjoin(args, ctx):
                   f"2*{N}*{d}*{nq} FLOP per step ({nq} query rows per rank)",
                   kname, traffic, tsrc)
     if ctx.rank == 0:
+        # the writer's rows: (a, b, sim) with sim >= threshold (main.py:350-354),
+        # counted from the gathered arrays of the last step (not timed)
+        if ctx.world > 1:
+            Sall = torch.cat([g[:shard_bounds(N, ctx.world, r)[1] - shard_bounds(N, ctx.world, r)[0]]
+                              for r, g in enumerate(gD)])
+            Iall = torch.cat([g[:shard_bounds(N, ctx.world, r)[1] - shard_bounds(N, ctx.world, r)[0]]
+                              for r, g in enumerate(gI)])
+        else:
+            Sall, Iall = D, I
+        writer = {"rows_gathered_on_rank0": int(Sall.shape[0]),
+                  "edges_sim_ge_0.75": int(((Iall >= 0) & (Sall >= 0.75)).sum().item()),
+                  "edges_total": int((Iall >= 0).sum().item())}
         res = base_result(args, ctx, args.steps * N / elapsed, elapsed, unit="students/s")
         res["config"] = {"workload": f"C4: self-join {N}x{d} cosine top-{k} excluding self",
                          "ntotal": N, "d": d, "k": k,
-                         "parallelism": f"replicated corpus, query rows split x{ctx.world}"}
+                         "parallelism": f"replicated corpus, query rows split x{ctx.world}, "
+                                        "RCCL gather of the rows to rank 0 (the writer)"}
+        res["writer"] = writer
         res["roofline"] = rf
         if fq:
             res["filter_verify"] = {"students": fq, "wide_checked": fw, "fallback_students": ff,
@@ -554,10 +684,32 @@ def run_c5(args, ctx):
     return None
 
 
+def run_dry(args, ctx):
+    """Launcher / collective rehearsal without a GPU (see --dry-run)."""
+    torch = ctx.torch
+    B, k = max(1, args.batch or 1), args.k
+    kin = min(2 * k - 1, 64) if args.metric == "ip" else k
+    D = torch.zeros((B, kin), dtype=torch.float32)
+    outs = [torch.empty_like(D) for _ in range(ctx.world)]
+    elapsed, _, _, _ = ctx.timed(lambda i: ctx.dist.all_gather(outs, D), args.steps, args.warmup)
+    if ctx.rank == 0:
+        res = base_result(args, ctx, args.steps * B / elapsed, elapsed)
+        res["dry_run"] = True
+        res["data"] = "none: dry run (gloo all-gather of a (batch, 2k-1) list per step, no kernel)"
+        res["config"] = {"workload": f"dry run of {args.workload.upper()}", "batch": B, "k": k,
+                         "parallelism": f"row-shard x{ctx.world} (gloo rehearsal)"}
+        return res
+    return None
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     ctx = Ctx(args)
-    if args.workload in ("c3", "c2"):
+    if args.dry_run:
+        res = run_dry(args, ctx)
+    elif args.workload in ("c3", "c2"):
         res = run_knn(args, ctx)
     elif args.workload == "c4":
         res = run_selfjoin(args, ctx)

@@ -290,7 +290,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
 
 int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
              int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
-             hipStream_t st, const float* xaux, int force_engine);
+             hipStream_t st, const float* xaux, int force_engine, int raw);
 
 // The filter-and-verify engine (vs_gemm_x3.hip): an NP = 2 pass keeps the KF
 // best approximate candidates of every query, verify_rescore_kernel proves the
@@ -298,7 +298,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
 // the usual merge emits (D, I).  Flagged queries are redone by the exact engine.
 int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq,
                       int nq_pad, int k, int need, int KF, float min_score, float* D, int64_t* I,
-                      hipStream_t st, const float* xaux, int xd, int64_t self0,
+                      hipStream_t st, const float* xaux, int xd, int64_t self0, int raw,
                       int level = 0) {
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
@@ -399,7 +399,7 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
     for (int q = 0; q < nq; ++q)
       if (fh[q]) F.push_back(q);
   }
-  VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st),
+  VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st, raw),
          "vs: merge");
   const int nf = (int)F.size();
   // More than 32 flagged queries (and room for more candidates): a second filter
@@ -443,7 +443,7 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   }
   if (second) {
     int rc = run_filter_verify(idx, mode, q2, a2, nf, nf_pad, k, need, 64, min_score, D2, I2, st,
-                               xaux, xd, -1, 1);
+                               xaux, xd, -1, raw, 1);
     if (rc) return rc;
   }
   // a few queries: 16 at a time through the small-batch kernels (one corpus
@@ -454,7 +454,7 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
     const int nc_pad = (int)round_up(std::max(nc, kGemvMaxQ), kBQ);
     int rc = run_topk(idx, mode, q2 + (int64_t)f0 * idx->ld, nullptr, a2 + f0, nc, nc_pad, kf, -1,
                       min_score, D2 + (int64_t)f0 * kf, I2 + (int64_t)f0 * kf, st, xaux,
-                      VS_ENGINE_BF16X3);
+                      VS_ENGINE_BF16X3, raw);
     if (rc) return rc;
   }
   {
@@ -504,10 +504,13 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
 // zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
 int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
              int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
-             hipStream_t st, const float* xaux, int force_engine = VS_ENGINE_AUTO) {
+             hipStream_t st, const float* xaux, int force_engine = VS_ENGINE_AUTO,
+             int raw = 0) {
   // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
-  // lowest 2k-1 (key, label) entries of every partial list to be exact.
-  const int KP = mode == MODE_IP ? kp_for(std::min(2 * k - 1, VS_MAX_K)) : kp_for(k);
+  // lowest 2k-1 (key, label) entries of every partial list to be exact; `raw`
+  // output (plain lexicographic order) needs k.
+  const bool tie_rule = mode == MODE_IP && !raw;
+  const int KP = tie_rule ? kp_for(std::min(2 * k - 1, VS_MAX_K)) : kp_for(k);
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
   Partials part;
@@ -550,7 +553,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
                               ntotal, nblocks, part, st),
            "vs: skinny_topk launch");
     tm.stop();
-    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
            "vs: merge launch");
     return VS_OK;
   }
@@ -569,7 +572,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
                             part, st),
            "vs: gemv_topk launch");
     tm.stop();
-    VS_HIP(launch_merge_partials(gmode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+    VS_HIP(launch_merge_partials(gmode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
            "vs: merge launch");
     return VS_OK;
   }
@@ -581,7 +584,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
                : idx->engine != VS_ENGINE_AUTO ? idx->engine
                                                : engine_from_env();
   // entries of each partial list the final merge needs (faiss's IP tie rule: 2k-1)
-  const int need = mode == MODE_IP ? std::min(2 * k - 1, VS_MAX_K) : k;
+  const int need = tie_rule ? std::min(2 * k - 1, VS_MAX_K) : k;
   const int KF = x2f_list_len(need);
   const bool library_choice = engine == VS_ENGINE_AUTO;
   if (engine == VS_ENGINE_AUTO) engine = KF > 0 ? VS_ENGINE_BF16X2_VERIFY : VS_ENGINE_BF16X3;
@@ -602,7 +605,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     const int xd = x2f_source();
     if (xd ? ensure_planes(idx, st) : ensure_blocked(idx, st))
       return run_filter_verify(idx, mode, qbuf, qaux, nq, nq_pad, k, need, KF, min_score, D, I,
-                               st, xaux, xd, self0);
+                               st, xaux, xd, self0, raw);
   }
   const int KR = x3_list_len(need);
   if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KR > 0 && ensure_blocked(idx, st)) {
@@ -635,7 +638,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
     VS_HIP(launch_gemm_topk_x3(KR, mode, 3, 0, a, part, st, &tm.dispatches),
            "vs: gemm_topk_x3 launch");
     tm.stop();
-    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
            "vs: merge launch");
     return VS_OK;
   }
@@ -653,7 +656,7 @@ int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const
                           nq_pad, nsplit, self0, part, st),
          "vs: gemm_topk launch");
   tm.stop();
-  VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st),
+  VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
          "vs: merge launch");
   return VS_OK;
 }
@@ -946,7 +949,8 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
       if (mode == MODE_L2)
         VS_HIP(launch_row_norms(qbuf, 4, idx->ld, 0, nq_pad, qaux, st), "vs_search: query norms");
       int rc = run_topk(idx, mode, qbuf, qb16, qaux, (int)nc, (int)nq_pad, (int)k, -1, 0.0f,
-                        Dd + c0 * k, Id + c0 * k, st, idx->norms);
+                        Dd + c0 * k, Id + c0 * k, st, idx->norms, VS_ENGINE_AUTO,
+                        (flags & VS_RAW_ORDER) ? 1 : 0);
       if (rc) return rc;
     }
   }

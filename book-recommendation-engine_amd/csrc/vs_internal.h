@@ -129,9 +129,11 @@ hipError_t launch_block_rows(const float* X, int64_t ld, int64_t r0, int64_t n, 
 hipError_t launch_split_rows(const float* X, int64_t ld, int64_t r0, int64_t n, int np,
                              uint4* XP, hipStream_t st);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
+// Inner product applies faiss's tie rule unless `raw` (plain lexicographic
+// (key, label) order, the per-shard half of an exact sharded merge).
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
-                                 hipStream_t st);
+                                 hipStream_t st, int raw = 0);
 // Shard lists [nparts][nq][k_in] (scores, int64 labels) -> [nq][k].
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts,
                               int nq, int k_in, int k, float* D, int64_t* I, hipStream_t st);

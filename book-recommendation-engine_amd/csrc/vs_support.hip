@@ -112,8 +112,8 @@ __device__ __forceinline__ void emit_result(int mode, float key, int64_t id, int
 template <int KP>
 __global__ __launch_bounds__(64) void merge_lists_kernel(
     const float* __restrict__ pkey, const int* __restrict__ pid, int P, float* __restrict__ okey,
-    int* __restrict__ oid, int P2, int emit, int k, int mode, int64_t id_base, float min_score,
-    float* __restrict__ D, int64_t* __restrict__ I, int64_t ldo) {
+    int* __restrict__ oid, int P2, int emit, int k, int mode, int raw, int64_t id_base,
+    float min_score, float* __restrict__ D, int64_t* __restrict__ I, int64_t ldo) {
   __shared__ float sk[64 * KP];
   __shared__ int si[64 * KP];
   const int lane = threadIdx.x;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64) void merge_lists_kernel(
       sk[j] = lk[j];
       si[j] = li[j];
     }
-    if (mode == MODE_IP) faiss_ip_tie_order<int>(sk, si, KP, k);
+    if (mode == MODE_IP && !raw) faiss_ip_tie_order<int>(sk, si, KP, k);
   }
   __syncthreads();
   if (lane < k) emit_result(mode, sk[lane], si[lane], id_base, min_score, D + q * ldo + lane,
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64) void merge_lists_kernel(
 
 template <int KP>
 static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t id_base,
-                               float min_score, float* D, int64_t* I, int64_t ldo,
+                               float min_score, float* D, int64_t* I, int64_t ldo, int raw,
                                hipStream_t st) {
   const float* ck = part.key;
   const int* ci = part.id;
@@ -185,7 +185,7 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
     float* ok = (float*)buf;
     int* oi = (int*)(ok + (size_t)nq * P2 * KP);
     hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, P2), dim3(64), 0, st, ck, ci, P, ok, oi,
-                       P2, 0, k, mode, id_base, min_score, D, I, ldo);
+                       P2, 0, k, mode, raw, id_base, min_score, D, I, ldo);
     e = hipGetLastError();
     if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
     tmp[cur] = buf;
@@ -195,8 +195,8 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
   }
   if (e == hipSuccess) {
     hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, 1), dim3(64), 0, st, ck, ci, P,
-                       (float*)nullptr, (int*)nullptr, 1, 1, k, mode, id_base, min_score, D, I,
-                       ldo);
+                       (float*)nullptr, (int*)nullptr, 1, 1, k, mode, raw, id_base, min_score, D,
+                       I, ldo);
     e = hipGetLastError();
   }
   if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
@@ -205,18 +205,18 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
 
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
-                                 hipStream_t st) {
+                                 hipStream_t st, int raw) {
   if (k < 1 || k > part.KP || nq < 0 || part.P < 1) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   switch (part.KP) {
     case 8:
-      return merge_levels<8>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+      return merge_levels<8>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
     case 16:
-      return merge_levels<16>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+      return merge_levels<16>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
     case 32:
-      return merge_levels<32>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+      return merge_levels<32>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
     case 64:
-      return merge_levels<64>(mode, part, nq, k, id_base, min_score, D, I, ldo, st);
+      return merge_levels<64>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
     default:
       return hipErrorInvalidValue;
   }
@@ -264,7 +264,11 @@ hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int 
                               int k_in, int k, float* D, int64_t* I, hipStream_t st) {
   if (k < 1 || k > 64 || nq < 0 || nparts < 1 || k_in < 1) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
-  const int KP = k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64;
+  // the pool keeps the lexicographically best `need` entries of all parts: k for
+  // L2; for inner product the 2k-1 that faiss's tie rule reads (capped at 64)
+  const bool asc = (mode == MODE_L2 || mode == MODE_L2D);
+  const int need = asc ? k : (2 * k - 1 < 64 ? 2 * k - 1 : 64);
+  const int KP = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 64;
   switch (KP) {
 #define VS_MERGEP_CASE(KPV)                                                                   \
   case KPV:                                                                                  \

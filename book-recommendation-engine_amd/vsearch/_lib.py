@@ -21,6 +21,7 @@ DTYPE_F32 = 0
 DTYPE_BF16 = 1
 IN_DEVICE = 1
 OUT_DEVICE = 2
+RAW_ORDER = 4
 MAX_K = 64
 ENGINE_AUTO = 0
 ENGINE_FP32_MFMA = 1

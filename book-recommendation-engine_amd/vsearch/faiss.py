@@ -201,8 +201,12 @@ class IndexFlat(Index):
         _lib.check(self._lib.vs_set_id_base(self._h, int(base)), "vs_set_id_base")
 
     # -- queries -----------------------------------------------------------------------
-    def search(self, x, k, *, D=None, I=None):
-        """faiss Index.search: returns (D float32 (n,k), I int64 (n,k))."""
+    def search(self, x, k, *, D=None, I=None, raw: bool = False):
+        """faiss Index.search: returns (D float32 (n,k), I int64 (n,k)).
+
+        ``raw=True`` returns the k lexicographically best (key, label) entries
+        instead of faiss's inner-product tie order (VS_RAW_ORDER; the per-shard
+        half of an exact sharded search, see vsearch.sharded)."""
         x = _as_f32_rows(x)
         n, d = x.shape
         assert d == self._d
@@ -219,16 +223,17 @@ class IndexFlat(Index):
         if n == 0:
             return D, I
         _lib.check(self._lib.vs_search(self._h, x.ctypes.data, n, k, D.ctypes.data,
-                                       I.ctypes.data, 0, None), "vs_search")
+                                       I.ctypes.data, _lib.RAW_ORDER if raw else 0, None),
+                   "vs_search")
         return D, I
 
     def search_device(self, xq_ptr: int, n: int, k: int, D_ptr: int, I_ptr: int,
-                      stream: int = 0) -> None:
+                      stream: int = 0, raw: bool = False) -> None:
         """Device-resident search: all buffers are device pointers on this index's
         device; asynchronous on `stream` (a hipStream_t, 0 = default stream)."""
+        flags = _lib.IN_DEVICE | _lib.OUT_DEVICE | (_lib.RAW_ORDER if raw else 0)
         _lib.check(self._lib.vs_search(self._h, ctypes.c_void_p(xq_ptr), int(n), int(k),
-                                       ctypes.c_void_p(D_ptr), ctypes.c_void_p(I_ptr),
-                                       _lib.IN_DEVICE | _lib.OUT_DEVICE,
+                                       ctypes.c_void_p(D_ptr), ctypes.c_void_p(I_ptr), flags,
                                        ctypes.c_void_p(stream)), "vs_search")
 
     def reconstruct(self, key) -> np.ndarray:

@@ -524,6 +524,15 @@ class FAISS:
                 "random site on the internet.)."
             )
         path = Path(folder_path)
+        if not (path / f"{index_name}.docstore.json").exists() and \
+                (path / f"{index_name}.pkl").exists():
+            # a store written by LangChain itself: its docstore is a pickle of
+            # LangChain classes, which this loader never unpickles
+            raise ReferenceStoreError(
+                f"{path}: found {index_name}.pkl (a LangChain pickle) but no "
+                f"{index_name}.docstore.json. Rebuild the store once from the catalog "
+                "with vsearch.langchain.full_faiss_rebuild (the reference's own "
+                "book_vector full_faiss_rebuild, main.py:428-471); the pickle is not loaded.")
         index = vfaiss.read_index(str(path / f"{index_name}.faiss"),
                                   device=kwargs.pop("device", None),
                                   index_factory=kwargs.pop("index_factory", None))
@@ -533,3 +542,24 @@ class FAISS:
                                      for k, v in payload["docstore"].items()})
         index_to_docstore_id = {int(i): _id for i, _id in payload["index_to_docstore_id"]}
         return cls(embeddings, index, docstore, index_to_docstore_id, **kwargs)
+
+
+class ReferenceStoreError(ValueError):
+    """load_local found a LangChain-written store (index.pkl docstore) that this
+    drop-in does not unpickle; see full_faiss_rebuild."""
+
+
+def full_faiss_rebuild(texts: List[str], embeddings, metadatas: List[dict], folder_path: str,
+                       ids: Optional[List[str]] = None, index_name: str = "index",
+                       **kwargs: Any) -> "FAISS":
+    """The migration path from a reference-written store: the reference's own
+    full rebuild (src/incremental_workers/book_vector/main.py:428-471: one
+    ``FAISS.from_texts`` over every catalog row with the main.py:449-466 text
+    and metadata, then ``save_local(vec_dir)``), writing this drop-in's format
+    (index.faiss + index.docstore.json) into the same directory.  Files the
+    reference wrote there (index.pkl) are left untouched and no longer read."""
+    store = FAISS.from_texts(list(texts), embeddings, metadatas=list(metadatas), ids=ids,
+                             **kwargs)
+    store.save_local(folder_path, index_name=index_name)
+    return store
+

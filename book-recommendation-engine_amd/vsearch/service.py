@@ -21,6 +21,10 @@ HBM and serves the same vector-store calls to any number of clients:
   faiss gives (concurrent ``search`` allowed, ``add`` exclusive).
 * ``RemoteFAISS(address, authkey)`` is the client: the LangChain ``FAISS`` read /
   write surface the reference's call sites use, plus ``.index.ntotal/.d/.search``.
+* Access: the HMAC auth key has no default (the caller supplies a secret);
+  ``read_only=True`` refuses every write op; ``save_local`` writes only inside
+  the ``save_root`` directory fixed when the server starts (refused when no
+  root was given), never at an arbitrary client-chosen path.
 
 Wire format: every message is one ``send_bytes`` frame = u32 header length +
 UTF-8 JSON header + raw little-endian payload (float32 vectors, int64 labels).
@@ -32,6 +36,7 @@ from __future__ import annotations
 import argparse
 import json
 import logging
+import os
 import struct
 import threading
 from multiprocessing.connection import Client, Listener
@@ -46,7 +51,14 @@ logger = logging.getLogger(__name__)
 __all__ = ["IndexService", "RemoteFAISS", "serve"]
 
 _ERRORS = {"ValueError": ValueError, "AssertionError": AssertionError, "KeyError": KeyError,
-           "TypeError": TypeError}
+           "TypeError": TypeError, "PermissionError": PermissionError}
+_WRITE_OPS = ("add_texts", "upsert_texts", "delete", "save_local")
+
+
+def _check_authkey(authkey) -> bytes:
+    if not isinstance(authkey, (bytes, bytearray)) or len(authkey) == 0:
+        raise ValueError("authkey: a non-empty bytes secret is required (no default)")
+    return bytes(authkey)
 
 
 def _pack(header: dict, payload: bytes = b"") -> bytes:
@@ -178,11 +190,14 @@ class _Coalescer:
 class IndexService:
     """Serve one resident ``FAISS`` store (index in HBM) over TCP."""
 
-    def __init__(self, store: FAISS, address=("127.0.0.1", 0), authkey: bytes = b"vsearch",
-                 max_batch: int = 4096):
+    def __init__(self, store: FAISS, address=("127.0.0.1", 0), *, authkey: bytes,
+                 max_batch: int = 4096, save_root: Optional[str] = None,
+                 read_only: bool = False):
         self.store = store
         self._lock = _RWLock()
-        self._authkey = authkey
+        self._authkey = authkey = _check_authkey(authkey)
+        self._save_root = os.path.realpath(save_root) if save_root is not None else None
+        self._read_only = bool(read_only)
         self._listener = Listener(address, backlog=128, authkey=authkey)
         self.address = self._listener.address
         self._coalescer = _Coalescer(self, max_batch)
@@ -276,9 +291,20 @@ class IndexService:
         finally:
             self._lock.release_read()
 
+    def _save_path(self, folder_path: str) -> str:
+        """save_local's target, confined to the server's save_root."""
+        if self._save_root is None:
+            raise PermissionError("save_local is disabled: the server has no save_root")
+        target = os.path.realpath(os.path.join(self._save_root, str(folder_path)))
+        if os.path.commonpath([target, self._save_root]) != self._save_root:
+            raise PermissionError(f"save_local: {folder_path!r} is outside the save root")
+        return target
+
     def _dispatch(self, h: dict, payload: memoryview):
         op = h["op"]
         st = self.store
+        if self._read_only and op in _WRITE_OPS:
+            raise PermissionError(f"{op}: the service is read-only")
         if op == "info":
             return self._read(lambda: {"ntotal": st.index.ntotal, "d": st.index.d,
                                        "metric_type": st.index.metric_type,
@@ -308,7 +334,10 @@ class IndexService:
             docs = self._read(st.get_by_ids, h["ids"])
             return {"docs": [d.to_json() for d in docs]}, b""
         if op == "save_local":
-            self._write(st.save_local, h["folder_path"], h.get("index_name", "index"))
+            name = str(h.get("index_name", "index"))
+            if os.path.basename(name) != name or name in ("", ".", ".."):
+                raise PermissionError(f"save_local: bad index_name {name!r}")
+            self._write(st.save_local, self._save_path(h["folder_path"]), name)
             return {}, b""
         if op == "reconstruct":
             v = self._read(st.index.reconstruct, int(h["key"]))
@@ -384,9 +413,9 @@ class RemoteFAISS:
     (mcp_book_server.py:142, candidate_builder.py:321, book_vector/main.py:148, ...).
     Thread-safe (one request in flight per connection)."""
 
-    def __init__(self, address, authkey: bytes = b"vsearch"):
+    def __init__(self, address, authkey: bytes):
         self._conn = Client(tuple(address) if isinstance(address, list) else address,
-                            authkey=authkey)
+                            authkey=_check_authkey(authkey))
         self._mu = threading.Lock()
         self.index = _RemoteIndex(self)
 
@@ -461,17 +490,19 @@ class RemoteFAISS:
         return self._call({"op": "delete", "ids": list(ids)})[0]["result"]
 
     def save_local(self, folder_path: str, index_name: str = "index") -> None:
+        """Saved on the server, under its save_root (folder_path is relative to it)."""
         self._call({"op": "save_local", "folder_path": str(folder_path),
                     "index_name": index_name})
 
 
-def serve(folder_path: str, embeddings, host: str = "127.0.0.1", port: int = 0,
-          authkey: bytes = b"vsearch", device: Optional[int] = None,
-          max_batch: int = 4096) -> IndexService:
+def serve(folder_path: str, embeddings, host: str = "127.0.0.1", port: int = 0, *,
+          authkey: bytes, device: Optional[int] = None, max_batch: int = 4096,
+          save_root: Optional[str] = None, read_only: bool = False) -> IndexService:
     """Load a saved store once (``FAISS.load_local``) and serve it until closed."""
     store = FAISS.load_local(folder_path, embeddings, allow_dangerous_deserialization=True,
                              device=device)
-    return IndexService(store, (host, port), authkey=authkey, max_batch=max_batch)
+    return IndexService(store, (host, port), authkey=authkey, max_batch=max_batch,
+                        save_root=save_root, read_only=read_only)
 
 
 def main(argv=None):  # pragma: no cover - CLI wrapper
@@ -481,11 +512,16 @@ def main(argv=None):  # pragma: no cover - CLI wrapper
     ap.add_argument("folder")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8765)
-    ap.add_argument("--authkey", default="vsearch")
     ap.add_argument("--device", type=int, default=None)
     ap.add_argument("--dim", type=int, default=1536)
+    ap.add_argument("--save-root", default=None, help="directory save_local may write into")
+    ap.add_argument("--read-only", action="store_true")
     a = ap.parse_args(argv)
-    svc = serve(a.folder, SynthEmbeddings(a.dim), a.host, a.port, a.authkey.encode(), a.device)
+    key = os.environ.get("VSEARCH_AUTHKEY", "")
+    if not key:
+        raise SystemExit("set VSEARCH_AUTHKEY to the shared secret (no default)")
+    svc = serve(a.folder, SynthEmbeddings(a.dim), a.host, a.port, authkey=key.encode(),
+                device=a.device, save_root=a.save_root, read_only=a.read_only)
     logger.warning("vsearch service on %s:%s", *svc.address)
     svc.serve_forever()
 

@@ -3,10 +3,17 @@
 Global labels 0..N-1 are split into contiguous blocks; rank g owns
 [off_g, off_g + n_g) and its shard reports global labels (vs_set_id_base).
 A search runs the local fused top-k on every rank, all-gathers the per-shard
-(B x k) lists over RCCL (torch.distributed backend "nccl" = RCCL on ROCm, over
-xGMI), and merges them on the GPU by (score, label) — so the result equals the
-single-index result, ties included.  The exchange is B*k*12 bytes per rank:
-latency-bound, not link-bound.
+lists over RCCL (torch.distributed backend "nccl" = RCCL on ROCm, over xGMI),
+and merges them on the GPU — so the result equals the single-index result,
+ties included:
+  * L2: each shard returns its k best by (distance, label); the k best of the
+    union are among them, in the same lexicographic order faiss's CMax heap uses.
+  * inner product: faiss's CMin heap tie rule is a function of the 2k-1
+    lexicographically best (-score, label) pairs of the whole corpus
+    (oracle/flat.py faiss_order), so each shard returns its RAW best
+    m = min(2k-1, 64) pairs (VS_RAW_ORDER, no tie rule applied) and the merge
+    (vs_merge_topk) applies the rule once to the union of those lists.
+The exchange is B*m*12 bytes per rank: latency-bound, not link-bound.
 
 Appends go to the last shard; removals compact inside each shard and shift the
 later shards' id bases, so global labels stay faiss positions.
@@ -117,12 +124,19 @@ class ShardedIndexFlat:
         return int(t.item())
 
     # -- search ---------------------------------------------------------------------
+    def shard_k(self, k: int) -> int:
+        """Entries each shard contributes to the merge (see the module docstring)."""
+        if self.metric_type == vfaiss.METRIC_INNER_PRODUCT:
+            return min(2 * int(k) - 1, _lib.MAX_K)
+        return int(k)
+
     def search(self, x, k: int):
         """Host-array convenience wrapper: same contract as IndexFlat.search."""
         import torch
 
         x = np.ascontiguousarray(x, dtype=np.float32)
-        D, I = self.shard.search(x, k)
+        kin = self.shard_k(k)
+        D, I = self.shard.search(x, kin, raw=True)
         dev = self._coll_device()
         Dt = torch.from_numpy(D).to(dev)
         It = torch.from_numpy(I).to(dev)
@@ -133,7 +147,7 @@ class ShardedIndexFlat:
             # gloo gathered host tensors: the merge itself still runs on the GPU
             gpu = torch.device("cuda", self.shard.device)
             Dall, Iall = Dall.to(gpu), Iall.to(gpu)
-        Dm, Im = self.merge_device(Dall, Iall, x.shape[0], k, k)
+        Dm, Im = self.merge_device(Dall, Iall, x.shape[0], kin, k)
         return Dm.cpu().numpy(), Im.cpu().numpy()
 
     def _gather(self, Dt, It):
@@ -166,11 +180,16 @@ class ShardedIndexFlat:
         import torch
 
         nq = xq.shape[0]
-        Dl = torch.empty((nq, k), dtype=torch.float32, device=xq.device)
-        Il = torch.empty((nq, k), dtype=torch.int64, device=xq.device)
-        self.shard.search_device(xq.data_ptr(), nq, k, Dl.data_ptr(), Il.data_ptr(), stream)
-        if self.world == 1:
+        if self.world == 1:  # the shard is the whole index: faiss order directly
+            Dl = torch.empty((nq, k), dtype=torch.float32, device=xq.device)
+            Il = torch.empty((nq, k), dtype=torch.int64, device=xq.device)
+            self.shard.search_device(xq.data_ptr(), nq, k, Dl.data_ptr(), Il.data_ptr(), stream)
             return Dl, Il
+        kin = self.shard_k(k)
+        Dl = torch.empty((nq, kin), dtype=torch.float32, device=xq.device)
+        Il = torch.empty((nq, kin), dtype=torch.int64, device=xq.device)
+        self.shard.search_device(xq.data_ptr(), nq, kin, Dl.data_ptr(), Il.data_ptr(), stream,
+                                 raw=True)
         Dall, Iall = self._gather(Dl, Il)
-        return self.merge_device(Dall, Iall, nq, k, k, stream)
+        return self.merge_device(Dall, Iall, nq, kin, k, stream)
 

@@ -69,11 +69,58 @@ def student_neighbours(keys: Sequence[str], vectors, *, k: int = DEFAULT_K,
     return rows
 
 
+class StudentIndex:
+    """Resident student vectors for per-event similarity (the similarity worker,
+    src/incremental_workers/similarity/main.py:57-102, runs one student's query
+    per STUDENT_EMBEDDING event).  The matrix is uploaded once; each event is one
+    single-row self-join on the kept index (an HBM-bound scan, no re-upload), and
+    a re-embedded student replaces its own row (the student_embeddings upsert of
+    student_embedding/main.py:120-146)."""
+
+    def __init__(self, keys: Sequence[str], vectors, *, quantize: bool = True,
+                 device: Optional[int] = None):
+        self.keys: List[str] = list(keys)
+        if len(set(self.keys)) != len(self.keys):
+            raise ValueError("StudentIndex: duplicate student keys")
+        self.quantize = quantize
+        self.index = build_student_index(vectors, quantize=quantize, device=device)
+        self._row = {key: i for i, key in enumerate(self.keys)}
+
+    def __len__(self) -> int:
+        return len(self.keys)
+
+    def neighbours_of(self, student: str, k: int = DEFAULT_K) -> List[Tuple[str, str, float]]:
+        q = self._row[student]
+        S, I = self.index.selfjoin(k, q0=q, nq=1, exclude_self=True)
+        return [(student, self.keys[int(b)], float(s)) for s, b in zip(S[0], I[0]) if b >= 0]
+
+    def neighbours(self, k: int = DEFAULT_K,
+                   threshold: Optional[float] = DEFAULT_THRESHOLD) -> List[Tuple[str, str, float]]:
+        min_sim = -np.inf if threshold is None else float(threshold)
+        S, I = self.index.selfjoin(k, exclude_self=True, min_sim=min_sim)
+        return [(self.keys[a], self.keys[int(b)], float(S[a, j]))
+                for a in range(S.shape[0]) for j, b in enumerate(I[a]) if b >= 0]
+
+    def upsert(self, student: str, vector) -> None:
+        """Insert or replace one student's vector (a removed row compacts the
+        later rows, faiss remove_ids semantics; the key list follows)."""
+        v = np.asarray(vector, dtype=np.float32).reshape(1, -1)
+        v = pgvector_quantize(v) if self.quantize else v
+        if student in self._row:
+            r = self._row.pop(student)
+            self.index.remove_ids(np.array([r], dtype=np.int64))
+            del self.keys[r]
+            self._row = {key: i for i, key in enumerate(self.keys)}
+        self.index.add(v)
+        self._row[student] = len(self.keys)
+        self.keys.append(student)
+
+
 def student_neighbours_of(student: str, keys: Sequence[str], vectors, *, k: int = DEFAULT_K,
-                          quantize: bool = True, device: Optional[int] = None):
-    """One student's rows (the similarity worker's compute_similarity)."""
-    keys = list(keys)
-    q = keys.index(student)
-    index = build_student_index(vectors, quantize=quantize, device=device)
-    S, I = index.selfjoin(k, q0=q, nq=1, exclude_self=True)
-    return [(student, keys[int(b)], float(s)) for s, b in zip(S[0], I[0]) if b >= 0]
+                          quantize: bool = True, device: Optional[int] = None,
+                          index: Optional[StudentIndex] = None):
+    """One student's rows (the similarity worker's compute_similarity).  Pass a
+    resident ``StudentIndex`` to avoid uploading the matrix on every event."""
+    if index is None:
+        index = StudentIndex(keys, vectors, quantize=quantize, device=device)
+    return index.neighbours_of(student, k)

@@ -43,6 +43,13 @@ extern "C" {
 /* Buffer-location flags. */
 #define VS_IN_DEVICE 1  /* input vectors / ids are device pointers */
 #define VS_OUT_DEVICE 2 /* output buffers are device pointers      */
+/* vs_search: return the k entries with the lexicographically smallest
+ * (key, label), key = distance (L2) or -score (IP), in that order, instead of
+ * faiss's inner-product tie order.  The per-shard half of an exact row-sharded
+ * search: faiss's IP tie rule is a function of the 2k-1 best (key, label) pairs
+ * of the union, so each shard returns its raw best 2k-1 and vs_merge_topk
+ * applies the rule once (vsearch/sharded.py).  No effect on L2. */
+#define VS_RAW_ORDER 4
 
 /* Status codes. */
 #define VS_OK 0

@@ -148,6 +148,18 @@ def knn_exact(xb, xq, k: int, metric: int):
     return select_topk(exact_scores(xb, xq, metric), k, metric)
 
 
+def knn_lex(xb, xq, k: int, metric: int):
+    """The k lexicographically best (key, label) rows, in that order, fp64
+    scores: what libvsearch returns under VS_RAW_ORDER (one shard's half of an
+    exact sharded search; faiss_order then reproduces faiss on the union)."""
+    xb = np.ascontiguousarray(xb, dtype=np.float32)
+    xq = np.ascontiguousarray(xq, dtype=np.float32)
+    if xb.shape[0] == 0:
+        return (np.full((xq.shape[0], k), neutral(metric), np.float32),
+                np.full((xq.shape[0], k), -1, np.int64))
+    return select_topk(exact_scores(xb, xq, metric), k, metric, rule="lex")
+
+
 def knn_faiss_fp32(xb, xq, k: int, metric: int, bs_x: int = 4096, bs_y: int = 65536):
     """faiss's fp32 arithmetic (BLAS branch): blocked sgemm + norms + clamp + a
     running top-k per query.  Used as the timed CPU baseline (kind "port"):

@@ -30,11 +30,14 @@ class OracleIndex:
         assert x.shape[1] == self.d
         self._x = np.concatenate([self._x, x])
 
-    def search(self, x, k):
+    def search(self, x, k, raw=False):
         x = np.ascontiguousarray(x, dtype=np.float32)
         assert x.shape[1] == self.d
         assert k > 0
-        D, I = flat.knn_exact(self._x, x, k, self.metric_type)
+        if raw:  # VS_RAW_ORDER: lexicographic (key, label), no IP tie rule
+            D, I = flat.knn_lex(self._x, x, k, self.metric_type)
+        else:
+            D, I = flat.knn_exact(self._x, x, k, self.metric_type)
         I = np.where(I >= 0, I + self._base, -1)
         return D, I
 

@@ -648,3 +648,41 @@ def test_bf16x2v_wide_check_settles_scattered_near_duplicates(vf):
         Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
         bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
         assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("nshard", [2, 3, 8])
+def test_sharded_raw_merge_exact_on_ties(vf, metric, nshard):
+    """The multi-GPU search's data flow on one device: shards (id_base = their
+    first label) return their raw lexicographic best min(2k-1, 64) (IP) or k (L2)
+    entries (VS_RAW_ORDER), vs_merge_topk applies faiss's tie rule once — labels
+    and scores equal the C faiss-heap restatement bit for bit on tie-heavy data."""
+    torch = pytest.importorskip("torch")
+    import ctypes
+
+    from vsearch import _lib
+    from vsearch.sharded import shard_bounds
+
+    xb = _rand(600, 3, 31, "int")
+    for nq in (1, 7, 40):
+        xq = _rand(nq, 3, 32 + nq, "int")
+        for k in (1, 4, 10, 16):
+            kin = min(2 * k - 1, 64) if metric == IP else k
+            parts = []
+            for r in range(nshard):
+                lo, hi = shard_bounds(600, nshard, r)
+                idx = vf.IndexFlat(3, metric)
+                idx.add(xb[lo:hi])
+                idx.set_id_base(lo)
+                parts.append(idx.search(xq, kin, raw=True))
+            Dp = torch.from_numpy(np.stack([p[0] for p in parts])).cuda()
+            Ip = torch.from_numpy(np.stack([p[1] for p in parts])).cuda()
+            D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+            I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+            _lib.check(_lib.load().vs_merge_topk(
+                ctypes.c_void_p(Dp.data_ptr()), ctypes.c_void_p(Ip.data_ptr()), nshard, nq, kin,
+                k, metric, ctypes.c_void_p(D.data_ptr()), ctypes.c_void_p(I.data_ptr()), None))
+            torch.cuda.synchronize()
+            Dc, Ic = cfaiss.knn_seq(xb, xq, k, metric)
+            np.testing.assert_array_equal(I.cpu().numpy(), Ic)
+            np.testing.assert_array_equal(D.cpu().numpy(), Dc)

@@ -87,6 +87,36 @@ def test_student_neighbours(golden, golden_vectors):
     assert one == [r for r in rows if r[0] == keys[3]]
 
 
+def test_student_index_resident_events(golden, golden_vectors):
+    """Per-event similarity on a resident StudentIndex: every event queries the
+    kept index (no re-upload), equals the oracle, and a re-embedded student's
+    row is replaced in place of a re-build."""
+    from vsearch.students import StudentIndex, pgvector_quantize
+
+    inputs, _ = golden
+    keys = list(inputs["student_keys"])
+    _, _, xs = golden_vectors
+    si = StudentIndex(keys, xs)
+    xq = pgvector_quantize(xs)
+    S, I = flat.pgvector_cosine_topk(xq, 15)
+    for a in (0, 3, 24):
+        want = [(keys[a], keys[int(b)], float(S[a, j])) for j, b in enumerate(I[a]) if b >= 0]
+        got = si.neighbours_of(keys[a], 15)
+        assert [(x, y) for x, y, _ in got] == [(x, y) for x, y, _ in want]
+        np.testing.assert_allclose([z for *_, z in got], [z for *_, z in want], rtol=1e-5,
+                                   atol=1e-6)
+    # student 5 re-embedded as a near copy of student 9: they become neighbours
+    newv = xs[9] + 0.01 * xs[5]
+    si.upsert(keys[5], newv)
+    assert len(si) == 25 and si.index.ntotal == 25
+    x2 = np.concatenate([np.delete(xs, 5, axis=0), newv[None, :]])
+    keys2 = keys[:5] + keys[6:] + [keys[5]]
+    S2, I2 = flat.pgvector_cosine_topk(pgvector_quantize(x2), 15)
+    got = si.neighbours_of(keys[5], 15)
+    assert got[0][1] == keys[9]
+    assert [y for _, y, _ in got] == [keys2[int(b)] for b in I2[24] if b >= 0]
+
+
 def test_sharded_single_rank_nccl():
     """The multi-GPU code path with world_size 1 over RCCL (merge kernel included)."""
     import os
@@ -139,21 +169,24 @@ def test_upsert_on_gpu(golden):
 
 def test_service_on_gpu(catalog_store, golden):
     """§8 f2 resident service: concurrent remote searches, coalesced into shared
-    engine calls on the HIP index, return what the in-process store returns."""
+    engine calls on the HIP index, return the golden (oracle) book order and
+    scores for every keyword — and what the in-process store returns."""
     import threading
 
     from vsearch.service import IndexService, RemoteFAISS
 
-    inputs, _ = golden
+    inputs, exp = golden
     kws = inputs["keywords"][:32]
+    pos = {m["book_id"]: i for i, m in enumerate(inputs["book_metadata"])}
     want = {kw: [(d.id, float(s)) for d, s in catalog_store.similarity_search_with_score(kw, k=5)]
             for kw in kws}
     got = {}
-    with IndexService(catalog_store) as svc:
+    key = b"gpu-test-secret"
+    with IndexService(catalog_store, authkey=key) as svc:
         barrier = threading.Barrier(8, timeout=60)
 
         def worker(qs):
-            with RemoteFAISS(svc.address) as cli:
+            with RemoteFAISS(svc.address, key) as cli:
                 barrier.wait()
                 for kw in qs:
                     got[kw] = [(d.id, float(s)) for d, s in cli.similarity_search_with_score(kw, k=5)]
@@ -166,7 +199,36 @@ def test_service_on_gpu(catalog_store, golden):
         assert svc.stats["search_rows"] == 32
     # a stacked batch may take faiss's other branch (nq >= 20: norm expansion,
     # SURVEY.md §8 a7), so scores agree to the fp32 tolerance, ids exactly
-    for kw in kws:
+    for qi, kw in enumerate(kws):
         assert [i for i, _ in got[kw]] == [i for i, _ in want[kw]]
         np.testing.assert_allclose([s for _, s in got[kw]], [s for _, s in want[kw]],
                                    rtol=1e-5, atol=1e-5)
+        # against the oracle's golden vectors (tests/golden/make_golden.py)
+        ids = [catalog_store.docstore.search(i).metadata["book_id"] for i, _ in got[kw]]
+        assert [pos[b] for b in ids] == exp["books_l2_I"][341 + qi, :5].tolist()
+        np.testing.assert_allclose([s for _, s in got[kw]], exp["books_l2_D"][341 + qi, :5],
+                                   rtol=1e-5, atol=1e-5)
+
+
+def test_reference_store_migration_on_gpu(tmp_path, golden):
+    """A reference-written directory (index.faiss + pickled index.pkl) is refused,
+    rebuilt by full_faiss_rebuild on the HIP index, and reopened by load_local
+    with the golden search order."""
+    from vsearch import langchain as vlc
+    from vsearch.synth import SynthEmbeddings
+
+    inputs, exp = golden
+    emb = SynthEmbeddings()
+    d = tmp_path / "vector_store"
+    d.mkdir()
+    (d / "index.pkl").write_bytes(b"not loaded")
+    (d / "index.faiss").write_bytes(b"IxF2")
+    with pytest.raises(vlc.ReferenceStoreError):
+        vlc.FAISS.load_local(str(d), emb, allow_dangerous_deserialization=True)
+    vlc.full_faiss_rebuild(inputs["book_texts"], emb, inputs["book_metadata"], str(d))
+    store = vlc.FAISS.load_local(str(d), emb, allow_dangerous_deserialization=True)
+    assert store.index.ntotal == 341
+    pos = {m["book_id"]: i for i, m in enumerate(inputs["book_metadata"])}
+    for qi, kw in enumerate(inputs["keywords"][:8]):
+        got = [pos[doc.metadata["book_id"]] for doc in store.similarity_search(kw, k=5)]
+        assert got == exp["books_l2_I"][341 + qi, :5].tolist()

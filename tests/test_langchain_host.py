@@ -142,6 +142,38 @@ def test_save_load_roundtrip(tmp_path, patched_indexes):
     assert loaded.similarity_search("t3", k=1)[0].metadata["book_id"] == 3
 
 
+def test_reference_written_store_migrates_by_full_rebuild(tmp_path, patched_indexes, golden):
+    """A directory as the reference leaves it (index.faiss + LangChain's pickled
+    index.pkl, book_vector/main.py:151,470): load_local refuses it without ever
+    unpickling; the reference's own full rebuild (main.py:428-471) run through
+    the drop-in rewrites it, and the rebuilt directory reopens with the same
+    rows, labels and search results."""
+    inputs, _ = golden
+    emb = SynthEmbeddings(32)
+    texts, metas = inputs["book_texts"][:40], inputs["book_metadata"][:40]
+    ref_dir = tmp_path / "vector_store"
+    ref_dir.mkdir()
+    idx = OracleIndex(32, flat.METRIC_L2)
+    idx.add(np.asarray(emb.embed_documents(texts), dtype=np.float32))
+    vfaiss.write_index(idx, str(ref_dir / "index.faiss"))
+    poison = b"\x80\x04cos\nsystem\n."  # a pickle that must never be loaded
+    (ref_dir / "index.pkl").write_bytes(poison)
+    with pytest.raises(vlc.ReferenceStoreError):
+        vlc.FAISS.load_local(str(ref_dir), emb, allow_dangerous_deserialization=True,
+                             index_factory=lambda d, m: OracleIndex(d, m))
+    built = vlc.full_faiss_rebuild(texts, emb, metas, str(ref_dir))
+    assert (ref_dir / "index.pkl").read_bytes() == poison  # untouched, not read
+    loaded = vlc.FAISS.load_local(str(ref_dir), emb, allow_dangerous_deserialization=True,
+                                  index_factory=lambda d, m: OracleIndex(d, m))
+    assert loaded.index.ntotal == 40
+    np.testing.assert_array_equal(loaded.index.reconstruct_n(0, 40), idx.reconstruct_n(0, 40))
+    assert loaded.index_to_docstore_id == built.index_to_docstore_id
+    for kw in inputs["keywords"][:5]:
+        a = [(d.id, d.metadata["book_id"]) for d in built.similarity_search(kw, k=5)]
+        b = [(d.id, d.metadata["book_id"]) for d in loaded.similarity_search(kw, k=5)]
+        assert a == b
+
+
 def test_faiss_flat_file_layout(tmp_path):
     idx = OracleIndex(3, flat.METRIC_INNER_PRODUCT)
     x = np.arange(12, dtype=np.float32).reshape(4, 3)

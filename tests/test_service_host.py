@@ -15,6 +15,8 @@ from vsearch import langchain as vlc
 from vsearch.service import IndexService, RemoteFAISS
 from vsearch.synth import SynthEmbeddings
 
+KEY = b"test-secret"
+
 
 @pytest.fixture
 def store(monkeypatch):
@@ -35,7 +37,7 @@ def _same(a, b):
 
 
 def test_remote_reads_match_local(store):
-    with IndexService(store) as svc, RemoteFAISS(svc.address) as cli:
+    with IndexService(store, authkey=KEY) as svc, RemoteFAISS(svc.address, KEY) as cli:
         assert cli.index.ntotal == 200 and cli.index.d == 48
         assert cli.index.metric_type == flat.METRIC_L2
         for q in ["book 7", "space adventure", "friendship animals"]:
@@ -66,9 +68,9 @@ def test_concurrent_searches_coalesce_and_match(store):
     got = {}
     barrier = threading.Barrier(16, timeout=30)
 
-    with IndexService(store) as svc:
+    with IndexService(store, authkey=KEY) as svc:
         def worker(qs):
-            with RemoteFAISS(svc.address) as cli:
+            with RemoteFAISS(svc.address, KEY) as cli:
                 barrier.wait()
                 for q in qs:
                     got[q] = cli.similarity_search_with_score(q, k=5)
@@ -102,11 +104,11 @@ def test_slow_engine_requests_are_stacked(store):
     want = {q: store.similarity_search_with_score(q, k=3) for q in queries}
     calls.clear()
     got = {}
-    with IndexService(store) as svc:
+    with IndexService(store, authkey=KEY) as svc:
         barrier = threading.Barrier(16, timeout=30)
 
         def worker(q):
-            with RemoteFAISS(svc.address) as cli:
+            with RemoteFAISS(svc.address, KEY) as cli:
                 barrier.wait()
                 got[q] = cli.similarity_search_with_score(q, k=3)
 
@@ -121,7 +123,8 @@ def test_slow_engine_requests_are_stacked(store):
 
 
 def test_remote_writes_and_errors(store, tmp_path):
-    with IndexService(store) as svc, RemoteFAISS(svc.address) as cli:
+    with IndexService(store, authkey=KEY, save_root=str(tmp_path)) as svc, \
+            RemoteFAISS(svc.address, KEY) as cli:
         ids = cli.add_texts(["new book"], metadatas=[{"book_id": "B999"}])
         assert cli.index.ntotal == 201 and store.index.ntotal == 201
         assert cli.get_by_ids(ids)[0].page_content == "new book"
@@ -138,8 +141,42 @@ def test_remote_writes_and_errors(store, tmp_path):
             cli.similarity_search("x", filter=lambda m: True)
         assert cli.delete(ids=store.ids_for_key("B000")) is True
         assert cli.index.ntotal == 200
-        cli.save_local(str(tmp_path / "vs"))
+        cli.save_local("vs")
     assert (tmp_path / "vs" / "index.faiss").exists()
+
+
+def test_save_confined_and_read_only(store, tmp_path):
+    root = tmp_path / "root"
+    root.mkdir()
+    with IndexService(store, authkey=KEY) as svc, RemoteFAISS(svc.address, KEY) as cli:
+        with pytest.raises(PermissionError):  # no save_root: save_local disabled
+            cli.save_local("vs")
+    with IndexService(store, authkey=KEY, save_root=str(root)) as svc, \
+            RemoteFAISS(svc.address, KEY) as cli:
+        for bad in (str(tmp_path / "elsewhere"), "../escape", "/etc"):
+            with pytest.raises(PermissionError):
+                cli.save_local(bad)
+        with pytest.raises(PermissionError):
+            cli.save_local("ok", index_name="../../x")
+        cli.save_local("sub/ok")
+        assert (root / "sub" / "ok" / "index.faiss").exists()
+    assert not (tmp_path / "elsewhere").exists() and not (tmp_path / "escape").exists()
+    with IndexService(store, authkey=KEY, read_only=True, save_root=str(root)) as svc, \
+            RemoteFAISS(svc.address, KEY) as cli:
+        assert cli.index.ntotal == 200
+        for call in (lambda: cli.add_texts(["x"]), lambda: cli.delete(["a"]),
+                     lambda: cli.upsert_texts(["x"], [{"book_id": "B1"}]),
+                     lambda: cli.save_local("ro")):
+            with pytest.raises(PermissionError):
+                call()
+        assert cli.index.ntotal == 200
+
+
+def test_authkey_required(store):
+    with pytest.raises(TypeError):
+        IndexService(store)  # noqa: the key has no default
+    with pytest.raises(ValueError):
+        IndexService(store, authkey=b"")
 
 
 def test_bad_authkey_rejected(store):

@@ -1,5 +1,7 @@
-"""CPU, world_size 2 (gloo): the row-sharded index's layout, label bases,
-all-gather and merge reproduce the single-index result, ties included.
+"""CPU, world_size 2 and 3 (gloo): the row-sharded index's layout, label bases,
+all-gather and merge reproduce the single-index result, ties included (the
+inner-product tie rule too: shards send raw lexicographic lists, the merge
+applies faiss's rule once).
 
 Each rank's shard is the oracle-backed test double and the merge is the
 oracle's (faiss tie rule), because there is no GPU here; on the GPU the shard is
@@ -24,6 +26,63 @@ def _free_port():
     return port
 
 
+def _simulate_sharded(x, xq, k, metric, world):
+    """The sharded search's data flow without processes: per-shard raw lists of
+    shard_k(k) entries with global labels, concatenated as the all-gather lays
+    them out, merged with faiss's rule (oracle_merge)."""
+    from helpers import OracleIndex, oracle_merge
+    from vsearch.sharded import shard_bounds
+
+    kin = min(2 * k - 1, 64) if metric == 0 else k
+    Ds, Is = [], []
+    for r in range(world):
+        lo, hi = shard_bounds(x.shape[0], world, r)
+        sh = OracleIndex(x.shape[1], metric)
+        if hi > lo:
+            sh.add(x[lo:hi])
+        sh.set_id_base(lo)
+        D, I = sh.search(xq, kin, raw=True)
+        Ds.append(D)
+        Is.append(I)
+    return oracle_merge(np.stack(Ds), np.stack(Is), metric, k)
+
+
+def test_sharded_ip_tie_counterexample():
+    """Rows [2,0,1,0,0,0,1,1,1,2,2] (d=1), query 1, k=4, two shards: faiss's IP
+    heap returns [10, 9, 0, 7]; merging per-shard tie-ordered top-k lists gave
+    [10, 9, 0, 8] (round-1 verdict).  Raw per-shard lists fix it."""
+    from oracle import flat
+
+    x = np.array([2, 0, 1, 0, 0, 0, 1, 1, 1, 2, 2], dtype=np.float32)[:, None]
+    xq = np.ones((1, 1), dtype=np.float32)
+    Dr, Ir = flat.knn_exact(x, xq, 4, 0)
+    assert Ir[0].tolist() == [10, 9, 0, 7]
+    for world in (2, 3, 8):
+        D, I = _simulate_sharded(x, xq, 4, 0, world)
+        assert I[0].tolist() == [10, 9, 0, 7], (world, I[0].tolist())
+        assert np.array_equal(D, Dr)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_merge_equals_single_index_on_ties(metric, world):
+    """Tie-heavy integer data: every (n, k, world) split gives the single-index
+    labels and scores bit for bit."""
+    from oracle import flat
+
+    rng = np.random.default_rng(100 * world + metric)
+    for trial in range(12):
+        n = int(rng.integers(1, 120))
+        d = int(rng.integers(1, 3))
+        x = rng.integers(-2, 3, size=(n, d)).astype(np.float32)
+        xq = rng.integers(-2, 3, size=(5, d)).astype(np.float32)
+        for k in (1, 3, 4, 7, 12, 33):
+            Dr, Ir = flat.knn_exact(x, xq, k, metric)
+            D, I = _simulate_sharded(x, xq, k, metric, world)
+            assert np.array_equal(I, Ir), (trial, n, d, k, I, Ir)
+            assert np.array_equal(D, Dr)
+
+
 def _worker(rank, world, port, metric, q):
     import sys
 
@@ -36,6 +95,15 @@ def _worker(rank, world, port, metric, q):
         from oracle import flat
         from vsearch.sharded import ShardedIndexFlat, shard_bounds
 
+        res = {}
+        # the round-1 counterexample (d=1): faiss's IP tie rule across shards
+        xc = np.array([2, 0, 1, 0, 0, 0, 1, 1, 1, 2, 2], dtype=np.float32)[:, None]
+        idc = ShardedIndexFlat(1, metric, shard=OracleIndex(1, metric), merge=oracle_merge)
+        idc.add_global(xc)
+        D, I = idc.search(np.ones((1, 1), np.float32), 4)
+        Dr, Ir = flat.knn_exact(xc, np.ones((1, 1), np.float32), 4, metric)
+        res["counterexample"] = (np.array_equal(I, Ir), np.array_equal(D, Dr))
+
         rng = np.random.default_rng(0)
         x = rng.integers(-2, 3, size=(203, 4)).astype(np.float32)  # tie-heavy
         xq = rng.integers(-2, 3, size=(9, 4)).astype(np.float32)
@@ -44,8 +112,7 @@ def _worker(rank, world, port, metric, q):
         assert idx.ntotal == 203
         lo, hi = shard_bounds(203, world, rank)
         assert idx.shard.ntotal == hi - lo
-        res = {}
-        for k in (1, 4, 10):
+        for k in (1, 4, 10, 20):
             D, I = idx.search(xq, k)
             Dr, Ir = flat.knn_exact(x, xq, k, metric)
             res[k] = (np.array_equal(I, Ir), np.array_equal(D, Dr))
@@ -68,11 +135,11 @@ def _worker(rank, world, port, metric, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_sharded_search_equals_single_index(metric):
+def test_sharded_search_equals_single_index(metric, world):
     import sys
 
-    world = 2
     port = _free_port()
     mgr = mp.Manager()
     q = mgr.dict()
