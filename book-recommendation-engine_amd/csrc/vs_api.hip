@@ -29,37 +29,26 @@ struct vs_index {
   int dtype = VS_DTYPE_F32;
   int device = 0;
   int esize = 4;         // bytes per stored element (4 fp32, 2 bf16)
-  int64_t ld = 0;        // row stride in elements (ld * esize is a multiple of 128)
+  int64_t ld = 0;        // row stride in elements, a multiple of 64 (zero padding)
   int64_t ntotal = 0;
-  int64_t capacity = 0;  // rows allocated (multiple of kRowPad, >= ntotal + kBQ)
+  int64_t capacity = 0;  // rows allocated (multiple of kRowPad, >= ntotal + 256)
   int64_t id_base = 0;
   char* codes = nullptr;   // [capacity][ld] elements
   int64_t rowbytes() const { return ld * esize; }
   char* row(int64_t r) const { return codes + r * rowbytes(); }
   float* norms = nullptr;  // [capacity] squared L2 norms
-  // fp32 indexes: a copy of the rows in the blocked layout the bf16x3 GEMM
-  // streams (vs_gemm_x3.hip), derived lazily from `codes`; valid for rows
-  // [0, blocked_rows).  capacity x ld floats.
-  float* blocked = nullptr;
-  int64_t blocked_rows = 0;
-  // fp32 indexes, filter pass from planes (VS_X2F_SRC=planes): the hi/mid bf16
-  // planes of the rows in the order of the filter kernel's LDS images
-  // (split_rows_kernel); valid for rows [0, planes_rows).  capacity x ld x 2 bf16.
-  uint4* planes = nullptr;
-  int64_t planes_rows = 0;
+  // fp32 indexes: the bf16 (round-to-nearest-even) copy of every row that the
+  // filter pass multiplies ([capacity][ld] uint16, kept in step with the rows by
+  // add / remove_ids / growth) and |x - hi(x)|^2 per row, for the bound.
+  // bf16 indexes: the rows themselves are the plane.
+  uint16_t* hplane = nullptr;
+  float* rn2 = nullptr;
+  const uint16_t* plane() const { return esize == 2 ? (const uint16_t*)codes : hplane; }
   int engine = VS_ENGINE_AUTO;
-  // filter-and-verify fallback rate (moving average over large searches) and a
-  // probe counter: see the adaptive choice in run_topk
-  double x2v_fallback = 0.0;
-  int64_t x2v_probe = 0;
-  std::mutex x2v_mu;
-  std::mutex blocked_mu;
   std::shared_mutex mu;
 };
 
 namespace {
-
-constexpr double kX2vMaxFallback = 0.4;  // filter-and-verify: adaptive switch point
 
 thread_local std::string g_err;
 
@@ -93,7 +82,8 @@ struct DeviceGuard {
   }
 };
 
-// Stream-ordered scratch allocation, released on scope exit (on the same stream).
+// Stream-ordered scratch allocation, released on scope exit (on the same stream;
+// the device's default pool keeps the memory cached, vs_create).
 struct Scratch {
   hipStream_t st;
   std::vector<void*> ptrs;
@@ -118,17 +108,30 @@ struct TimedSpan {
   int dispatches;
 };
 std::vector<TimedSpan> g_timer_events;
-
 const char* g_timer_kernel = "";
-// filter-and-verify statistics (vs_filter_stats)
-int64_t g_filter_queries = 0;
-int64_t g_filter_fallbacks = 0;
-int64_t g_filter_wide = 0;  // flagged queries given to launch_verify_wide
 
-// The wide verification of flagged queries (VS_X2F_WIDE=0 turns it off, for A/B).
-bool x2f_wide_enabled() {
+// Filter-and-verify statistics, counted on the device (no host sync in a
+// search): [0] queries, [1] flagged by the first check (given to the wide
+// check), [2] flagged by both (redone by the exact engine).  One buffer per device.
+std::mutex g_stats_mu;
+std::vector<unsigned long long*> g_dev_stats;
+
+unsigned long long* device_stats(int dev) {
+  std::lock_guard<std::mutex> g(g_stats_mu);
+  if ((int)g_dev_stats.size() <= dev) g_dev_stats.resize(dev + 1, nullptr);
+  if (!g_dev_stats[dev]) {
+    unsigned long long* p = nullptr;
+    if (hipMalloc(&p, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    g_dev_stats[dev] = p;
+  }
+  return g_dev_stats[dev];
+}
+
+// The wide verification of flagged queries (VS_X1_WIDE=0 turns it off, for A/B).
+bool wide_enabled() {
   static const bool on = [] {
-    const char* e = getenv("VS_X2F_WIDE");
+    const char* e = getenv("VS_X1_WIDE");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -139,11 +142,8 @@ struct KernelTimer {
   hipStream_t st;
   int dispatches = 1;  // kernel launches between the two events
   KernelTimer(hipStream_t s, const char* name) : st(s) {
-    {
-      std::lock_guard<std::mutex> g(g_timer_mu);
-      g_timer_kernel = name;
-    }
     std::lock_guard<std::mutex> g(g_timer_mu);
+    g_timer_kernel = name;
     if (!g_timer_on) return;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
       a = b = nullptr;
@@ -164,111 +164,77 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
 
-// Default source of the filter pass (x2f_source): blocked fp32 rows.
-constexpr int kX2fDefaultSource = 0;
-
-void drop_blocked(vs_index* idx) {  // both derived copies of the rows
-  if (idx->blocked) (void)hipFree(idx->blocked);
-  idx->blocked = nullptr;
-  idx->blocked_rows = 0;
-  if (idx->planes) (void)hipFree(idx->planes);
-  idx->planes = nullptr;
-  idx->planes_rows = 0;
-}
-
-// Makes the hi/mid planes valid for all rows (as ensure_blocked).
-bool ensure_planes(vs_index* idx, hipStream_t st) {
-  std::lock_guard<std::mutex> g(idx->blocked_mu);
-  const size_t bytes = (size_t)idx->capacity * idx->ld * 2 * sizeof(uint16_t);
-  if (!idx->planes) {
-    if (hipMalloc(&idx->planes, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      idx->planes = nullptr;
-      return false;
-    }
-    idx->planes_rows = 0;
-    if (hipMemsetAsync(idx->planes, 0, bytes, st) != hipSuccess) return false;
-  }
-  if (idx->planes_rows < idx->ntotal) {
-    if (launch_split_rows((const float*)idx->codes, idx->ld, idx->planes_rows,
-                          idx->ntotal - idx->planes_rows, 2, idx->planes, st) != hipSuccess)
-      return false;
-    idx->planes_rows = idx->ntotal;
-  }
-  return true;
-}
-
-// Source of the filter pass's database operand: 1 = pre-split planes by
-// LDS-DMA, 0 = blocked fp32 rows split in the kernel.  VS_X2F_SRC=planes|blocked
-// overrides (read per search, so tests and A/B runs can switch it).
-int x2f_source() {
-  const char* e = getenv("VS_X2F_SRC");
-  if (e && strcmp(e, "planes") == 0) return 1;
-  if (e && strcmp(e, "blocked") == 0) return 0;
-  return kX2fDefaultSource;
-}
-
-// Makes the blocked copy valid for all rows (called under the shared lock;
-// builds are serialised by blocked_mu).  Returns false when it cannot be
-// allocated (the caller then uses the fp32 MFMA kernel).
-bool ensure_blocked(vs_index* idx, hipStream_t st) {
-  std::lock_guard<std::mutex> g(idx->blocked_mu);
-  if (!idx->blocked) {
-    if (hipMalloc(&idx->blocked, (size_t)idx->capacity * idx->ld * sizeof(float)) != hipSuccess) {
-      (void)hipGetLastError();
-      idx->blocked = nullptr;
-      return false;
-    }
-    idx->blocked_rows = 0;
-    // padding rows must hold zeros, like the row storage
-    if (hipMemsetAsync(idx->blocked, 0, (size_t)idx->capacity * idx->ld * sizeof(float), st) !=
-        hipSuccess)
-      return false;
-  }
-  if (idx->blocked_rows < idx->ntotal) {
-    if (launch_block_rows((const float*)idx->codes, idx->ld, idx->blocked_rows,
-                          idx->ntotal - idx->blocked_rows, idx->blocked, st) != hipSuccess)
-      return false;
-    idx->blocked_rows = idx->ntotal;
-  }
-  return true;
-}
-
 int engine_from_env() {
   const char* e = getenv("VS_ENGINE");
   if (!e) return VS_ENGINE_AUTO;
   if (strcmp(e, "fp32") == 0) return VS_ENGINE_FP32_MFMA;
-  if (strcmp(e, "bf16x3") == 0) return VS_ENGINE_BF16X3;
-  if (strcmp(e, "bf16x2v") == 0) return VS_ENGINE_BF16X2_VERIFY;
+  if (strcmp(e, "bf16v") == 0) return VS_ENGINE_BF16_VERIFY;
   return VS_ENGINE_AUTO;
+}
+
+// The filter plane and residual norms of fp32 rows [r0, r0+n) (after the rows
+// and their norms are in place).
+int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
+  if (idx->esize != 4 || n <= 0) return VS_OK;
+  VS_HIP(launch_f32_to_bf16((const float*)idx->row(r0), idx->ld, idx->hplane + r0 * idx->ld,
+                            idx->ld, n, idx->ld, st),
+         "vs: filter plane");
+  VS_HIP(launch_resid_norms((const float*)idx->codes, idx->ld, r0, n, idx->rn2, st),
+         "vs: residual norms");
+  return VS_OK;
 }
 
 // Grows storage to hold `rows` rows (plus the tile slack), preserving content.
 int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
-  const int64_t need = round_up(rows + kBQ, kRowPad);
+  const int64_t need = round_up(rows + 256, kRowPad);  // 256-row query tiles of self-joins
   if (need <= idx->capacity) return VS_OK;
   int64_t cap = std::max(need, round_up(idx->capacity + idx->capacity / 2, kRowPad));
+  const bool f32 = idx->esize == 4;
   char* codes = nullptr;
   float* norms = nullptr;
-  hipError_t e = hipMalloc(&codes, (size_t)cap * idx->rowbytes());
-  if (e != hipSuccess) {
-    // retry without the growth headroom
+  uint16_t* hplane = nullptr;
+  float* rn2 = nullptr;
+  auto release = [&]() {
+    if (codes) (void)hipFree(codes);
+    if (norms) (void)hipFree(norms);
+    if (hplane) (void)hipFree(hplane);
+    if (rn2) (void)hipFree(rn2);
+  };
+  auto allocate = [&](int64_t c) -> hipError_t {
+    hipError_t e = hipMalloc(&codes, (size_t)c * idx->rowbytes());
+    if (e == hipSuccess) e = hipMalloc(&norms, (size_t)c * sizeof(float));
+    if (e == hipSuccess && f32) e = hipMalloc(&hplane, (size_t)c * idx->ld * sizeof(uint16_t));
+    if (e == hipSuccess && f32) e = hipMalloc(&rn2, (size_t)c * sizeof(float));
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      release();
+      codes = nullptr;
+      norms = nullptr;
+      hplane = nullptr;
+      rn2 = nullptr;
+    }
+    return e;
+  };
+  hipError_t e = allocate(cap);
+  if (e != hipSuccess) {  // retry without the growth headroom
     cap = need;
-    e = hipMalloc(&codes, (size_t)cap * idx->rowbytes());
+    e = allocate(cap);
     if (e != hipSuccess) return hip_fail(e, "vs: allocating row storage");
   }
-  e = hipMalloc(&norms, (size_t)cap * sizeof(float));
-  if (e != hipSuccess) {
-    (void)hipFree(codes);
-    return hip_fail(e, "vs: allocating norm storage");
-  }
-  // zero the whole tail (tile reads past ntotal must see zeros, never NaN garbage)
+  // zero every tail (tile reads past ntotal must see zeros, never NaN garbage)
   const int64_t keep = idx->ntotal;
   VS_HIP(hipMemsetAsync(codes + keep * idx->rowbytes(), 0, (size_t)(cap - keep) * idx->rowbytes(),
                         st),
          "vs: zeroing storage");
   VS_HIP(hipMemsetAsync(norms + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
          "vs: zeroing norms");
+  if (f32) {
+    VS_HIP(hipMemsetAsync(hplane + keep * idx->ld, 0,
+                          (size_t)(cap - keep) * idx->ld * sizeof(uint16_t), st),
+           "vs: zeroing plane");
+    VS_HIP(hipMemsetAsync(rn2 + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
+           "vs: zeroing residual norms");
+  }
   if (idx->codes && keep > 0) {
     VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->rowbytes(),
                           hipMemcpyDeviceToDevice, st),
@@ -276,77 +242,155 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     VS_HIP(hipMemcpyAsync(norms, idx->norms, (size_t)keep * sizeof(float),
                           hipMemcpyDeviceToDevice, st),
            "vs: copying norms");
+    if (f32) {
+      VS_HIP(hipMemcpyAsync(hplane, idx->hplane, (size_t)keep * idx->ld * sizeof(uint16_t),
+                            hipMemcpyDeviceToDevice, st),
+             "vs: copying plane");
+      VS_HIP(hipMemcpyAsync(rn2, idx->rn2, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
+                            st),
+             "vs: copying residual norms");
+    }
   }
   // In-flight searches (any stream) may still read the old storage.
   VS_HIP(hipDeviceSynchronize(), "vs: storage growth");
-  drop_blocked(idx);  // rebuilt lazily at the new capacity
   if (idx->codes) (void)hipFree(idx->codes);
   if (idx->norms) (void)hipFree(idx->norms);
+  if (idx->hplane) (void)hipFree(idx->hplane);
+  if (idx->rn2) (void)hipFree(idx->rn2);
   idx->codes = codes;
   idx->norms = norms;
+  idx->hplane = hplane;
+  idx->rn2 = rn2;
   idx->capacity = cap;
   return VS_OK;
 }
 
-int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
-             int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
-             hipStream_t st, const float* xaux, int force_engine, int raw);
+void free_storage(vs_index* idx) {
+  if (idx->codes) (void)hipFree(idx->codes);
+  if (idx->norms) (void)hipFree(idx->norms);
+  if (idx->hplane) (void)hipFree(idx->hplane);
+  if (idx->rn2) (void)hipFree(idx->rn2);
+  idx->codes = nullptr;
+  idx->norms = nullptr;
+  idx->hplane = nullptr;
+  idx->rn2 = nullptr;
+  idx->capacity = 0;
+}
 
-// The filter-and-verify engine (vs_gemm_x3.hip): an NP = 2 pass keeps the KF
-// best approximate candidates of every query, verify_rescore_kernel proves the
-// exact top-`need` is among them (or flags the query), rescores them exactly and
-// the usual merge emits (D, I).  Flagged queries are redone by the exact engine.
-int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* qaux, int nq,
-                      int nq_pad, int k, int need, int KF, float min_score, float* D, int64_t* I,
-                      hipStream_t st, const float* xaux, int xd, int64_t self0, int raw,
-                      int level = 0) {
+// What a search computes, shared by every engine.
+struct SearchArgs {
+  int mode = MODE_IP;
+  const float* qbuf = nullptr;   // [nq_pad][ld] fp32 query rows (zero padded)
+  const void* qb16 = nullptr;    // bf16 copy of the queries (bf16 indexes)
+  const float* qaux = nullptr;   // |q|^2 (L2) or 1/|q| (COS), nq_pad entries
+  const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
+  int nq = 0, nq_pad = 0, k = 0;
+  int64_t self0 = -1;            // self-join: query q is row self0 + q
+  float min_score = 0.0f;
+  int raw = 0;                   // VS_RAW_ORDER
+  bool l2_direct = false;        // faiss's sequential branch (the call's nq < 20)
+  float* D = nullptr;
+  int64_t* I = nullptr;
+};
+
+int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engine);
+
+// The exact engine on fp32 / bf16 rows: the fused MFMA GEMM + merge.  With
+// qlist/qcount, the batch is the gathered queries qlist[0 .. *qcount)
+// (device-side count) and the results go to their rows of D / I.
+int run_gemm(vs_index* idx, const SearchArgs& a, int need, hipStream_t st,
+              const int* qlist = nullptr, const int* qcount = nullptr) {
+  const int KP = kp_for(need);
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
-  X3Args a;
-  a.nq_pad = (int)round_up(nq_pad, kX3Q);
-  const int nqt = a.nq_pad / kX3Q;
-  const int ntiles = (ntotal + kX3Q - 1) / kX3Q;
-  const int L = x2f_lane_len();  // lane list length (<= KF)
-  // enough lists that their 2*nsplit*L entries cover 4*KF candidates (KF = 64:
-  // eight database splits even when the query tiles alone fill the chip), so the
-  // list floors sit well behind the KF-th candidate for the wide check
-  a.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, (2 * KF + L - 1) / L),
-                                    std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
-  a.nsplit = std::max(a.nsplit, 1);
   Partials part;
-  part.KP = kp_for(KF);  // lists padded past L, so the merge can emit KF
-  part.P = 2 * a.nsplit;
-  const size_t np_ = (size_t)a.nq_pad * part.P * part.KP;
+  part.KP = KP;
+  const int nqt = a.nq_pad / kBQ;
+  const int ntiles = (ntotal + kBN - 1) / kBN;
+  // ~2 workgroups per CU on 256 CUs; never more splits than database tiles.
+  // A gathered batch of unknown size spreads each query tile over the chip.
+  const int nsplit = qlist ? (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, 256))
+                           : (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
+  part.P = 2 * nsplit;
+  const size_t n = (size_t)a.nq_pad * part.P * KP;
+  VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
+  const void* qmat = a.qb16 ? a.qb16 : (const void*)a.qbuf;
+  {
+    KernelTimer tm(st, "gemm_topk");
+    VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, qmat, a.qaux, idx->ld, idx->esize,
+                            ntotal, a.nq_pad, nsplit, a.self0, part, st, qlist, qcount),
+           "vs: gemm_topk launch");
+    tm.stop();
+  }
+  VS_HIP(launch_merge_partials(a.mode, part, qlist ? a.nq_pad : a.nq, a.k, idx->id_base,
+                               a.min_score, a.D, a.I, a.k, st, a.raw, qlist, qcount),
+         "vs: merge launch");
+  return VS_OK;
+}
+
+// The filter-and-verify engine (vs_gemm_x1.hip), entirely stream-ordered:
+//  1. split the queries to bf16; the x1 pass keeps 8-entry lane lists per query;
+//  2. merge them to the KF best approximate candidates;
+//  3. verify_rescore: exact keys of the candidates + the bound check (fail[]);
+//  4. the flagged queries are compacted on the device and re-checked by the
+//     wide verification (every lane-list entry below the list floors);
+//  5. those still flagged are redone by the exact fp32 engine over the gathered
+//     rows (a launch whose tiles past the device-side count exit at once);
+//  6. the merges emit (D, I): all queries, then the redone rows over theirs.
+// The host never waits: counts live in device memory.
+int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st) {
+  const int ntotal = (int)idx->ntotal;
+  const int nq = a.nq;
+  const int mode = a.mode;
+  Scratch scr(st);
+  X1Args x;
+  x.nq_pad = (int)round_up(a.nq_pad, kX1Q);
+  const int nqt = x.nq_pad / kX1Q;
+  const int ntiles = (ntotal + kX1Q - 1) / kX1Q;
+  const int L = x1_lane_len();
+  // enough lists that their 4*nsplit*L entries cover 4*KF candidates, and one
+  // workgroup per CU on 256 CUs
+  x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, (KF + L - 1) / L),
+                                    std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
+  x.nsplit = std::max(x.nsplit, 1);
+  Partials part;  // lane lists: L entries each
+  part.KP = L;
+  part.P = 4 * x.nsplit;
+  const size_t np_ = (size_t)x.nq_pad * part.P * part.KP;
   VS_HIP(scr.alloc((void**)&part.key, np_ * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&part.id, np_ * sizeof(int)), "vs: scratch");
-  uint4* qp = nullptr;
-  const size_t qpb = (size_t)2 * a.nq_pad * idx->ld * sizeof(uint16_t);
-  VS_HIP(scr.alloc((void**)&qp, qpb), "vs: scratch");
-  if (a.nq_pad > nq_pad) VS_HIP(hipMemsetAsync(qp, 0, qpb, st), "vs: query planes");
-  VS_HIP(launch_split_queries(qbuf, idx->ld, nq_pad, a.nq_pad, 2, qp, st), "vs: query planes");
-  // |q|^2 (L2 searches stage it in qaux already) and max |x|^2 for the bound
-  const float* qn = qaux;
-  if (mode != MODE_L2) {
-    float* t = nullptr;
-    VS_HIP(scr.alloc((void**)&t, (size_t)nq_pad * sizeof(float)), "vs: scratch");
-    VS_HIP(launch_row_norms(qbuf, 4, idx->ld, 0, nq_pad, t, st), "vs: query norms");
-    qn = t;
+  // bf16 query plane: a split of the staged queries, or the stored rows' plane
+  const uint16_t* QH = nullptr;
+  const float* Q = a.qbuf;  // fp32 query rows for the rescoring
+  if (a.self0 >= 0) {
+    QH = idx->hplane + a.self0 * idx->ld;
+    Q = (const float*)idx->row(a.self0);
+  } else {
+    uint16_t* qh = nullptr;
+    VS_HIP(scr.alloc((void**)&qh, (size_t)x.nq_pad * idx->ld * sizeof(uint16_t)), "vs: scratch");
+    VS_HIP(launch_f32_to_bf16(a.qbuf, idx->ld, qh, idx->ld, a.nq_pad, idx->ld, st),
+           "vs: query plane");
+    if (x.nq_pad > a.nq_pad)
+      VS_HIP(hipMemsetAsync(qh + (size_t)a.nq_pad * idx->ld, 0,
+                            (size_t)(x.nq_pad - a.nq_pad) * idx->ld * sizeof(uint16_t), st),
+             "vs: query plane");
+    QH = qh;
   }
-  unsigned* xmax2 = nullptr;
-  VS_HIP(scr.alloc((void**)&xmax2, sizeof(unsigned)), "vs: scratch");
-  VS_HIP(launch_max_norm(idx->norms, ntotal, xmax2, st), "vs: max norm");
-  a.XB = xd ? (const float*)idx->planes : idx->blocked;
-  a.xaux = xaux;
-  a.QP = qp;
-  a.qaux = qaux;
-  a.nqa = nq_pad;
-  a.ld = idx->ld;
-  a.ntotal = ntotal;
-  a.self0 = self0;  // self-join: query q is row self0 + q, never its own candidate
+  unsigned* stats = nullptr;
+  VS_HIP(scr.alloc((void**)&stats, 4 * sizeof(unsigned)), "vs: scratch");
+  VS_HIP(launch_bound_stats(idx->norms, idx->rn2, ntotal, stats, st), "vs: bound stats");
+  x.XH = idx->hplane;
+  x.xaux = a.xaux;
+  x.QH = QH;
+  x.qaux = a.qaux;
+  x.nqa = a.nq_pad;
+  x.ld = idx->ld;
+  x.ntotal = ntotal;
+  x.self0 = a.self0;
   {
-    KernelTimer tm(st, "gemm_topk_x2f");
-    VS_HIP(launch_gemm_topk_x3(L, mode, 2, xd, a, part, st, &tm.dispatches),
-           "vs: gemm_topk_x2f launch");
+    KernelTimer tm(st, "gemm_topk_x1");
+    VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &tm.dispatches), "vs: gemm_topk_x1 launch");
     tm.stop();
   }
   // approximate top-KF per query (plain lexicographic order: the L2 merge)
@@ -354,311 +398,140 @@ int run_filter_verify(vs_index* idx, int mode, const float* qbuf, const float* q
   int64_t* Ik = nullptr;
   VS_HIP(scr.alloc((void**)&Dk, (size_t)nq * KF * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&Ik, (size_t)nq * KF * sizeof(int64_t)), "vs: scratch");
-  VS_HIP(launch_merge_partials(MODE_L2, part, nq, KF, 0, 0.0f, Dk, Ik, KF, st), "vs: merge");
+  Partials mp = part;
+  mp.KP = kp_for(KF);
+  mp.KL = L;
+  VS_HIP(launch_merge_partials(MODE_L2, mp, nq, KF, 0, 0.0f, Dk, Ik, KF, st), "vs: merge");
   Partials vp;
   vp.KP = kp_for(KF);
   vp.P = 1;
-  int* fail_d = nullptr;
+  int* flags = nullptr;
+  int* qlist = nullptr;
+  int* qcount = nullptr;
   VS_HIP(scr.alloc((void**)&vp.key, (size_t)nq * vp.KP * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&vp.id, (size_t)nq * vp.KP * sizeof(int)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&fail_d, (size_t)nq * sizeof(int)), "vs: scratch");
-  // cosine (self-join): qaux / xaux are the inverse norms the keys are scaled by
-  const double coef = mode == MODE_COS ? x2f_cos_key_bound(idx->ld) : x2f_bound_coef(idx->ld);
+  VS_HIP(scr.alloc((void**)&flags, (size_t)nq * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qlist, (size_t)a.nq_pad * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qcount, 2 * sizeof(int)), "vs: scratch");
+  const BoundArgs ba = make_bound_args(idx->ld);
+  const float* qinv = mode == MODE_COS ? a.qaux : nullptr;
+  const float* xinv = mode == MODE_COS ? a.xaux : nullptr;
   VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
-                               qbuf, qn, idx->ld, coef, xmax2, part, L, vp.key, vp.id, vp.KP,
-                               fail_d, st, mode == MODE_COS ? qaux : nullptr,
-                               mode == MODE_COS ? xaux : nullptr),
+                               Q, a.qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
+                               st, qinv, xinv),
          "vs: verify");
-  // queries the bound could not settle on KF candidates: rescore every lane-list
-  // entry below the list floors (launch_verify_wide), then the rest go on below
-  std::vector<int> fh(nq);
-  VS_HIP(hipMemcpyAsync(fh.data(), fail_d, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st),
-         "vs: verify flags");
-  VS_HIP(hipStreamSynchronize(st), "vs: verify flags");
-  std::vector<int> F;
-  for (int q = 0; q < nq; ++q)
-    if (fh[q]) F.push_back(q);
-  if (!F.empty() && x2f_wide_enabled()) {
-    int* qlist = nullptr;
-    VS_HIP(scr.alloc((void**)&qlist, F.size() * sizeof(int)), "vs: scratch");
-    VS_HIP(hipMemcpyAsync(qlist, F.data(), F.size() * sizeof(int), hipMemcpyHostToDevice, st),
-           "vs: verify list");
-    VS_HIP(launch_verify_wide(mode, (int)F.size(), qlist, KF, need, (const float*)idx->codes,
-                              idx->norms, qbuf, qn, idx->ld, coef, xmax2, part, L, vp.key, vp.id,
-                              vp.KP, fail_d, st, mode == MODE_COS ? qaux : nullptr,
-                              mode == MODE_COS ? xaux : nullptr),
+  unsigned long long* dst = device_stats(idx->device);
+  if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
+  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, dst + 0, st), "vs: flags");
+  if (wide_enabled())
+    VS_HIP(launch_verify_wide(mode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
+                              idx->norms, Q, a.qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
+                              vp.KP, flags, st, qinv, xinv),
            "vs: verify wide");
-    VS_HIP(hipMemcpyAsync(fh.data(), fail_d, (size_t)nq * sizeof(int), hipMemcpyDeviceToHost, st),
-           "vs: verify flags");
-    VS_HIP(hipStreamSynchronize(st), "vs: verify flags");  // qlist's copy is done too
-    {
-      std::lock_guard<std::mutex> g(g_timer_mu);
-      g_filter_wide += (int64_t)F.size();
-    }
-    F.clear();
-    for (int q = 0; q < nq; ++q)
-      if (fh[q]) F.push_back(q);
-  }
-  VS_HIP(launch_merge_partials(mode, vp, nq, k, idx->id_base, min_score, D, I, k, st, raw),
+  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, dst + 2, nullptr, st), "vs: flags");
+  VS_HIP(launch_merge_partials(mode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
+                               a.raw),
          "vs: merge");
-  const int nf = (int)F.size();
-  // More than 32 flagged queries (and room for more candidates): a second filter
-  // pass over just those, keeping 64 candidates, settles most of them for about
-  // 1/16 of a full pass per 256 queries; what it cannot settle goes to the exact
-  // engine.  The stats count queries that reach the exact engine.
-  const bool second = level == 0 && self0 < 0 && KF < 64 && x2f_list_len(need) > 0 &&
-                      need + 8 <= 64 && nf > 32;
   {
     std::lock_guard<std::mutex> g(g_timer_mu);
-    if (level == 0) g_filter_queries += nq;
-    if (!second) g_filter_fallbacks += nf;
+    g_timer_kernel = "gemm_topk_x1";
   }
-  if (level == 0) {
-    std::lock_guard<std::mutex> g(idx->x2v_mu);
-    const double w = std::min(1.0, nq / 1024.0) * 0.5;  // small batches move it less
-    idx->x2v_fallback = (1.0 - w) * idx->x2v_fallback + w * ((double)nf / nq);
-  }
-  if (F.empty()) return VS_OK;
-  // self-joins: the flagged queries are not consecutive rows, so they are redone
-  // as plain searches for k + 1 and their own row is dropped afterwards
-  const int kf = self0 >= 0 ? k + 1 : k;
-  const int nf_pad = (int)round_up(std::max(nf, kGemvMaxQ), kBQ) + kBQ;  // chunk tails
-  float* q2 = nullptr;
-  float* a2 = nullptr;
-  float* D2 = nullptr;
-  int64_t* I2 = nullptr;
-  VS_HIP(scr.alloc((void**)&q2, (size_t)nf_pad * idx->ld * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&a2, (size_t)nf_pad * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&D2, (size_t)nf * kf * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&I2, (size_t)nf * kf * sizeof(int64_t)), "vs: scratch");
-  VS_HIP(hipMemsetAsync(q2, 0, (size_t)nf_pad * idx->ld * sizeof(float), st), "vs: fallback");
-  VS_HIP(hipMemsetAsync(a2, 0, (size_t)nf_pad * sizeof(float), st), "vs: fallback");
-  for (int i = 0; i < nf; ++i) {
-    VS_HIP(hipMemcpyAsync(q2 + (int64_t)i * idx->ld, qbuf + (int64_t)F[i] * idx->ld,
-                          (size_t)idx->ld * sizeof(float), hipMemcpyDeviceToDevice, st),
-           "vs: fallback");
-    if (mode == MODE_L2 || mode == MODE_COS)  // |q|^2, or 1/|q| for cosine
-      VS_HIP(hipMemcpyAsync(a2 + i, qaux + F[i], sizeof(float), hipMemcpyDeviceToDevice, st),
-             "vs: fallback");
-  }
-  if (second) {
-    int rc = run_filter_verify(idx, mode, q2, a2, nf, nf_pad, k, need, 64, min_score, D2, I2, st,
-                               xaux, xd, -1, raw, 1);
-    if (rc) return rc;
-  }
-  // a few queries: 16 at a time through the small-batch kernels (one corpus
-  // stream each); more: one exact-engine launch
-  const int step = nf <= 64 ? 16 : nf;
-  for (int f0 = 0; f0 < (second ? 0 : nf); f0 += step) {
-    const int nc = std::min(step, nf - f0);
-    const int nc_pad = (int)round_up(std::max(nc, kGemvMaxQ), kBQ);
-    int rc = run_topk(idx, mode, q2 + (int64_t)f0 * idx->ld, nullptr, a2 + f0, nc, nc_pad, kf, -1,
-                      min_score, D2 + (int64_t)f0 * kf, I2 + (int64_t)f0 * kf, st, xaux,
-                      VS_ENGINE_BF16X3, raw);
-    if (rc) return rc;
-  }
+  // the exact redo of what is still flagged (usually nothing: every tile exits)
+  SearchArgs ex = a;
+  ex.qbuf = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
+  ex.nq_pad = (int)round_up(nq, kBQ);
+  int rc = run_gemm(idx, ex, need, st, qlist, qcount + 1);
   {
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_kernel = "gemm_topk_x2f";  // the fallback is part of this engine's search
+    g_timer_kernel = "gemm_topk_x1";  // the redo is part of this engine's search
   }
-  if (self0 >= 0) {  // drop each query's own row (first occurrence), keep k entries
-    std::vector<float> dh((size_t)nf * kf), dk((size_t)nf * k);
-    std::vector<int64_t> ih((size_t)nf * kf), ik((size_t)nf * k);
-    VS_HIP(hipMemcpyAsync(dh.data(), D2, dh.size() * sizeof(float), hipMemcpyDeviceToHost, st),
-           "vs: fallback");
-    VS_HIP(hipMemcpyAsync(ih.data(), I2, ih.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st),
-           "vs: fallback");
-    VS_HIP(hipStreamSynchronize(st), "vs: fallback");
-    for (int i = 0; i < nf; ++i) {
-      const int64_t self = idx->id_base + self0 + F[i];
-      int o = 0;
-      bool dropped = false;
-      for (int j = 0; j < kf && o < k; ++j) {
-        if (!dropped && ih[(size_t)i * kf + j] == self) {
-          dropped = true;
-          continue;
-        }
-        dk[(size_t)i * k + o] = dh[(size_t)i * kf + j];
-        ik[(size_t)i * k + o] = ih[(size_t)i * kf + j];
-        ++o;
-      }
-    }
-    VS_HIP(hipMemcpyAsync(D2, dk.data(), dk.size() * sizeof(float), hipMemcpyHostToDevice, st),
-           "vs: fallback");
-    VS_HIP(hipMemcpyAsync(I2, ik.data(), ik.size() * sizeof(int64_t), hipMemcpyHostToDevice, st),
-           "vs: fallback");
-    VS_HIP(hipStreamSynchronize(st), "vs: fallback");  // dk / ik leave scope
-  }
-  for (int i = 0; i < nf; ++i) {
-    VS_HIP(hipMemcpyAsync(D + (int64_t)F[i] * k, D2 + (int64_t)i * k, (size_t)k * sizeof(float),
-                          hipMemcpyDeviceToDevice, st),
-           "vs: fallback");
-    VS_HIP(hipMemcpyAsync(I + (int64_t)F[i] * k, I2 + (int64_t)i * k, (size_t)k * sizeof(int64_t),
-                          hipMemcpyDeviceToDevice, st),
-           "vs: fallback");
-  }
-  return VS_OK;
+  return rc;
 }
 
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
 // zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
-int run_topk(vs_index* idx, int mode, const float* qbuf, const void* qb16, const float* qaux,
-             int nq, int nq_pad, int k, int64_t self0, float min_score, float* D, int64_t* I,
-             hipStream_t st, const float* xaux, int force_engine = VS_ENGINE_AUTO,
-             int raw = 0) {
+int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engine) {
   // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
   // lowest 2k-1 (key, label) entries of every partial list to be exact; `raw`
   // output (plain lexicographic order) needs k.
-  const bool tie_rule = mode == MODE_IP && !raw;
-  const int KP = tie_rule ? kp_for(std::min(2 * k - 1, VS_MAX_K)) : kp_for(k);
+  const int mode = a.mode;
+  const bool tie_rule = mode == MODE_IP && !a.raw;
+  const int need = tie_rule ? std::min(2 * a.k - 1, VS_MAX_K) : a.k;
+  const int KP = kp_for(need);
   const int ntotal = (int)idx->ntotal;
+  const int nq = a.nq;
+
+  // Small batches stream the corpus once.  fp32 L2 searches whose CALL has
+  // fewer than 20 queries take faiss's sequential branch (direct sum (x-q)^2,
+  // faiss's distance_compute_blas_threshold): the GEMV kernel, 8 queries per
+  // pass.  Otherwise the skinny MFMA kernel (any metric / dtype, L2 by the norm
+  // expansion like faiss's BLAS branch), or the GEMV for one or two inner-product
+  // queries on fp32 rows (measured faster there, profiles/r01_small_batch_ab.txt).
+  static const char* pref = getenv("VS_SMALL_BATCH");
+  const bool small_ok = (mode == MODE_IP || mode == MODE_L2) && a.self0 < 0;
+  const bool gemv_fits =
+      (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
+  const bool direct = small_ok && mode == MODE_L2 && a.l2_direct && idx->esize == 4 && gemv_fits;
+  const bool skinny_ok = small_ok && !direct && nq <= kSkinnyMaxQ && KP <= 32 &&
+                         (nq <= 16 || KP <= 16) && (idx->ld * idx->esize) % 64 == 0;
+  bool gemv = small_ok && gemv_fits && idx->esize == 4 &&
+              (direct || (mode == MODE_IP && nq <= 2 && !(pref && strcmp(pref, "skinny") == 0)));
+  if (pref && strcmp(pref, "gemv") == 0 && small_ok && gemv_fits && nq <= kGemvMaxQ &&
+      (mode == MODE_IP || direct))
+    gemv = true;
   Scratch scr(st);
   Partials part;
   part.KP = KP;
-
-  // Small batches stream the corpus once: the skinny MFMA kernel (any metric /
-  // dtype), except fp32 L2 with nq <= 8, which keeps faiss's direct sum (x-q)^2
-  // branch on the GEMV kernel.  VS_SMALL_BATCH=gemv|skinny overrides (A/B runs).
-  static const char* pref = getenv("VS_SMALL_BATCH");
-  const bool small_ok = (mode == MODE_IP || mode == MODE_L2) && self0 < 0;
-  const bool gemv_ok = small_ok && nq <= kGemvMaxQ &&
-                       (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <=
-                           64 * 1024;
-  const bool skinny_ok = small_ok && nq <= kSkinnyMaxQ && KP <= 32 && (nq <= 16 || KP <= 16) &&
-                         (idx->ld * idx->esize) % 64 == 0;
-  bool gemv;
-  bool skinny;
-  if (pref && strcmp(pref, "gemv") == 0) {
-    gemv = gemv_ok;
-    skinny = !gemv && skinny_ok;
-  } else if (pref && strcmp(pref, "skinny") == 0) {
-    skinny = skinny_ok;
-    gemv = !skinny && gemv_ok;
-  } else {
-    // measured (MI355X, 10M x 1536): fp32 batch-1 GEMV 83 % of HBM vs skinny 76 %;
-    // bf16 batch-8 skinny 80 % vs GEMV 29 % (profiles/r01_small_batch_ab.txt)
-    gemv = gemv_ok && idx->esize == 4 && (nq <= 2 || mode == MODE_L2);
-    skinny = !gemv && skinny_ok;
+  if (gemv) {
+    const int gmode = direct ? MODE_L2D : MODE_IP;
+    const int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
+    part.P = nblocks;
+    const int step = kGemvMaxQ;  // queries per corpus pass
+    const size_t n = (size_t)std::min(nq, step) * part.P * KP;
+    VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
+    for (int q0 = 0; q0 < nq; q0 += step) {
+      const int nc = std::min(step, nq - q0);
+      KernelTimer tm(st, "gemv_topk");
+      VS_HIP(launch_gemv_topk(KP, gmode, nc, idx->codes, idx->esize, a.qbuf + (int64_t)q0 * idx->ld,
+                              idx->ld, ntotal, nblocks, part, st),
+             "vs: gemv_topk launch");
+      tm.stop();
+      VS_HIP(launch_merge_partials(gmode, part, nc, a.k, idx->id_base, a.min_score,
+                                   a.D + (int64_t)q0 * a.k, a.I + (int64_t)q0 * a.k, a.k, st,
+                                   a.raw),
+             "vs: merge launch");
+    }
+    return VS_OK;
   }
-  if (skinny) {
+  if (skinny_ok) {
     const int nblocks =
         (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
     part.P = nblocks;
     const size_t n = (size_t)nq * part.P * KP;
     VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
-    const void* qsk = qb16 ? qb16 : (const void*)qbuf;
+    const void* qsk = a.qb16 ? a.qb16 : (const void*)a.qbuf;
     KernelTimer tm(st, "skinny_topk");
-    VS_HIP(launch_skinny_topk(KP, mode, nq, idx->codes, idx->esize, xaux, qsk, qaux, idx->ld,
+    VS_HIP(launch_skinny_topk(KP, mode, nq, idx->codes, idx->esize, a.xaux, qsk, a.qaux, idx->ld,
                               ntotal, nblocks, part, st),
            "vs: skinny_topk launch");
     tm.stop();
-    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
+    VS_HIP(launch_merge_partials(mode, part, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k,
+                                 st, a.raw),
            "vs: merge launch");
     return VS_OK;
   }
-  // bf16 indexes hand the GEMM a bf16 copy of the (already rounded) queries
-  const void* qmat = qb16 ? qb16 : (const void*)qbuf;
-  if (gemv) {
-    const int gmode = mode == MODE_L2 ? MODE_L2D : MODE_IP;
-    int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
-    part.P = nblocks;
-    const int nql = nq <= 2 ? nq : (nq <= 4 ? 4 : 8);
-    const size_t n = (size_t)nql * part.P * KP;
-    VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
-    VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
-    KernelTimer tm(st, "gemv_topk");
-    VS_HIP(launch_gemv_topk(KP, gmode, nq, idx->codes, idx->esize, qbuf, idx->ld, ntotal, nblocks,
-                            part, st),
-           "vs: gemv_topk launch");
-    tm.stop();
-    VS_HIP(launch_merge_partials(gmode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
-           "vs: merge launch");
-    return VS_OK;
-  }
-
-  // fp32 indexes run the large-batch GEMM on the bf16 matrix cores through the
-  // exact 3-plane split (vs_gemm_x3.hip) unless disabled (VS_ENGINE=fp32 /
-  // vs_set_engine) or the blocked copy of the rows does not fit in HBM.
+  // Large batches of fp32 indexes: the filter-and-verify engine where it applies
+  // (IP k <= 28, L2 / cosine k <= 56), else (or VS_ENGINE=fp32) the fp32 MFMA
+  // GEMM.  bf16 indexes: the bf16 MFMA GEMM.
   int engine = force_engine != VS_ENGINE_AUTO ? force_engine
                : idx->engine != VS_ENGINE_AUTO ? idx->engine
                                                : engine_from_env();
-  // entries of each partial list the final merge needs (faiss's IP tie rule: 2k-1)
-  const int need = tie_rule ? std::min(2 * k - 1, VS_MAX_K) : k;
-  const int KF = x2f_list_len(need);
-  const bool library_choice = engine == VS_ENGINE_AUTO;
-  if (engine == VS_ENGINE_AUTO) engine = KF > 0 ? VS_ENGINE_BF16X2_VERIFY : VS_ENGINE_BF16X3;
-  // the filter pass: IP / L2 searches, and cosine self-joins from blocked rows
-  if (engine == VS_ENGINE_BF16X2_VERIFY &&
-      (KF == 0 || (mode == MODE_COS && (self0 < 0 || x2f_source() != 0))))
-    engine = VS_ENGINE_BF16X3;
-  // Adaptive: a query falls back when its top scores crowd inside the filter's
-  // error bound.  The filter pass costs ~0.53 of the exact engine, so once the
-  // recent fallback rate passes 0.4 (break-even ~0.47) the exact engine runs
-  // directly; every 16th search still takes the filter path to re-measure.
-  if (library_choice && engine == VS_ENGINE_BF16X2_VERIFY) {
-    std::lock_guard<std::mutex> g(idx->x2v_mu);
-    if (idx->x2v_fallback > kX2vMaxFallback && idx->x2v_probe++ % 16 != 0)
-      engine = VS_ENGINE_BF16X3;
-  }
-  if (idx->esize == 4 && engine == VS_ENGINE_BF16X2_VERIFY) {
-    const int xd = x2f_source();
-    if (xd ? ensure_planes(idx, st) : ensure_blocked(idx, st))
-      return run_filter_verify(idx, mode, qbuf, qaux, nq, nq_pad, k, need, KF, min_score, D, I,
-                               st, xaux, xd, self0, raw);
-  }
-  const int KR = x3_list_len(need);
-  if (idx->esize == 4 && engine == VS_ENGINE_BF16X3 && KR > 0 && ensure_blocked(idx, st)) {
-    X3Args a;
-    a.nq_pad = (int)round_up(nq_pad, kX3Q);
-    const int nqt3 = a.nq_pad / kX3Q;
-    const int ntiles3 = (ntotal + kX3Q - 1) / kX3Q;
-    // one 8-wave workgroup per CU on 256 CUs
-    a.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles3, (256 + nqt3 - 1) / nqt3));
-    part.P = 2 * a.nsplit;
-    const size_t n3 = (size_t)a.nq_pad * part.P * KP;
-    VS_HIP(scr.alloc((void**)&part.key, n3 * sizeof(float)), "vs: scratch");
-    VS_HIP(scr.alloc((void**)&part.id, n3 * sizeof(int)), "vs: scratch");
-    // query planes (self-join queries are stored rows, split the same way);
-    // rows past nq_pad stay zero
-    uint4* qp = nullptr;
-    const size_t qpb = (size_t)3 * a.nq_pad * idx->ld * sizeof(uint16_t);
-    VS_HIP(scr.alloc((void**)&qp, qpb), "vs: scratch");
-    if (a.nq_pad > nq_pad) VS_HIP(hipMemsetAsync(qp, 0, qpb, st), "vs: query planes");
-    VS_HIP(launch_split_queries(qbuf, idx->ld, nq_pad, a.nq_pad, 3, qp, st), "vs: query planes");
-    a.XB = idx->blocked;
-    a.xaux = xaux;
-    a.QP = qp;
-    a.qaux = qaux;
-    a.nqa = nq_pad;
-    a.ld = idx->ld;
-    a.ntotal = ntotal;
-    a.self0 = self0;
-    KernelTimer tm(st, "gemm_topk_x3");
-    VS_HIP(launch_gemm_topk_x3(KR, mode, 3, 0, a, part, st, &tm.dispatches),
-           "vs: gemm_topk_x3 launch");
-    tm.stop();
-    VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
-           "vs: merge launch");
-    return VS_OK;
-  }
-
-  const int nqt = nq_pad / kBQ;
-  const int ntiles = (ntotal + kBN - 1) / kBN;
-  // ~2 workgroups per CU on 256 CUs; never more splits than database tiles.
-  int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
-  part.P = 2 * nsplit;
-  const size_t n = (size_t)nq_pad * part.P * KP;
-  VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
-  KernelTimer tm(st, "gemm_topk");
-  VS_HIP(launch_gemm_topk(KP, mode, idx->codes, xaux, qmat, qaux, idx->ld, idx->esize, ntotal,
-                          nq_pad, nsplit, self0, part, st),
-         "vs: gemm_topk launch");
-  tm.stop();
-  VS_HIP(launch_merge_partials(mode, part, nq, k, idx->id_base, min_score, D, I, k, st, raw),
-         "vs: merge launch");
-  return VS_OK;
+  const int KF = x1_list_len(need);
+  if (idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0)
+    return run_filter_verify(idx, a, need, KF, st);
+  return run_gemm(idx, a, need, st);
 }
 
 }  // namespace
@@ -708,7 +581,7 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
   idx->dtype = dtype;
   idx->device = device;
   idx->esize = dtype == VS_DTYPE_BF16 ? 2 : 4;
-  idx->ld = round_up(d, 128 / idx->esize);  // 128-B rows per GEMM stage
+  idx->ld = round_up(d, 64);  // 64-element K-steps of the filter pass (128-B plane rows)
   *out = idx;
   return VS_OK;
 }
@@ -718,9 +591,7 @@ int vs_destroy(vs_index* idx) {
   {
     DeviceGuard g(idx->device);
     (void)hipDeviceSynchronize();
-    drop_blocked(idx);
-    if (idx->codes) (void)hipFree(idx->codes);
-    if (idx->norms) (void)hipFree(idx->norms);
+    free_storage(idx);
   }
   delete idx;
   return VS_OK;
@@ -771,6 +642,8 @@ int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
   }
   VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add: norms");
+  rc = derive_plane(idx, idx->ntotal, n, st);
+  if (rc) return rc;
   // Source host buffers may be released by the caller as soon as we return.
   VS_HIP(hipStreamSynchronize(st), "vs_add: synchronise");
   idx->ntotal += n;
@@ -793,6 +666,8 @@ int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void
          "vs_add_synthetic: fill");
   VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add_synthetic: norms");
+  rc = derive_plane(idx, idx->ntotal, n, st);
+  if (rc) return rc;
   VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic: synchronise");
   idx->ntotal += n;
   return VS_OK;
@@ -821,6 +696,8 @@ int vs_add_synthetic_ids(vs_index* idx, const int64_t* ids, int64_t n, uint64_t 
          "vs_add_synthetic_ids: fill");
   VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add_synthetic_ids: norms");
+  rc = derive_plane(idx, idx->ntotal, n, st);
+  if (rc) return rc;
   VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic_ids: synchronise");
   idx->ntotal += n;
   return VS_OK;
@@ -831,12 +708,7 @@ int vs_reset(vs_index* idx) {
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
   VS_HIP(hipDeviceSynchronize(), "vs_reset");
-  drop_blocked(idx);
-  if (idx->codes) (void)hipFree(idx->codes);
-  if (idx->norms) (void)hipFree(idx->norms);
-  idx->codes = nullptr;
-  idx->norms = nullptr;
-  idx->capacity = 0;
+  free_storage(idx);
   idx->ntotal = 0;
   return VS_OK;
 }
@@ -867,8 +739,8 @@ int vs_dtype(const vs_index* idx, int* out) {
 
 int vs_set_engine(vs_index* idx, int engine) {
   if (!idx) return fail(VS_E_INVALID, "vs_set_engine: null index");
-  if (engine != VS_ENGINE_AUTO && engine != VS_ENGINE_FP32_MFMA && engine != VS_ENGINE_BF16X3 &&
-      engine != VS_ENGINE_BF16X2_VERIFY)
+  if (engine != VS_ENGINE_AUTO && engine != VS_ENGINE_FP32_MFMA &&
+      engine != VS_ENGINE_BF16_VERIFY)
     return fail(VS_E_INVALID, "vs_set_engine: unknown engine");
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   idx->engine = engine;
@@ -948,9 +820,20 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
       }
       if (mode == MODE_L2)
         VS_HIP(launch_row_norms(qbuf, 4, idx->ld, 0, nq_pad, qaux, st), "vs_search: query norms");
-      int rc = run_topk(idx, mode, qbuf, qb16, qaux, (int)nc, (int)nq_pad, (int)k, -1, 0.0f,
-                        Dd + c0 * k, Id + c0 * k, st, idx->norms, VS_ENGINE_AUTO,
-                        (flags & VS_RAW_ORDER) ? 1 : 0);
+      SearchArgs sa;
+      sa.mode = mode;
+      sa.qbuf = qbuf;
+      sa.qb16 = qb16;
+      sa.qaux = qaux;
+      sa.xaux = idx->norms;
+      sa.nq = (int)nc;
+      sa.nq_pad = (int)nq_pad;
+      sa.k = (int)k;
+      sa.raw = (flags & VS_RAW_ORDER) ? 1 : 0;
+      sa.l2_direct = n < kBlasThreshold;  // faiss decides on the whole call's nq
+      sa.D = Dd + c0 * k;
+      sa.I = Id + c0 * k;
+      int rc = run_topk(idx, sa, st, VS_ENGINE_AUTO);
       if (rc) return rc;
     }
   }
@@ -1057,14 +940,32 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
                             hipMemcpyDeviceToDevice, st),
              "vs_remove_ids: move norms");
     }
+    if (idx->hplane) {  // the filter plane and residual norms move with their rows
+      const int64_t pb = idx->ld * (int64_t)sizeof(uint16_t);
+      VS_HIP(launch_gather_kept(idx->hplane, idx->rn2, pb, s0, cn, drm, nrem, tmp, tmpn, st),
+             "vs_remove_ids: gather plane");
+      if (kept > 0) {
+        VS_HIP(hipMemcpyAsync(idx->hplane + dst * idx->ld, tmp, (size_t)kept * pb,
+                              hipMemcpyDeviceToDevice, st),
+               "vs_remove_ids: move plane");
+        VS_HIP(hipMemcpyAsync(idx->rn2 + dst, tmpn, (size_t)kept * sizeof(float),
+                              hipMemcpyDeviceToDevice, st),
+               "vs_remove_ids: move residual norms");
+      }
+    }
   }
   const int64_t nt = idx->ntotal - nrem;
-  idx->blocked_rows = std::min(idx->blocked_rows, first);  // rows from `first` on moved
-  idx->planes_rows = std::min(idx->planes_rows, first);
   VS_HIP(hipMemsetAsync(idx->row(nt), 0, (size_t)nrem * idx->rowbytes(), st),
          "vs_remove_ids: zero tail");
   VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),
          "vs_remove_ids: zero tail");
+  if (idx->hplane) {
+    VS_HIP(hipMemsetAsync(idx->hplane + nt * idx->ld, 0,
+                          (size_t)nrem * idx->ld * sizeof(uint16_t), st),
+           "vs_remove_ids: zero tail");
+    VS_HIP(hipMemsetAsync(idx->rn2 + nt, 0, (size_t)nrem * sizeof(float), st),
+           "vs_remove_ids: zero tail");
+  }
   VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
   idx->ntotal = nt;
   if (nremoved) *nremoved = nrem;
@@ -1101,10 +1002,20 @@ int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_se
     const int64_t nq_pad = round_up(nc, kBQ);
     const int64_t qrow = q0 + c0;
     const bool b16 = idx->esize == 2;
-    int rc = run_topk(idx, MODE_COS, b16 ? nullptr : (const float*)idx->row(qrow),
-                      b16 ? (const void*)idx->row(qrow) : nullptr, rinv + qrow, (int)nc,
-                      (int)nq_pad, (int)k, exclude_self ? qrow : -1, min_sim, Dd + c0 * k,
-                      Id + c0 * k, st, rinv);
+    SearchArgs sa;
+    sa.mode = MODE_COS;
+    sa.qbuf = b16 ? nullptr : (const float*)idx->row(qrow);
+    sa.qb16 = b16 ? (const void*)idx->row(qrow) : nullptr;
+    sa.qaux = rinv + qrow;
+    sa.xaux = rinv;
+    sa.nq = (int)nc;
+    sa.nq_pad = (int)nq_pad;
+    sa.k = (int)k;
+    sa.self0 = exclude_self ? qrow : -1;
+    sa.min_score = min_sim;
+    sa.D = Dd + c0 * k;
+    sa.I = Id + c0 * k;
+    int rc = run_topk(idx, sa, st, VS_ENGINE_AUTO);
     if (rc) return rc;
   }
   if (!out_dev) {
@@ -1142,19 +1053,39 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
   return VS_OK;
 }
 
+// The counters live on the devices (written by the searches' own kernels); reading
+// them waits for every search already queued on those devices.
+static int read_filter_stats(unsigned long long out[3], int reset) {
+  out[0] = out[1] = out[2] = 0;
+  std::lock_guard<std::mutex> g(g_stats_mu);
+  for (int dev = 0; dev < (int)g_dev_stats.size(); ++dev) {
+    if (!g_dev_stats[dev]) continue;
+    DeviceGuard dg(dev);
+    unsigned long long h[4] = {0, 0, 0, 0};
+    VS_HIP(hipDeviceSynchronize(), "vs_filter_stats");
+    VS_HIP(hipMemcpy(h, g_dev_stats[dev], sizeof(h), hipMemcpyDeviceToHost), "vs_filter_stats");
+    for (int i = 0; i < 3; ++i) out[i] += h[i];
+    if (reset) VS_HIP(hipMemset(g_dev_stats[dev], 0, sizeof(h)), "vs_filter_stats");
+  }
+  return VS_OK;
+}
+
 int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
   if (!queries || !fallbacks) return fail(VS_E_INVALID, "vs_filter_stats: null output");
-  std::lock_guard<std::mutex> g(g_timer_mu);
-  *queries = g_filter_queries;
-  *fallbacks = g_filter_fallbacks;
-  if (reset) g_filter_queries = g_filter_fallbacks = g_filter_wide = 0;
+  unsigned long long c[3];
+  int rc = read_filter_stats(c, reset);
+  if (rc) return rc;
+  *queries = (int64_t)c[0];
+  *fallbacks = (int64_t)c[2];
   return VS_OK;
 }
 
 int vs_filter_wide_stats(int64_t* wide) {
   if (!wide) return fail(VS_E_INVALID, "vs_filter_wide_stats: null output");
-  std::lock_guard<std::mutex> g(g_timer_mu);
-  *wide = g_filter_wide;
+  unsigned long long c[3];
+  int rc = read_filter_stats(c, 0);
+  if (rc) return rc;
+  *wide = (int64_t)c[1];
   return VS_OK;
 }
 

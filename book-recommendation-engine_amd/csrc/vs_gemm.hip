@@ -40,7 +40,8 @@ template <int KP, int MODE, typename T>
 __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
     const T* __restrict__ X, const float* __restrict__ xaux, const T* __restrict__ Q,
     const float* __restrict__ qaux, int64_t ld, int nstage, int ntotal, int ntiles, int nsplit,
-    int nqt, int64_t self0, float* __restrict__ pkey, int* __restrict__ pid) {
+    int nqt, int64_t self0, float* __restrict__ pkey, int* __restrict__ pid,
+    const int* __restrict__ qlist, const int* __restrict__ qcount) {
   static_assert(sizeof(T) == 4 || sizeof(T) == 2, "fp32 or bf16 rows");
   // [buf][X|Q][128 rows][128 B]; viewed as floats (32 per row) for addressing.
   __shared__ __attribute__((aligned(16))) float smem[2 * 2 * kBN * kBK];
@@ -64,17 +65,22 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
   const int t0 = (int)((int64_t)sp * ntiles / nsplit);
   const int t1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
 
+  // gathered batch (the exact redo of flagged queries): slot s is query row
+  // qlist[s]; tiles past the device-side count have nothing to do
+  const int nf = qlist ? *qcount : 0;
+  if (qlist && qt * kBQ >= nf) return;  // uniform
   const int qloc = 32 * w + c32;
   const int gq = qt * kBQ + qloc;
+  const int qsrc = qlist ? qlist[min(gq, nf - 1)] : gq;
   float qa = 0.0f;
-  if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa = qaux[gq];
-  const int selfrow = self0 >= 0 ? (int)(self0 + gq) : -1;
+  if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa = qaux[qsrc];
+  const int selfrow = self0 >= 0 ? (int)(self0 + qsrc) : -1;
 
   float lk[KP];
   int li[KP];
   list_init<KP, int>(lk, li);
 
-  const T* Qblk = Q + (int64_t)qt * kBQ * ld;
+  const T* Qblk = qlist ? Q : Q + (int64_t)qt * kBQ * ld;
   // glds geometry: a wave instruction moves 8 rows x 128 B; wave w stages row
   // groups g = 4w..4w+3 of both operands.  The per-lane source offset is 32-bit
   // on a wave-uniform base (saddr form); the swizzle (row >> 1) & 7 depends on
@@ -88,6 +94,19 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
     const int row = par * 8 + srow;  // any group with g & 1 == par has this swizzle
     const int c = sphys ^ ((row >> 1) & 7);
     soff[par] = (uint32_t)(w * 32 + srow) * ldb + (uint32_t)c * 16u;
+  }
+  // query source offsets (per lane): contiguous tile rows, or the gathered rows
+  uint32_t qoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (qlist) {
+      const int slot = qt * kBQ + w * 32 + i * 8 + srow;
+      const int src = qlist[min(slot, nf - 1)];
+      const int row = (w * 4 + i) * 8 + srow;  // the LDS row decides the swizzle
+      qoff[i] = (uint32_t)src * ldb + (uint32_t)(sphys ^ ((row >> 1) & 7)) * 16u;
+    } else {
+      qoff[i] = soff[i & 1] + (uint32_t)(i * 8) * ldb;
+    }
   }
   // fragment-read geometry: (row >> 1) & 7 is the same for every subtile.
   const int fsw = (c32 >> 1) & 7;
@@ -111,7 +130,7 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
         const int g = w * 4 + i;
         const uint32_t o = soff[i & 1] + (uint32_t)(i * 8) * ldb;
         __builtin_amdgcn_global_load_lds(xs + o, VS_LDS(dX + g * 256), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(qs + o, VS_LDS(dQ + g * 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(qs + qoff[i], VS_LDS(dQ + g * 256), 16, 0, 0);
       }
     };
 
@@ -213,7 +232,7 @@ template <int KP, int MODE>
 static hipError_t gemm_dispatch_mode(const void* X, const float* xaux, const void* Q,
                                      const float* qaux, int64_t ld, int esize, int ntotal,
                                      int nq_pad, int nsplit, int64_t self0, Partials part,
-                                     hipStream_t st) {
+                                     hipStream_t st, const int* qlist, const int* qcount) {
   const int ntiles = (ntotal + kBN - 1) / kBN;
   const int nqt = nq_pad / kBQ;
   const int nblk = nqt * nsplit;
@@ -221,28 +240,29 @@ static hipError_t gemm_dispatch_mode(const void* X, const float* xaux, const voi
   if (esize == 4)
     hipLaunchKernelGGL((gemm_topk<KP, MODE, float>), dim3(nblk), dim3(256), 0, st,
                        (const float*)X, xaux, (const float*)Q, qaux, ld, nstage, ntotal, ntiles,
-                       nsplit, nqt, self0, part.key, part.id);
+                       nsplit, nqt, self0, part.key, part.id, qlist, qcount);
   else
     hipLaunchKernelGGL((gemm_topk<KP, MODE, uint16_t>), dim3(nblk), dim3(256), 0, st,
                        (const uint16_t*)X, xaux, (const uint16_t*)Q, qaux, ld, nstage, ntotal,
-                       ntiles, nsplit, nqt, self0, part.key, part.id);
+                       ntiles, nsplit, nqt, self0, part.key, part.id, qlist, qcount);
   return hipGetLastError();
 }
 
 template <int KP>
 static hipError_t gemm_dispatch(int mode, const void* X, const float* xaux, const void* Q,
                                 const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
-                                int nsplit, int64_t self0, Partials part, hipStream_t st) {
+                                int nsplit, int64_t self0, Partials part, hipStream_t st,
+                                const int* qlist, const int* qcount) {
   switch (mode) {
     case MODE_IP:
       return gemm_dispatch_mode<KP, MODE_IP>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0,
-                                             part, st);
+                                             part, st, qlist, qcount);
     case MODE_L2:
       return gemm_dispatch_mode<KP, MODE_L2>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0,
-                                             part, st);
+                                             part, st, qlist, qcount);
     case MODE_COS:
       return gemm_dispatch_mode<KP, MODE_COS>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
-                                              nsplit, self0, part, st);
+                                              nsplit, self0, part, st, qlist, qcount);
     default:
       return hipErrorInvalidValue;
   }
@@ -250,19 +270,20 @@ static hipError_t gemm_dispatch(int mode, const void* X, const float* xaux, cons
 
 hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, const void* Q,
                             const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
-                            int nsplit, int64_t self0, Partials part, hipStream_t st) {
+                            int nsplit, int64_t self0, Partials part, hipStream_t st,
+                            const int* qlist, const int* qcount) {
   if (nq_pad % kBQ != 0 || (ld * esize) % 128 != 0 || part.KP != KP || part.P != 2 * nsplit ||
-      (esize != 4 && esize != 2))
+      (esize != 4 && esize != 2) || ((qlist == nullptr) != (qcount == nullptr)))
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:
-      return gemm_dispatch<8>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<8>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st, qlist, qcount);
     case 16:
-      return gemm_dispatch<16>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<16>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st, qlist, qcount);
     case 32:
-      return gemm_dispatch<32>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<32>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st, qlist, qcount);
     case 64:
-      return gemm_dispatch<64>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st);
+      return gemm_dispatch<64>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st, qlist, qcount);
     default:
       return hipErrorInvalidValue;
   }

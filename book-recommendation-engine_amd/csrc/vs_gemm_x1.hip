@@ -1,0 +1,798 @@
+// vs_gemm_x1.hip — the filter pass of the filter-and-verify engine: one bf16
+// MFMA product per fp32 product, fused with per-lane candidate lists.
+//
+// Every fp32 index keeps, beside its fp32 rows, the bf16 (round-to-nearest-even)
+// copy of every row ("hi plane", [capacity][ld] uint16, row-major) and the
+// squared norm of each row's residual x - hi.  A search splits its queries the
+// same way and the kernel below scores every (query, row) pair with the single
+// product hi(q) . hi(x) on v_mfma_f32_32x32x16_bf16 — a plain bf16 GEMM over
+// Q (nq x d) and X (N x d) whose output never leaves the chip: each lane keeps
+// the best approximate keys of its queries.  The exact answer is then proved and
+// produced by verify_rescore_kernel (below): the candidates are rescored in
+// fp64 from the fp32 rows, and a rigorous bound on |approx - exact| decides
+// whether the candidate set must contain the exact top-M.
+//
+// Tile: 256 database rows x 256 queries per workgroup of 8 waves (two per SIMD,
+// one workgroup per CU; 128 KB of LDS).  Wave w owns rows [128 (w&1), +128) and
+// queries [64 (w>>1), +64): 4 x 2 accumulators of 32x32 (128 registers); lane l
+// sees queries c = l&31 of its two 32-query blocks and keeps one sorted list of
+// KR entries per query (lanes l and l+32 hold disjoint rows of the same query).
+// K advances 64 elements (128 B per row) per step: both operand tiles (32 KB
+// each) are staged by global_load_lds_dwordx4 into the step's LDS image — eight
+// 1-KiB instructions per wave, whole 128-B lines per row — double-buffered, one
+// barrier per step.  16-B chunk c of LDS row r sits at c ^ ((r >> 1) & 7): every
+// 16-lane ds_read_b128 group of a fragment read hits 16 distinct bank slots
+// (the swizzle is applied to the per-lane GLOBAL source address, as LDS-DMA
+// writes LDS lane-linearly).
+//
+// Epilogue per 256-row tile (rare work after the first tiles): the keys of a
+// lane's 16 rows of one 32-row block are reduced to their minimum; only when it
+// can enter the lane's list are they inserted one by one.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+
+#include "vs_device.h"
+
+// waves 4-7 share their SIMDs with waves 0-3 and lose VALU arbitration on age:
+// one static priority for that half (MI355X_MICROARCH.md, "Two waves per SIMD" 4)
+#ifndef VS_X1_PRIO
+#define VS_X1_PRIO 1
+#endif
+
+namespace vs {
+
+namespace {
+
+constexpr int kT = 256;               // rows (and queries) per tile
+constexpr int kTileB = kT * 128;      // one operand tile of one K-step: 32 KB
+constexpr int kX1ChunkTiles = 16;     // database tiles per workgroup per launch
+
+__device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
+
+__device__ __forceinline__ float sel16(const f32x16& v, int i) {
+  float r = v[0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) r = i == j ? v[j] : r;
+  return r;
+}
+
+}  // namespace
+
+template <int KR, int MODE>
+__global__ __launch_bounds__(512, 1) void gemm_topk_x1(
+    const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
+    const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
+    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
+    int KP, float* __restrict__ pkey, int* __restrict__ pid) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * kTileB];  // [buf][X|Q][256][128 B]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int c32 = lane & 31;
+  const int wr = w & 1;   // row half
+  const int wq = w >> 1;  // query quarter
+
+  // Bijective XCD remap: the workgroups of one database split run on one XCD,
+  // so each database tile is fetched into that XCD's L2 once for all query tiles.
+  const int nblk = gridDim.x;
+  const int b = blockIdx.x;
+  int lb;
+  {
+    const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
+    lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+  }
+  const int qt = lb % nqt;
+  const int sp = lb / nqt;
+  const int s0 = (int)((int64_t)sp * ntiles / nsplit);
+  const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
+  const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
+  const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
+
+  int gq[2], selfrow[2];
+  float qa[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    gq[qb] = qt * kT + 64 * wq + 32 * qb + c32;
+    qa[qb] = 0.0f;
+    if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
+    selfrow[qb] = self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
+  }
+
+  // list (sp, wr, h) of each query
+  const int P = nsplit * 4;
+  const int pl = sp * 4 + wr * 2 + h;
+  float lk[2][KR];
+  int li[2][KR];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+    if (chunk == 0) {
+      list_init<KR, int>(lk[qb], li[qb]);
+    } else {  // resume the list the previous launch wrote
+#pragma unroll
+      for (int e = 0; e < KR; ++e) {
+        lk[qb][e] = pkey[o + e];
+        li[qb][e] = pid[o + e];
+      }
+    }
+  }
+
+  if (t1 > t0) {  // uniform over the workgroup
+    const uint32_t ldb = (uint32_t)ld * 2u;  // row stride in bytes
+    // LDS-DMA geometry: lane L of an instruction moves 16 B of row L>>3 of an
+    // 8-row group into slot L&7 of that LDS row; the source chunk is the slot
+    // XOR the row's swizzle, which depends on the group only through its parity.
+    const int srow = lane >> 3;
+    uint32_t soff[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int row = par * 8 + srow;
+      soff[par] = (uint32_t)srow * ldb + (uint32_t)((lane & 7) ^ ((row >> 1) & 7)) * 16u;
+    }
+    const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld);
+    const int fsw = (c32 >> 1) & 7;  // fragment rows 32i + c32 share (row >> 1) & 7
+
+    // wave w stages row groups 4w .. 4w+3 (rows 32w .. 32w+31) of both tiles
+    auto stage = [&](int buf, int t, int ks) {
+      char* dX = smem + buf * 2 * kTileB;
+      char* dQ = dX + kTileB;
+      const char* xs = (const char*)(XH + (int64_t)t * kT * ld) + ks * 128;
+      const char* qs = qtile + ks * 128;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t o = soff[i & 1] + (uint32_t)(32 * w + 8 * i) * ldb;
+        __builtin_amdgcn_global_load_lds(xs + o, VS_LDS(dX + (4 * w + i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(qs + o, VS_LDS(dQ + (4 * w + i) * 1024), 16, 0, 0);
+      }
+    };
+
+    f32x16 acc[4][2];
+    auto zero = [&]() {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[rb][qb][r] = 0.0f;
+    };
+
+    // one K-step: 4 sub-steps of 16 elements; lane (c32, h) reads chunk 2s+h of
+    // its fragment rows (A: database rows 128wr + 32rb + c32; B: queries
+    // 64wq + 32qb + c32) — the same k order on both operands
+    auto mma = [&](int buf) {
+      const char* cX = smem + buf * 2 * kTileB + (128 * wr + c32) * 128;
+      const char* cQ = smem + buf * 2 * kTileB + kTileB + (64 * wq + c32) * 128;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int co = ((2 * s4 + h) ^ fsw) * 16;
+        const uint4 b0 = *(const uint4*)(cQ + co);
+        const uint4 b1 = *(const uint4*)(cQ + 32 * 128 + co);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const uint4 a = *(const uint4*)(cX + rb * 32 * 128 + co);
+          acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b0), acc[rb][0], 0, 0, 0);
+          acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b1), acc[rb][1], 0, 0, 0);
+        }
+      }
+    };
+
+    // Keys of the lane's 16 rows of a block (row r0 + 8jj + 4h + e in register
+    // 4jj + e); their minimum against the list's last entry decides whether any
+    // can enter (lexicographic admission: a key equal to the last one may).
+    auto epilogue = [&](int t) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int r0 = t * kT + 128 * wr + 32 * rb;
+        f32x4 xa[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
+            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          f32x16 key;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = acc[rb][qb][jj * 4 + e];
+              float kk;
+              if constexpr (MODE == MODE_IP) {
+                kk = -v;
+              } else if constexpr (MODE == MODE_L2) {
+                kk = l2_from_ip(qa[qb], xa[jj][e], v);
+              } else {
+                kk = -(v * (qa[qb] * xa[jj][e]));
+              }
+              key[jj * 4 + e] = kk;
+            }
+          }
+          float m = key[0];
+#pragma unroll
+          for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
+          if (m <= lk[qb][KR - 1]) {  // rare after the first tiles
+            uint32_t cm = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              const bool c = row < ntotal && row != selfrow[qb] &&
+                             lex_less(key[r], row, lk[qb][KR - 1], li[qb][KR - 1]);
+              cm |= (uint32_t)c << r;
+            }
+            while (cm) {
+              const int bi = __builtin_ctz(cm);
+              cm &= cm - 1;
+              const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+              list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+            }
+          }
+        }
+      }
+    };
+
+    if (VS_X1_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
+
+    int t = t0, ks = 0, buf = 0;
+    stage(0, t, 0);
+    __syncthreads();
+    zero();
+    for (;;) {
+      int nt = t, nk = ks + 1;
+      if (nk == nksteps) {
+        nk = 0;
+        ++nt;
+      }
+      if (nt < t1) stage(buf ^ 1, nt, nk);
+      mma(buf);
+      if (nk == 0) {
+        epilogue(t);
+        zero();
+      }
+      if (nt >= t1) break;
+      __syncthreads();  // this wave's next-step loads landed; everyone is done with `buf`
+      buf ^= 1;
+      t = nt;
+      ks = nk;
+    }
+  }
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+#pragma unroll
+    for (int e = 0; e < KR; ++e) {
+      pkey[o + e] = lk[qb][e];
+      pid[o + e] = li[qb][e];
+    }
+    for (int e = KR; e < KP; ++e) {  // the merge reads KP entries per list
+      pkey[o + e] = FLT_MAX;
+      pid[o + e] = -1;
+    }
+  }
+}
+
+template <int KR, int MODE>
+static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
+  const int ntiles = (a.ntotal + kT - 1) / kT;
+  const int nqt = a.nq_pad / kT;
+  static const int chunk_tiles = [] {
+    const char* e = getenv("VS_X1_CHUNK_TILES");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kX1ChunkTiles;
+  }();
+  const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
+  const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
+  const int nksteps = (int)(a.ld / 64);
+  for (int c = 0; c < nchunk; ++c) {
+    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE>), dim3(nqt * a.nsplit), dim3(512), 0, st, a.XH,
+                       a.xaux, a.QH, a.qaux, a.nqa, a.ld, nksteps, a.ntotal, ntiles, a.nsplit, nqt,
+                       a.self0, c, nchunk, part.KP, part.key, part.id);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (ndispatch) *ndispatch = nchunk;
+  return hipSuccess;
+}
+
+int x1_lane_len() { return 8; }
+
+hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStream_t st,
+                               int* ndispatch) {
+  // 64-element K-steps of 128-B rows; 256-query tiles; the lists of a query
+  // are (split, row half, lane half)
+  if (a.nq_pad % kT != 0 || a.ld % 64 != 0 || a.ld <= 0 || part.KP < x1_lane_len() ||
+      part.P != 4 * a.nsplit || a.nsplit < 1 || a.ntotal <= 0)
+    return hipErrorInvalidValue;
+  switch (mode) {
+    case MODE_IP:
+      return x1_launch<8, MODE_IP>(a, part, st, ndispatch);
+    case MODE_L2:
+      return x1_launch<8, MODE_L2>(a, part, st, ndispatch);
+    case MODE_COS:
+      return x1_launch<8, MODE_COS>(a, part, st, ndispatch);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+// Filter-pass candidate count: the merged approximate candidates for `need`
+// exact entries, with a margin of at least 8 (0 = not served by the filter).
+int x1_list_len(int need) {
+  return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : need + 8 <= 64 ? 64 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Per-index maxima for the bound: max |x|^2, max |x - hi(x)|^2 and
+// max |x - hi(x)|^2 / |x|^2 over rows [0, n) (non-negative floats order as their
+// bits; NaN sorts above every number and makes the bound non-finite).
+__global__ __launch_bounds__(256) void bound_stats_kernel(const float* __restrict__ norms,
+                                                          const float* __restrict__ rn2, int64_t n,
+                                                          unsigned* __restrict__ out) {
+  unsigned m0 = 0, m1 = 0, m2 = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float a = norms[i], r = rn2[i];
+    m0 = max(m0, __float_as_uint(a) & 0x7FFFFFFFu);
+    m1 = max(m1, __float_as_uint(r) & 0x7FFFFFFFu);
+    if (a > 0.0f) m2 = max(m2, __float_as_uint(r / a) & 0x7FFFFFFFu);
+    else if (r > 0.0f || a != a) m2 = 0x7F800000u;  // a residual without a norm: no bound
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    m0 = max(m0, (unsigned)__shfl_xor((int)m0, o));
+    m1 = max(m1, (unsigned)__shfl_xor((int)m1, o));
+    m2 = max(m2, (unsigned)__shfl_xor((int)m2, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(out + 0, m0);
+    atomicMax(out + 1, m1);
+    atomicMax(out + 2, m2);
+  }
+}
+
+hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, unsigned* out,
+                              hipStream_t st) {
+  hipError_t e = hipMemsetAsync(out, 0, 3 * sizeof(unsigned), st);
+  if (e != hipSuccess || n <= 0) return e;
+  const int64_t blocks = std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(bound_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, st, norms, rn2, n,
+                     out);
+  return hipGetLastError();
+}
+
+// |x - hi(x)|^2 of rows [r0, r0+n) (fp32 rows, stride ld), one wave per row,
+// fp64 sums rounded up to float (an upper bound, as the verification needs).
+__global__ __launch_bounds__(256) void resid_norms_kernel(const float* __restrict__ X, int64_t ld,
+                                                          int64_t r0, int64_t n,
+                                                          float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* xr = X + (r0 + row) * ld;
+  double s = 0.0;
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = v[i];
+      const float hi = __uint_as_float((uint32_t)f32_to_bf16_rne(x) << 16);
+      const double r = (double)x - (double)hi;
+      s += r * r;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) {
+    float f = (float)s;
+    if ((double)f < s) f = nextafterf(f, INFINITY);
+    out[r0 + row] = f;
+  }
+}
+
+hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(resid_norms_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, ld,
+                     r0, n, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Verification (engine VS_ENGINE_BF16_VERIFY).  With x = hi(x) + r(x) and
+// q = hi(q) + r(q) (bf16 round-to-nearest-even, residuals exact in fp32):
+//   x.q - hi(x).hi(q) = hi(x).r(q) + r(x).hi(q) + r(x).r(q)
+// and the MFMA sums ld exact products in fp32 (each add off by <= 1 ulp), so
+// for every row (Cauchy-Schwarz on each term)
+//   |approx - x.q| <= gam |hi(x)||hi(q)| + |hi(x)||r(q)| + |r(x)||hi(q)| + |r(x)||r(q)|,
+// gam = n u / (1 - n u), n = ld + 1, u = 2^-23; the exact key is the fp32
+// rounding of x.q (one more 2^-23 |x||q|).  |hi(x)| <= |x| + |r(x)|, and the
+// verification takes the maxima of |x| and |r(x)| over the index.  Let a = the
+// sorted approximate keys of the KF candidates of a query and E their exact
+// keys, sorted; E[M-1] bounds the true M-th best key from above, and every row
+// outside the candidates has approximate key >= T (the KF-th candidate, or a
+// full lane list's last entry, whichever is smaller), so whenever
+//     T - B > E[M-1]
+// the exact top-M (ties included) is among the candidates and E's first M
+// entries are it.  Otherwise the query is flagged for the exact engine.
+
+
+__device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, double qh2, double qr2,
+                                            double qn2, const unsigned* stats) {
+  const double xm = sqrt((double)__uint_as_float(stats[0]) * (1.0 + ba.norm_inf));
+  const double rx = sqrt((double)__uint_as_float(stats[1]));
+  const double hx = xm + rx;
+  const double hq = sqrt(qh2), rq = sqrt(qr2), qn = sqrt(qn2);
+  double b = ba.gam * hx * hq + hx * rq + rx * hq + rx * rq + 2.0 * ldexp(1.0, -24) * xm * qn;
+  b *= 1.0 + 1e-6;
+  if (mode == MODE_L2) {  // key = (|q|^2 + |x|^2) - 2 ip, every step rounded
+    const double xm2 = (double)__uint_as_float(stats[0]);
+    b = 2.0 * b + 8.0 * ldexp(1.0, -24) * (qn2 + xm2);
+  } else if (mode == MODE_COS) {
+    // keys -(s qinv xinv) with qinv, xinv from the stored norms (relative error
+    // ~gam); |s_a - s_e| / (|x||q|) <= gam (1+rho)^2 + 2 rho (1+rho) + rho^2 +
+    // 2^-23, rho = max |r(x)| / |x| (the queries are stored rows); two roundings
+    // of a key of magnitude <= 1 add 2^-22
+    const double rho = sqrt((double)__uint_as_float(stats[2]) * (1.0 + ba.norm_inf));
+    const double rel = ba.gam * (1 + rho) * (1 + rho) + 2 * rho * (1 + rho) + rho * rho +
+                       ldexp(1.0, -23);
+    b = (rel * (1.0 + 3.0 * ba.gam) + ldexp(1.0, -22)) * (1.0 + 1e-6);
+  }
+  return b;
+}
+
+// the query's split norms |hi(q)|^2, |r(q)|^2, |q|^2 (fp64, across the wave)
+__device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow, int64_t ld,
+                                                  int lane, double& qh2, double& qr2,
+                                                  double& qn2) {
+  double a = 0.0, r = 0.0, n = 0.0;
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 v = *(const f32x4*)(qrow + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = v[i];
+      const float hi = __uint_as_float((uint32_t)f32_to_bf16_rne(x) << 16);
+      const double rr = (double)x - (double)hi;
+      a += (double)hi * hi;
+      r += rr * rr;
+      n += (double)x * x;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    r += __shfl_xor(r, o);
+    n += __shfl_xor(n, o);
+  }
+  qh2 = a;
+  qr2 = r;
+  qn2 = n;
+}
+
+// exact dot product of two fp32 rows (fp64 accumulation across the wave)
+__device__ __forceinline__ double wave_dot(const float* __restrict__ x, const float* __restrict__ q,
+                                           int64_t ld, int lane) {
+  double acc = 0.0;
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 xv = *(const f32x4*)(x + c);
+    const f32x4 qv = *(const f32x4*)(q + c);
+    acc = fma((double)xv.x, (double)qv.x, acc);
+    acc = fma((double)xv.y, (double)qv.y, acc);
+    acc = fma((double)xv.z, (double)qv.z, acc);
+    acc = fma((double)xv.w, (double)qv.w, acc);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  return acc;
+}
+
+template <int MODE>
+__device__ __forceinline__ float exact_key(float ip, int q, int r, const float* __restrict__ qn,
+                                           const float* __restrict__ xn,
+                                           const float* __restrict__ qinv,
+                                           const float* __restrict__ xinv) {
+  return MODE == MODE_L2    ? l2_from_ip(qn[q], xn[r], ip)
+         : MODE == MODE_COS ? -(ip * (qinv[q] * xinv[r]))
+                            : -ip;
+}
+
+// One wave per query.  Dk/Ik: the KF best approximate keys (ascending) and
+// local rows; X/xn: fp32 rows (stride ld) and squared norms; Q: query rows
+// (stride ld); qn: |q|^2 as staged for L2.  Writes KF exact (key, row) entries
+// sorted, padded to KP, and fail[q].
+template <int MODE>
+__global__ __launch_bounds__(64) void verify_rescore_kernel(
+    int KF, int M, const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
+    const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
+    const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
+    const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
+    float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
+    const float* __restrict__ qinv, const float* __restrict__ xinv) {
+  __shared__ float ek[64];
+  const int lane = threadIdx.x;
+  const int q = blockIdx.x;
+  const float a = lane < KF ? Dk[(int64_t)q * KF + lane] : FLT_MAX;
+  const int id = lane < KF ? (int)Ik[(int64_t)q * KF + lane] : -1;
+  const float aK = __shfl(a, KF - 1);
+  const int idK = __shfl(id, KF - 1);
+  // T: the KF-th merged key (if the merge found KF) and the last key of every
+  // full lane list; `bounded` = false when neither exists (the candidates are
+  // every admissible row)
+  bool bounded = idK >= 0;
+  float T = idK >= 0 ? aK : FLT_MAX;
+  for (int j = lane; j < P; j += 64) {
+    const int64_t o = ((int64_t)q * P + j) * LKP + L - 1;
+    if (lid[o] >= 0) {
+      bounded = true;
+      T = fminf(T, lkey[o]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) T = fminf(T, __shfl_xor(T, o));
+  bounded = __any(bounded);
+
+  const float* qrow = Q + (int64_t)q * ld;
+  double qh2, qr2, qn2;
+  query_split_norms(qrow, ld, lane, qh2, qr2, qn2);
+  for (int j = 0; j < KF; ++j) {
+    const int r = __shfl(id, j);
+    if (r < 0) {
+      if (lane == 0) ek[j] = FLT_MAX;
+      continue;
+    }
+    const double acc = wave_dot(X + (int64_t)r * ld, qrow, ld, lane);
+    if (lane == 0) ek[j] = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
+  }
+  __syncthreads();
+  // rank sort of (key, row); empty slots last, in lane order among themselves
+  const float k0 = lane < KF ? ek[lane] : FLT_MAX;
+  const int i0 = id < 0 ? INT_MAX : id;
+  int rank = 0;
+  for (int j = 0; j < KF; ++j) {
+    const float kj = __shfl(k0, j);
+    const int ij = __shfl(i0, j);
+    rank += (lex_less(kj, ij, k0, i0) || (kj == k0 && ij == i0 && j < lane)) ? 1 : 0;
+  }
+  float* ok = okey + (int64_t)q * KP;
+  int* oi = oid + (int64_t)q * KP;
+  if (lane < KF) {
+    ok[rank] = k0;
+    oi[rank] = id;  // -1 for empty slots
+  } else if (lane < KP) {
+    ok[lane] = FLT_MAX;
+    oi[lane] = -1;
+  }
+  // the M-th exact key (the lane whose rank is M-1 publishes it)
+  if (lane < KF && rank == M - 1) ek[63] = k0;
+  __syncthreads();
+  const float eM = ek[63];
+  const double bkey = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
+  const bool pass = !bounded || ((double)T - bkey > (double)eM && isfinite(T) && isfinite(eM) &&
+                                  isfinite(bkey));
+  if (lane == 0) fail[q] = pass ? 0 : 1;
+}
+
+hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
+                                 const int64_t* Ik, const float* X, const float* xn,
+                                 const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
+                                 const unsigned* stats, Partials lists, int L, float* okey,
+                                 int* oid, int KP, int* fail, hipStream_t st, const float* qinv,
+                                 const float* xinv) {
+  if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
+      L > lists.KP)
+    return hipErrorInvalidValue;
+  if (nq <= 0) return hipSuccess;
+#define VS_VERIFY(MD)                                                                             \
+  hipLaunchKernelGGL(verify_rescore_kernel<MD>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, X, xn, \
+                     Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey, oid,  \
+                     KP, fail, qinv, xinv)
+  if (mode == MODE_IP)
+    VS_VERIFY(MODE_IP);
+  else if (mode == MODE_L2)
+    VS_VERIFY(MODE_L2);
+  else if (mode == MODE_COS && qinv && xinv)
+    VS_VERIFY(MODE_COS);
+  else
+    return hipErrorInvalidValue;
+#undef VS_VERIFY
+  return hipGetLastError();
+}
+
+// Flagged queries -> ascending list qlist[0 .. *count) (one workgroup; a
+// block-wide prefix count per 1024-query chunk).  Running statistics: adds
+// the count to *total and n to *total_n (when not null).
+__global__ __launch_bounds__(1024) void compact_flags_kernel(const int* __restrict__ flags, int n,
+                                                             int* __restrict__ list,
+                                                             int* __restrict__ count,
+                                                             unsigned long long* __restrict__ total,
+                                                             unsigned long long* __restrict__ total_n) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) base = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int i = c0 + tid;
+    const int f = i < n && flags[i] != 0 ? 1 : 0;
+    const uint64_t bal = __ballot(f);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int j = 0; j < wv; ++j) off += wsum[j];
+    if (f) list[off + before] = i;
+    __syncthreads();
+    if (tid == 0) {
+      int s = 0;
+      for (int j = 0; j < 16; ++j) s += wsum[j];
+      base += s;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    *count = base;
+    if (total) atomicAdd(total, (unsigned long long)base);
+    if (total_n) atomicAdd(total_n, (unsigned long long)n);
+  }
+}
+
+hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
+                                unsigned long long* total, unsigned long long* total_n,
+                                hipStream_t st) {
+  if (n < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(compact_flags_kernel, dim3(1), dim3(1024), 0, st, flags, n, list, count,
+                     total, total_n);
+  return hipGetLastError();
+}
+
+// Wide verification of the flagged queries qlist[0 .. *count) (one 256-thread
+// workgroup per flagged query, a fixed grid striding over the device-side
+// count, so the host never reads it).  The condition above only needs a
+// threshold T such that every row outside the rescored set has approximate key
+// >= T: the smallest last entry of the full lane lists is one (a full list
+// dropped only rows lexicographically after its last entry), and then the set
+// may be *all* list entries below T, not just the KF merged ones.  More than
+// kWideCap entries below T, fewer than M, or a non-finite key: the query stays
+// flagged.
+template <int MODE>
+__global__ __launch_bounds__(256) void verify_wide_kernel(
+    const int* __restrict__ qlist, const int* __restrict__ count, int KF, int M,
+    const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
+    const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
+    const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
+    float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
+    const float* __restrict__ qinv, const float* __restrict__ xinv) {
+  __shared__ float ck[kWideCap];
+  __shared__ int cid[kWideCap];
+  __shared__ float wT[4];
+  __shared__ int wB[4];
+  __shared__ int cnt, bad;
+  __shared__ float eMs;
+  __shared__ double qs[3];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nflag = *count;
+  for (int jq = blockIdx.x; jq < nflag; jq += gridDim.x) {
+    const int q = qlist[jq];
+    const int64_t lbase = (int64_t)q * P * LKP;
+    float T = FLT_MAX;
+    bool bounded = false;
+    for (int j = tid; j < P; j += 256) {
+      const int64_t o = lbase + (int64_t)j * LKP + L - 1;
+      if (lid[o] >= 0) {
+        bounded = true;
+        T = fminf(T, lkey[o]);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) T = fminf(T, __shfl_xor(T, o));
+    bounded = __any(bounded);
+    if (lane == 0) {
+      wT[wv] = T;
+      wB[wv] = bounded ? 1 : 0;
+    }
+    if (tid == 0) {
+      cnt = 0;
+      bad = 0;
+      eMs = FLT_MAX;
+    }
+    const float* qrow = Q + (int64_t)q * ld;
+    if (wv == 0) {
+      double a, b, c;
+      query_split_norms(qrow, ld, lane, a, b, c);
+      if (lane == 0) {
+        qs[0] = a;
+        qs[1] = b;
+        qs[2] = c;
+      }
+    }
+    __syncthreads();
+    T = fminf(fminf(wT[0], wT[1]), fminf(wT[2], wT[3]));
+    bounded = (wB[0] | wB[1] | wB[2] | wB[3]) != 0;
+    // gather every entry below T (all entries when no list is full)
+    for (int j = tid; j < P * L; j += 256) {
+      const int64_t o = lbase + (int64_t)(j / L) * LKP + j % L;
+      const int r = lid[o];
+      if (r >= 0 && (!bounded || lkey[o] < T)) {
+        const int s = atomicAdd(&cnt, 1);
+        if (s < kWideCap) cid[s] = r;
+      }
+    }
+    __syncthreads();
+    const int n = cnt;
+    if (!(n > kWideCap || n < M || !isfinite(T))) {  // uniform
+      for (int j = wv; j < n; j += 4) {
+        const int r = cid[j];
+        const double acc = wave_dot(X + (int64_t)r * ld, qrow, ld, lane);
+        if (lane == 0) {
+          const float key = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
+          ck[j] = key;
+          if (!isfinite(key)) bad = 1;
+        }
+      }
+      __syncthreads();
+      if (!bad) {  // uniform
+        // rank of each (key, row) among the n (rows are distinct: the lists are disjoint)
+        float* ok = okey + (int64_t)q * KP;
+        int* oi = oid + (int64_t)q * KP;
+        for (int j = tid; j < n; j += 256) {
+          const float kj = ck[j];
+          const int ij = cid[j];
+          int rank = 0;
+          for (int t = 0; t < n; ++t) rank += lex_less(ck[t], cid[t], kj, ij) ? 1 : 0;
+          if (rank < KF) {
+            ok[rank] = kj;
+            oi[rank] = ij;
+          }
+          if (rank == M - 1) eMs = kj;
+        }
+        for (int j = min(n, KF) + tid; j < KP; j += 256) {
+          ok[j] = FLT_MAX;
+          oi[j] = -1;
+        }
+        __syncthreads();
+        const float eM = eMs;
+        const double bkey =
+            bound_key(MODE, ba, qs[0], qs[1], MODE == MODE_L2 ? (double)qn[q] : qs[2], stats);
+        const bool pass =
+            !bounded || ((double)T - bkey > (double)eM && isfinite(eM) && isfinite(bkey));
+        if (tid == 0 && pass) fail[q] = 0;
+      }
+    }
+    __syncthreads();  // the shared state is reused by the next flagged query
+  }
+}
+
+hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
+                              int M, const float* X, const float* xn, const float* Q,
+                              const float* qn, int64_t ld, const BoundArgs& ba,
+                              const unsigned* stats, Partials lists, int L, float* okey, int* oid,
+                              int KP, int* fail, hipStream_t st, const float* qinv,
+                              const float* xinv) {
+  if (KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
+  if (nq_max <= 0) return hipSuccess;
+  const int grid = std::min(nq_max, 512);
+#define VS_WIDE(MD)                                                                               \
+  hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(grid), dim3(256), 0, st, qlist, count, KF, M, X, \
+                     xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey,   \
+                     oid, KP, fail, qinv, xinv)
+  if (mode == MODE_IP)
+    VS_WIDE(MODE_IP);
+  else if (mode == MODE_L2)
+    VS_WIDE(MODE_L2);
+  else if (mode == MODE_COS && qinv && xinv)
+    VS_WIDE(MODE_COS);
+  else
+    return hipErrorInvalidValue;
+#undef VS_WIDE
+  return hipGetLastError();
+}
+
+// Bound constants for `ld` K elements (see above).
+BoundArgs make_bound_args(int64_t ld) {
+  BoundArgs ba;
+  const double u = std::ldexp(1.0, -23);
+  const double n = (double)ld + 1.0;
+  ba.gam = n * u / (1.0 - n * u);
+  ba.norm_inf = 2.0 * ba.gam;  // fp32 norm sums undercount by at most ~gam(ld) u/2-based
+  return ba;
+}
+
+}  // namespace vs

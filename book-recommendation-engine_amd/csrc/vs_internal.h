@@ -28,6 +28,9 @@ constexpr int kBK = 32;
 constexpr int kRowPad = 256;
 // The GEMV (small batch) path handles up to this many queries per launch.
 constexpr int kGemvMaxQ = 8;
+// faiss's distance_compute_blas_threshold: a search CALL with fewer queries runs
+// the sequential branch (L2 as the direct sum of squares).
+constexpr int kBlasThreshold = 20;
 // The skinny MFMA (small batch) path handles up to this many queries per launch.
 constexpr int kSkinnyMaxQ = 32;
 
@@ -46,14 +49,20 @@ struct Partials {
   int* id = nullptr;
   int P = 0;   // lists per query
   int KP = 0;  // entries per list
+  int KL = 0;  // for launch_merge_partials: entries stored per list when fewer
+               // than the merge keeps (0 = KP; a multiple of 4)
 };
 
 // ---- launchers (return the launch status; all asynchronous on `st`) -------
 // Fused MFMA distance + top-k over database tiles, writing 2*nsplit lists/query.
 // X / Q are fp32 (esize 4) or bf16 (esize 2) rows of stride ld elements.
+// With `qlist`, query slot s of the (nq_pad-row) batch is row qlist[s] of Q (and
+// of qaux; self row self0 + qlist[s]), only slots s < *qcount are computed
+// (query tiles past the device-side count return at once), lists indexed by slot.
 hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, const void* Q,
                             const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
-                            int nsplit, int64_t self0, Partials part, hipStream_t st);
+                            int nsplit, int64_t self0, Partials part, hipStream_t st,
+                            const int* qlist = nullptr, const int* qcount = nullptr);
 // Streaming (HBM-bound) distance + top-k for nq <= kGemvMaxQ.
 // X fp32 or bf16 rows; Q always fp32 (values already rounded for bf16 indexes).
 hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, const float* Q,
@@ -63,77 +72,77 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,
                               int ntotal, int nblocks, Partials part, hipStream_t st);
-// fp32-accurate GEMM path on bf16 MFMA (in-kernel exact 3-plane split,
-// vs_gemm_x3.hip).  Database and query rows in the blocked fp32 layout.
-struct X3Args {
-  const float* XB = nullptr;    // database rows, blocked (capacity rows)
-  const float* xaux = nullptr;  // per-row norms (L2) or 1/|x| (COS)
-  const uint4* QP = nullptr;    // query planes (launch_split_queries, nq_pad rows)
-  const float* qaux = nullptr;  // per-query aux, nqa entries (padding queries read 0)
+// The filter pass of the filter-and-verify engine (vs_gemm_x1.hip): one bf16
+// MFMA product per fp32 product over the bf16 (RNE) planes of rows and queries.
+struct X1Args {
+  const uint16_t* XH = nullptr;  // database hi plane [capacity][ld] (row-major)
+  const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
+  const uint16_t* QH = nullptr;  // query hi plane [nq_pad][ld] (self-join: stored rows)
+  const float* qaux = nullptr;   // per-query aux, nqa entries (padding queries read 0)
   int nqa = 0;
-  int64_t ld = 0;
+  int64_t ld = 0;                // elements per row, a multiple of 64
   int ntotal = 0;
-  int nq_pad = 0;               // multiple of kX3Q
+  int nq_pad = 0;                // multiple of kX1Q
   int nsplit = 1;
   int64_t self0 = -1;
 };
-constexpr int kX3Q = 256;  // queries (and database rows) per x3 tile
-// Register list length for `need` entries (8, 12, 16, 20 or 24; 0 = too long).
-int x3_list_len(int need);
-// Filter pass (NP = 2) list length for `need` exact entries (24 or 32; 0 = too long).
-int x2f_list_len(int need);
-int x2f_lane_len();
-// Writes 2*nsplit lists of part.KP entries per query (nq_pad queries): KR register
-// entries padded with empty slots.  np = 3: exact split (KR <= 24, IP/L2/COS);
-// np = 2: filter pass (KR 24 or 32, IP/L2).  xd = 0: a.XB holds the blocked fp32
-// rows (launch_block_rows); xd = 1 (np = 2 only): the pre-split planes
-// (launch_split_rows).  *ndispatch = kernel launches used.
-hipError_t launch_gemm_topk_x3(int KR, int mode, int np, int xd, const X3Args& a, Partials part,
-                               hipStream_t st, int* ndispatch);
-// |approx - exact| <= coef * |x| * |q| for the filter pass over ld K elements.
-double x2f_bound_coef(int64_t ld);
-double x2f_cos_key_bound(int64_t ld);
-// *out = bits of max(norms[0..n)) (norms >= 0; NaN propagates as the maximum).
-hipError_t launch_max_norm(const float* norms, int64_t n, unsigned* out, hipStream_t st);
-// Checks and rescores the filter candidates (see vs_gemm_x3.hip): Dk/Ik hold the
-// KF best approximate keys of each query (ascending, local rows), `lists` the
-// filter pass's lane lists (L entries each) for their floors; writes sorted
-// exact lists of KP entries (okey/oid) and fail[q] = 1 where the exact engine
-// must redo query q.
+constexpr int kX1Q = 256;  // queries (and database rows) per x1 tile
+// Candidates merged from the lane lists for `need` exact entries (24, 32 or 64;
+// 0 = not served by the filter engine).
+int x1_list_len(int need);
+// Entries per lane list of the filter pass (8).
+int x1_lane_len();
+// Writes 4*nsplit lists of part.KP entries per query (nq_pad queries), each holding
+// x1_lane_len() entries and empty padding.  *ndispatch = kernel launches used.
+hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStream_t st,
+                               int* ndispatch);
+// Bound constants of the verification (vs_gemm_x1.hip).
+struct BoundArgs {
+  double gam = 0.0;       // fp32 accumulation of ld + 1 terms: n u / (1 - n u), u = 2^-23
+  double norm_inf = 0.0;  // relative undercount of the stored fp32 norms
+};
+BoundArgs make_bound_args(int64_t ld);
+// out[0..3) = bits of max norms, max rn2, max rn2/norms over rows [0, n).
+hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, unsigned* out,
+                              hipStream_t st);
+// rn2[r] = |x_r - bf16_rne(x_r)|^2 (rounded up) for fp32 rows [r0, r0+n).
+hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
+                              hipStream_t st);
+// Checks and rescores the filter candidates: Dk/Ik hold the KF best approximate
+// keys of each query (ascending, local rows), `lists` the filter pass's lane
+// lists (L entries each) for their floors; writes sorted exact lists of KP
+// entries (okey/oid) and fail[q] = 1 where the exact engine must redo query q.
 hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
                                  const int64_t* Ik, const float* X, const float* xn,
-                                 const float* Q, const float* qn, int64_t ld, double coef,
-                                 const unsigned* xmax2, Partials lists, int L, float* okey,
+                                 const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
+                                 const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st,
                                  const float* qinv = nullptr, const float* xinv = nullptr);
-// Second verification of the nf queries qlist[] flagged by verify_rescore: every
-// lane-list entry below the smallest full-list floor is rescored exactly (up to
-// kWideCap per query) and the condition re-checked on that wider set; passing
-// queries get their sorted exact list in okey/oid and fail[q] = 0.
+// Flagged queries (flags[i] != 0) -> ascending qlist[0 .. *count), all on the
+// device; *total += count and *total_n += n when not null.
+hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
+                                unsigned long long* total, unsigned long long* total_n,
+                                hipStream_t st);
+// Second verification of the queries qlist[0 .. *count) (device count, fixed
+// grid): every lane-list entry below the smallest full-list floor is rescored
+// exactly (up to kWideCap per query) and the condition re-checked on that wider
+// set; passing queries get their sorted exact list in okey/oid and fail[q] = 0.
 constexpr int kWideCap = 1024;
-hipError_t launch_verify_wide(int mode, int nf, const int* qlist, int KF, int M, const float* X,
-                              const float* xn, const float* Q, const float* qn, int64_t ld,
-                              double coef, const unsigned* xmax2, Partials lists, int L,
-                              float* okey, int* oid, int KP, int* fail, hipStream_t st,
-                              const float* qinv = nullptr, const float* xinv = nullptr);
-// Splits fp32 query rows [0, n) (stride ld) into the x3 GEMM's np query planes
-// (np x nq_pad x ld bf16; rows n..nq_pad-1 must be zeroed by the caller).
-hipError_t launch_split_queries(const float* Q, int64_t ld, int64_t n, int nq_pad, int np,
-                                uint4* QP, hipStream_t st);
-// Copies fp32 rows [r0, r0+n) (stride ld, a multiple of 16) into the blocked
-// layout of 256-row tiles the x3 GEMM streams (vs_gemm_x3.hip).
-hipError_t launch_block_rows(const float* X, int64_t ld, int64_t r0, int64_t n, float* XB,
-                             hipStream_t st);
-// Splits fp32 rows [r0, r0+n) into the np bf16 planes of the x2f LDS images
-// (capacity x ld x np bf16 in total; vs_gemm_x3.hip, split_rows_kernel).
-hipError_t launch_split_rows(const float* X, int64_t ld, int64_t r0, int64_t n, int np,
-                             uint4* XP, hipStream_t st);
+hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
+                              int M, const float* X, const float* xn, const float* Q,
+                              const float* qn, int64_t ld, const BoundArgs& ba,
+                              const unsigned* stats, Partials lists, int L, float* okey, int* oid,
+                              int KP, int* fail, hipStream_t st, const float* qinv = nullptr,
+                              const float* xinv = nullptr);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
-// (key, label) order, the per-shard half of an exact sharded merge).
+// (key, label) order, the per-shard half of an exact sharded merge).  With
+// `qlist`, list q belongs to query qlist[q] (emitted to that row) and only
+// q < *qcount are merged (device-side count; the grid covers nq).
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
-                                 hipStream_t st, int raw = 0);
+                                 hipStream_t st, int raw = 0, const int* qlist = nullptr,
+                                 const int* qcount = nullptr);
 // Shard lists [nparts][nq][k_in] (scores, int64 labels) -> [nq][k].
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts,
                               int nq, int k_in, int k, float* D, int64_t* I, hipStream_t st);

@@ -111,22 +111,27 @@ __device__ __forceinline__ void emit_result(int mode, float key, int64_t id, int
 // left, which is emitted as (D, I) rows (grid x = query, y = list group).
 template <int KP>
 __global__ __launch_bounds__(64) void merge_lists_kernel(
-    const float* __restrict__ pkey, const int* __restrict__ pid, int P, float* __restrict__ okey,
+    const float* __restrict__ pkey, const int* __restrict__ pid, int P, int KL,
+    float* __restrict__ okey,
     int* __restrict__ oid, int P2, int emit, int k, int mode, int raw, int64_t id_base,
-    float min_score, float* __restrict__ D, int64_t* __restrict__ I, int64_t ldo) {
+    float min_score, float* __restrict__ D, int64_t* __restrict__ I, int64_t ldo,
+    const int* __restrict__ qlist, const int* __restrict__ qcount) {
   __shared__ float sk[64 * KP];
   __shared__ int si[64 * KP];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
   const int g = blockIdx.y;
+  if (qcount && q >= *qcount) return;  // gathered batch: slots past the count
   const int p = g * 64 + lane;
   float lk[KP];
   int li[KP];
-  if (p < P) {
-    const f32x4* ks = (const f32x4*)(pkey + ((int64_t)q * P + p) * KP);
-    const int4* is = (const int4*)(pid + ((int64_t)q * P + p) * KP);
+  list_init<KP, int>(lk, li);
+  if (p < P) {  // KL <= KP stored entries per list (a multiple of 4)
+    const f32x4* ks = (const f32x4*)(pkey + ((int64_t)q * P + p) * KL);
+    const int4* is = (const int4*)(pid + ((int64_t)q * P + p) * KL);
 #pragma unroll
     for (int j = 0; j < KP / 4; ++j) {
+      if (4 * j >= KL) break;
       const f32x4 kv = ks[j];
       const int4 iv = is[j];
       lk[4 * j + 0] = kv.x;
@@ -138,8 +143,6 @@ __global__ __launch_bounds__(64) void merge_lists_kernel(
       li[4 * j + 2] = iv.z;
       li[4 * j + 3] = iv.w;
     }
-  } else {
-    list_init<KP, int>(lk, li);
   }
   wave_tree_merge<KP, int>(lk, li, sk, si, lane);
   if (!emit) {
@@ -163,17 +166,19 @@ __global__ __launch_bounds__(64) void merge_lists_kernel(
     if (mode == MODE_IP && !raw) faiss_ip_tie_order<int>(sk, si, KP, k);
   }
   __syncthreads();
-  if (lane < k) emit_result(mode, sk[lane], si[lane], id_base, min_score, D + q * ldo + lane,
-                            I + q * ldo + lane);
+  const int64_t qe = qlist ? qlist[q] : q;  // output row
+  if (lane < k) emit_result(mode, sk[lane], si[lane], id_base, min_score, D + qe * ldo + lane,
+                            I + qe * ldo + lane);
 }
 
 template <int KP>
 static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t id_base,
                                float min_score, float* D, int64_t* I, int64_t ldo, int raw,
-                               hipStream_t st) {
+                               hipStream_t st, const int* qlist, const int* qcount) {
   const float* ck = part.key;
   const int* ci = part.id;
   int P = part.P;
+  int KL = part.KL > 0 ? part.KL : KP;
   void* tmp[2] = {nullptr, nullptr};
   int cur = 0;
   hipError_t e = hipSuccess;
@@ -184,19 +189,20 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
     if (e != hipSuccess) break;
     float* ok = (float*)buf;
     int* oi = (int*)(ok + (size_t)nq * P2 * KP);
-    hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, P2), dim3(64), 0, st, ck, ci, P, ok, oi,
-                       P2, 0, k, mode, raw, id_base, min_score, D, I, ldo);
+    hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, P2), dim3(64), 0, st, ck, ci, P, KL, ok,
+                       oi, P2, 0, k, mode, raw, id_base, min_score, D, I, ldo, qlist, qcount);
     e = hipGetLastError();
     if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
     tmp[cur] = buf;
     ck = ok;
     ci = oi;
     P = P2;
+    KL = KP;
   }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, 1), dim3(64), 0, st, ck, ci, P,
+    hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, 1), dim3(64), 0, st, ck, ci, P, KL,
                        (float*)nullptr, (int*)nullptr, 1, 1, k, mode, raw, id_base, min_score, D,
-                       I, ldo);
+                       I, ldo, qlist, qcount);
     e = hipGetLastError();
   }
   if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
@@ -205,18 +211,20 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
 
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
-                                 hipStream_t st, int raw) {
-  if (k < 1 || k > part.KP || nq < 0 || part.P < 1) return hipErrorInvalidValue;
+                                 hipStream_t st, int raw, const int* qlist, const int* qcount) {
+  if (k < 1 || k > part.KP || nq < 0 || part.P < 1 || part.KL < 0 || part.KL > part.KP ||
+      part.KL % 4 != 0)
+    return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   switch (part.KP) {
     case 8:
-      return merge_levels<8>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
+      return merge_levels<8>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st, qlist, qcount);
     case 16:
-      return merge_levels<16>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
+      return merge_levels<16>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st, qlist, qcount);
     case 32:
-      return merge_levels<32>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
+      return merge_levels<32>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st, qlist, qcount);
     case 64:
-      return merge_levels<64>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st);
+      return merge_levels<64>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st, qlist, qcount);
     default:
       return hipErrorInvalidValue;
   }

@@ -25,8 +25,7 @@ RAW_ORDER = 4
 MAX_K = 64
 ENGINE_AUTO = 0
 ENGINE_FP32_MFMA = 1
-ENGINE_BF16X3 = 2
-ENGINE_BF16X2_VERIFY = 3
+ENGINE_BF16_VERIFY = 3
 
 E_INVALID = -1
 E_HIP = -2

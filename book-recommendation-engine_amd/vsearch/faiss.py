@@ -190,11 +190,11 @@ class IndexFlat(Index):
         return int(nrem.value)
 
     def set_engine(self, engine: str) -> None:
-        """Large-batch arithmetic of fp32 indexes: "auto", "fp32" (fp32 MFMA),
-        "bf16x3" (fp32-accurate 3-plane bf16 split on the bf16 matrix cores) or
-        "bf16x2v" (3-product filter pass + rigorous bound + exact rescoring)."""
+        """Large-batch arithmetic of fp32 indexes: "auto", "fp32" (the exact fp32
+        MFMA engine) or "bf16v" (one-product bf16 filter pass + rigorous bound +
+        exact rescoring, the default where it applies)."""
         code = {"auto": _lib.ENGINE_AUTO, "fp32": _lib.ENGINE_FP32_MFMA,
-                "bf16x3": _lib.ENGINE_BF16X3, "bf16x2v": _lib.ENGINE_BF16X2_VERIFY}[engine]
+                "bf16v": _lib.ENGINE_BF16_VERIFY}[engine]
         _lib.check(self._lib.vs_set_engine(self._h, code), "vs_set_engine")
 
     def set_id_base(self, base: int) -> None:

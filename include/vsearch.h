@@ -107,24 +107,21 @@ int vs_metric(const vs_index* idx, int* out);
 int vs_dtype(const vs_index* idx, int* out);
 
 /* Arithmetic engine of the large-batch path of fp32 indexes:
- *   VS_ENGINE_AUTO       library default: BF16X2_VERIFY where it applies (IP/L2
- *                        searches needing <= 24 list entries), else BF16X3;
- *                        env VS_ENGINE=fp32|bf16x3|bf16x2v overrides
- *   VS_ENGINE_FP32_MFMA  v_mfma_f32_32x32x2_f32 on the fp32 rows
- *   VS_ENGINE_BF16X3     v_mfma_f32_32x32x16_bf16 on an exact 3-plane bf16 split of
- *                        every fp32 value (hi+mid+lo == v), 6 products per term
- *                        (dropped terms < 2^-24 |x q|): fp32-accurate, 2.7x the
- *                        fp32 matrix rate; keeps a blocked fp32 copy of the rows
- *   VS_ENGINE_BF16X2_VERIFY  filter and verify: a 3-product pass (hi/mid planes)
- *                        keeps 24-32 candidates per query, a rigorous error bound
- *                        proves the exact top-k is among them, and the candidates
- *                        are rescored exactly; queries the bound cannot settle are
- *                        redone by BF16X3 — results identical to an exact engine
- * bf16 indexes ignore it. */
+ *   VS_ENGINE_AUTO          library default: BF16_VERIFY where it applies (IP
+ *                           k <= 28, L2 / cosine k <= 56), else FP32_MFMA;
+ *                           env VS_ENGINE=fp32|bf16v overrides
+ *   VS_ENGINE_FP32_MFMA     v_mfma_f32_32x32x2_f32 on the fp32 rows
+ *   VS_ENGINE_BF16_VERIFY   filter and verify: one bf16 MFMA product per fp32
+ *                           product (bf16 copies of rows and queries) keeps the
+ *                           best candidates of every query, a rigorous error bound
+ *                           proves the exact top-k is among them, the candidates
+ *                           are rescored exactly, and queries the bound cannot
+ *                           settle are redone by FP32_MFMA — results identical to
+ *                           an exact engine
+ * bf16 indexes ignore it (bf16 MFMA on the stored values). */
 #define VS_ENGINE_AUTO 0
 #define VS_ENGINE_FP32_MFMA 1
-#define VS_ENGINE_BF16X3 2
-#define VS_ENGINE_BF16X2_VERIFY 3
+#define VS_ENGINE_BF16_VERIFY 3
 int vs_set_engine(vs_index* idx, int engine);
 
 /* Rows [0,ntotal) get labels id_base + row.  Used by the row-sharded multi-GPU
@@ -132,8 +129,14 @@ int vs_set_engine(vs_index* idx, int engine);
 int vs_set_id_base(vs_index* idx, int64_t id_base);
 
 /* faiss IndexFlat::search(n, x, k, D, I) (knn_L2sqr / knn_inner_product):
- * exact top-k, D ascending squared-L2 or descending inner product, ties broken
- * by the lower label, k > ntotal padded with (+FLT_MAX | -FLT_MAX, -1).
+ * exact top-k, D ascending squared-L2 or descending inner product, k > ntotal
+ * padded with (+FLT_MAX | -FLT_MAX, -1).  Ties follow faiss's heaps: L2 keeps the
+ * lower label first; inner product follows faiss's CMin-heap rule (equal scores
+ * come out in DESCENDING label order, and which tied labels stay depends on the
+ * labels of the better rows — vs_support.hip faiss_ip_tie_order, exact for
+ * k <= 32).  L2 calls with n < 20 use faiss's sequential branch (direct sum of
+ * squares), n >= 20 the BLAS branch (|q|^2 + |x|^2 - 2 q.x clamped at 0).
+ * Asynchronous on `stream` when every buffer is on the device (no host wait).
  * Caller: FAISS.similarity_search_with_score_by_vector, reached from
  * src/recommendation_api/mcp_book_server.py:142, candidate_builder.py:187,321,
  * service.py:529,627.  D is n*k float32, I is n*k int64. */
@@ -181,7 +184,7 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
  * distance+top-k kernel) is bracketed by HIP events on the launch stream.
  * vs_timer_read synchronises those events and returns the summed kernel time in
  * milliseconds and the number of kernel dispatches inside the timed spans since
- * the last reset (gemm_topk_x3 cuts one search into several dispatches). */
+ * the last reset (gemm_topk_x1 cuts one search into several dispatches). */
 int vs_timer_enable(int on);
 /* Queries searched by the filter-and-verify engine and how many of them the
  * exact engine had to redo, since the last reset (reset != 0 clears them). */
@@ -192,8 +195,8 @@ int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset);
 int vs_filter_wide_stats(int64_t* wide);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
-/* Name of the fused search kernel the last search launched ("gemm_topk_x2f",
- * "gemm_topk_x3", "gemm_topk", "skinny_topk" or "gemv_topk"). */
+/* Name of the fused search kernel the last search launched ("gemm_topk_x1",
+ * "gemm_topk", "skinny_topk" or "gemv_topk"). */
 const char* vs_timer_kernel(void);
 
 #ifdef __cplusplus

@@ -184,7 +184,7 @@ def test_selfjoin_filter_fallback_drops_self(vf, k):
     base = _rand(30, 96, 72)
     x = np.concatenate([np.repeat(base, 40, axis=0), _rand(600, 96, 73)])
     index = vf.IndexFlatIP(96)
-    index.set_engine("bf16x2v")
+    index.set_engine("bf16v")
     index.add(x)
     _lib.filter_stats(reset=True)
     S, I = index.selfjoin(k)
@@ -391,7 +391,7 @@ def test_small_batch_ragged_rows(vf, metric):
             _check(vf, xb, _rand(nq, 64, 33), 8, metric)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "bf16x3", "bf16x2v"])
+@pytest.mark.parametrize("engine", ["fp32", "bf16v"])
 @pytest.mark.parametrize("metric", [L2, IP])
 def test_large_batch_engines(vf, engine, metric):
     """Every large-batch engine of fp32 indexes meets the fp32 tolerance."""
@@ -408,15 +408,15 @@ def test_large_batch_engines(vf, engine, metric):
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
-@pytest.mark.parametrize("d", [64, 128, 192, 96, 160])
-def test_bf16x2v_stage_shapes(vf, metric, d):
-    """The filter pass takes two K-blocks per stage when ld % 64 == 0 (d = 64, 128,
-    192: one, two, three stage pairs per tile) and one otherwise (96, 160);
-    several tiles, a ragged last tile and a ragged query tile."""
+@pytest.mark.parametrize("d", [64, 128, 192, 96, 160, 1536])
+def test_filter_step_shapes(vf, metric, d):
+    """The filter pass walks K in 64-element steps of the zero-padded rows (d = 96
+    and 160 pad to 128 and 192); several tiles, a ragged last tile and a ragged
+    query tile."""
     xb = _rand(1800, d, 46)
     xq = _rand(300, d, 47)
     index = vf.IndexFlat(d, metric)
-    index.set_engine("bf16x2v")
+    index.set_engine("bf16v")
     index.add(xb)
     for k in (1, 10):
         D, I = index.search(xq, k)
@@ -425,16 +425,17 @@ def test_bf16x2v_stage_shapes(vf, metric, d):
         assert not bad, (d, k, bad[:5])
 
 
-@pytest.mark.parametrize("engine", ["bf16x3", "bf16x2v"])
-def test_blocked_rows_follow_mutations(vf, engine):
-    """The lazily built blocked copy of the rows tracks add / remove_ids / reset."""
+def test_filter_plane_follows_mutations(vf):
+    """The bf16 plane and residual norms follow add / remove_ids / reset /
+    storage growth (they are kept in step with the rows, never rebuilt lazily)."""
     xb = _rand(3000, 96, 42)
     xq = _rand(150, 96, 43)
     index = vf.IndexFlatIP(96)
-    index.set_engine(engine)
+    index.set_engine("bf16v")
     index.add(xb[:2000])
-    D, I = index.search(xq, 10)  # builds planes for 2000 rows
-    index.add(xb[2000:])  # planes now stale for the tail
+    D, I = index.search(xq, 10)
+    for i0 in range(2000, 3000, 250):  # several growths
+        index.add(xb[i0:i0 + 250])
     D, I = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
     assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
@@ -451,7 +452,7 @@ def test_blocked_rows_follow_mutations(vf, engine):
     assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "bf16x3", "bf16x2v"])
+@pytest.mark.parametrize("engine", ["fp32", "bf16v"])
 def test_selfjoin_engines(vf, engine):
     x = _rand(2000, 256, 44)
     index = vf.IndexFlatIP(256)
@@ -466,27 +467,30 @@ def test_selfjoin_engines(vf, engine):
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
-def test_bf16x3_ragged_shapes(vf, metric):
-    """Odd d (column padding), ragged row tiles and several query tiles per split."""
-    for n, d, nq in ((5000, 100, 1000), (257, 1536, 129), (70001, 32, 256)):
+def test_filter_ragged_shapes(vf, metric):
+    """Odd d (column padding), ragged row tiles, several query tiles per split,
+    fewer rows than one tile."""
+    for n, d, nq in ((5000, 100, 1000), (257, 1536, 129), (70001, 32, 256), (40, 64, 300)):
         xb = _rand(n, d, 45)
         xq = _rand(nq, d, 46)
         index = vf.IndexFlat(d, metric)
-        index.set_engine("bf16x3")
+        index.set_engine("bf16v")
         index.add(xb)
-        D, I = index.search(xq, 7)
-        Dr, Ir = flat.knn_exact(xb, xq, 7, metric)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
-        assert not bad, (n, d, nq, bad[:5])
+        for k in (5, 10):
+            D, I = index.search(xq, k)
+            Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+            assert not bad, (n, d, nq, k, bad[:5])
 
 
-def test_bf16x3_repeatable(vf):
-    """Race screen for the 4-buffer LDS-DMA pipeline: repeated launches over a
-    corpus large enough to keep every CU busy give identical, correct lists."""
+def test_filter_repeatable(vf):
+    """Race screen for the double-buffered LDS-DMA pipeline and the chunked
+    launches: repeated searches over a corpus large enough to keep every CU busy
+    give identical, correct lists."""
     xb = _rand(120000, 256, 47)
     xq = _rand(640, 256, 48)
     index = vf.IndexFlatIP(256)
-    index.set_engine("bf16x3")
+    index.set_engine("bf16v")
     index.add(xb)
     D0, I0 = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
@@ -497,12 +501,12 @@ def test_bf16x3_repeatable(vf):
         np.testing.assert_array_equal(D, D0)
 
 
-def test_bf16x3_selfjoin_offsets(vf):
-    """Self-join query tiles taken from the index's own planes at an offset, with
-    and without self exclusion."""
+def test_filter_selfjoin_offsets(vf):
+    """Self-join query tiles taken from the index's own bf16 plane at an offset,
+    with and without self exclusion."""
     x = _rand(3000, 128, 49)
     index = vf.IndexFlatIP(128)
-    index.set_engine("bf16x3")
+    index.set_engine("bf16v")
     index.add(x)
     Sr, Ir = flat.pgvector_cosine_topk(x, 12)
     S, I = index.selfjoin(12, q0=1000, nq=700)
@@ -514,21 +518,19 @@ def test_bf16x3_selfjoin_offsets(vf):
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
-def test_bf16x2v_matches_exact_engine(vf, metric):
+def test_filter_matches_exact_engine(vf, metric):
     """The filter-and-verify engine returns the exact lists: oracle parity (ids
-    equal except documented ties) and the exact engine's ids on (nearly) every
-    row — the two round their fp32 scores differently, so an exact near-tie may
-    order differently."""
+    equal except documented ties) and the fp32 engine's ids on (nearly) every row
+    — the two round their fp32 scores differently, so an exact near-tie may order
+    differently."""
     xb = _rand(200000, 256, 60)
     xq = _rand(600, 256, 61)
     index = vf.IndexFlat(256, metric)
     index.add(xb)
-    for k in (1, 4, 10, 12, 16):
-        if metric == IP and 2 * k - 1 + 8 > 32:
-            continue
-        index.set_engine("bf16x3")
+    for k in (1, 4, 10, 12, 16, 28):
+        index.set_engine("fp32")
         De, Ie = index.search(xq, k)
-        index.set_engine("bf16x2v")
+        index.set_engine("bf16v")
         D, I = index.search(xq, k)
         Dr, Ir = flat.knn_exact(xb, xq, k, metric)
         bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
@@ -538,31 +540,17 @@ def test_bf16x2v_matches_exact_engine(vf, metric):
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
-def test_bf16x2v_ragged_shapes(vf, metric):
-    for n, d, nq in ((5000, 100, 1000), (257, 1536, 129), (70001, 32, 256), (40, 64, 300)):
-        xb = _rand(n, d, 62)
-        xq = _rand(nq, d, 63)
-        index = vf.IndexFlat(d, metric)
-        index.set_engine("bf16x2v")
-        index.add(xb)
-        for k in (5, 10):
-            D, I = index.search(xq, k)
-            Dr, Ir = flat.knn_exact(xb, xq, k, metric)
-            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
-            assert not bad, (n, d, nq, k, bad[:5])
-
-
-@pytest.mark.parametrize("metric", [L2, IP])
-def test_bf16x2v_falls_back_on_ties(vf, metric):
+def test_filter_falls_back_on_ties(vf, metric):
     """Duplicated rows tie exactly, so the bound cannot separate the candidates:
-    those queries go to the exact engine, and the results keep oracle parity."""
+    those queries are redone by the exact engine (on the device, gathered by a
+    device-side list), and the results keep oracle parity."""
     from vsearch import _lib
 
     base = _rand(300, 64, 64)
     xb = np.concatenate([np.repeat(base[:20], 40, axis=0), base[20:]])  # 800 dup + 280
     xq = np.concatenate([base[:20] + 0.001 * _rand(20, 64, 65), _rand(300, 64, 66)])
     index = vf.IndexFlat(64, metric)
-    index.set_engine("bf16x2v")
+    index.set_engine("bf16v")
     index.add(xb)
     _lib.filter_stats(reset=True)
     D, I = index.search(xq, 10)
@@ -573,61 +561,32 @@ def test_bf16x2v_falls_back_on_ties(vf, metric):
     assert not bad, bad[:5]
 
 
-def test_auto_engine_adapts_to_fallback_rate(vf):
-    """Auto engine choice: when most queries of the recent filter passes fall back
-    (every query near a 40-fold duplicated row), large searches go straight to the
-    exact engine, with one filter pass every 16 searches to re-measure; results
-    keep oracle parity throughout."""
+def test_filter_every_query_falls_back(vf):
+    """Every row tied 40 times and every query next to one: the whole batch goes
+    to the exact redo (more flagged queries than one gathered tile, several query
+    tiles) and keeps oracle parity."""
     from vsearch import _lib
 
     base = _rand(300, 64, 70)
-    xb = np.repeat(base, 40, axis=0)  # every row tied 40 times
+    xb = np.repeat(base, 40, axis=0)
     xq = np.repeat(base, 4, axis=0)[:1024] + 0.001 * _rand(1024, 64, 71)
-    index = vf.IndexFlatIP(64)  # engine left on auto
-    index.add(xb)
-    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
-    filtered = []
-    for _ in range(17):
-        _lib.filter_stats(reset=True)
-        D, I = index.search(xq, 10)
-        filtered.append(_lib.filter_stats(reset=True)[0])
-        bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
-        assert not bad, bad[:5]
-    assert filtered[0] == 1024  # first search: filter pass, (nearly) all fall back
-    assert sum(1 for f in filtered[1:] if f) <= 2  # then the exact engine, re-probes only
-
-
-def test_bf16x2v_second_pass_settles_near_duplicates(vf):
-    """24 near-copies of every base row: with 24 candidates the bound cannot
-    separate a query's copies, with 64 it can (the next rows are far below), so
-    the second filter pass settles every flagged query and none reaches the exact
-    engine; results keep oracle parity."""
-    from vsearch import _lib
-
-    base = _rand(60, 64, 74)
-    xb = np.repeat(base, 24, axis=0) + 1e-4 * _rand(1440, 64, 75)
-    xb = np.concatenate([xb, _rand(2000, 64, 76)])
-    xq = base + 1e-4 * _rand(60, 64, 77)
-    xq = np.concatenate([xq, _rand(196, 64, 78)])
     index = vf.IndexFlatIP(64)
-    index.set_engine("bf16x2v")
     index.add(xb)
     _lib.filter_stats(reset=True)
     D, I = index.search(xq, 10)
-    nq, n_exact = _lib.filter_stats(reset=True)
-    assert nq == xq.shape[0]
-    assert n_exact == 0
+    nq, nfb = _lib.filter_stats(reset=True)
+    assert nq == 1024 and nfb > 900
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
     bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
     assert not bad, bad[:5]
 
 
-def test_bf16x2v_wide_check_settles_scattered_near_duplicates(vf):
+def test_filter_wide_check_settles_scattered_near_duplicates(vf):
     """40 near-copies of each base row, scattered over the corpus: the KF merged
     candidates are all copies, so the first check flags those queries; every lane
     list holds only one or two copies, so the wide check (all list entries below
-    the list floors rescored) settles them without a second pass or the exact
-    engine; results keep oracle parity."""
+    the list floors rescored) settles them without the exact engine; results keep
+    oracle parity."""
     from vsearch import _lib
 
     base = _rand(60, 64, 80)
@@ -637,7 +596,7 @@ def test_bf16x2v_wide_check_settles_scattered_near_duplicates(vf):
     xq = np.concatenate([base + 1e-4 * _rand(60, 64, 84), _rand(196, 64, 85)])
     for metric in (IP, L2):
         index = vf.IndexFlat(64, metric)
-        index.set_engine("bf16x2v")
+        index.set_engine("bf16v")
         index.add(xb)
         _lib.filter_stats(reset=True)
         D, I = index.search(xq, 10)
@@ -648,6 +607,47 @@ def test_bf16x2v_wide_check_settles_scattered_near_duplicates(vf):
         Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
         bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
         assert not bad, bad[:5]
+
+
+def test_search_device_is_stream_async(vf):
+    """A device-buffer search queues its work and returns: the host does not
+    wait for the kernels (the filter engine keeps its counts on the device)."""
+    torch = pytest.importorskip("torch")
+    import time
+
+    xb = _rand(200000, 512, 90)
+    index = vf.IndexFlatIP(512)
+    index.add(xb)
+    xq = torch.from_numpy(_rand(2048, 512, 91)).cuda()
+    D = torch.empty((2048, 10), dtype=torch.float32, device="cuda")
+    I = torch.empty((2048, 10), dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    index.search_device(xq.data_ptr(), 2048, 10, D.data_ptr(), I.data_ptr(), st)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(4):
+        index.search_device(xq.data_ptr(), 2048, 10, D.data_ptr(), I.data_ptr(), st)
+    t_enqueue = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t_total = time.perf_counter() - t0
+    assert t_enqueue < 0.5 * t_total, (t_enqueue, t_total)
+    Dh, Ih = index.search(xq.cpu().numpy(), 10)
+    np.testing.assert_array_equal(I.cpu().numpy(), Ih)
+
+
+def test_l2_small_calls_use_faiss_sequential_formula(vf):
+    """faiss switches formulas on the call's query count (nq < 20: direct sum of
+    squares; nq >= 20: |q|^2 + |x|^2 - 2 q.x): 9..19-query L2 calls match the C
+    restatement of the sequential branch bit for bit, like 1..8."""
+    xb = _rand(3000, 48, 92)
+    for nq in (1, 8, 9, 13, 19):
+        xq = _rand(nq, 48, 93 + nq)
+        index = vf.IndexFlatL2(48)
+        index.add(xb)
+        D, I = index.search(xq, 10)
+        Dc, Ic = cfaiss.knn_seq(xb, xq, 10, L2)
+        np.testing.assert_array_equal(I, Ic)
+        np.testing.assert_allclose(D, Dc, rtol=2e-6, atol=1e-5)
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
