@@ -487,7 +487,9 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
     const int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
     part.P = nblocks;
     const int step = kGemvMaxQ;  // queries per corpus pass
-    const size_t n = (size_t)std::min(nq, step) * part.P * KP;
+    // the kernel writes lists for its padded query count (1, 2, 4 or 8)
+    const int nql = nq <= 2 ? nq : (nq <= 4 ? 4 : kGemvMaxQ);
+    const size_t n = (size_t)nql * part.P * KP;
     VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
     for (int q0 = 0; q0 < nq; q0 += step) {

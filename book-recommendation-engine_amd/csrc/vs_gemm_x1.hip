@@ -51,6 +51,23 @@ constexpr int kX1ChunkTiles = 16;     // database tiles per workgroup per launch
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 
+// LDS-DMA of 16 B per lane into the wave-uniform LDS byte address `lds` (M0 is
+// written and restored inside the statement; cdna_hip_programming.md §5.7).
+// hipcc does not count it, so it inserts no waits of its own around it: the
+// caller retires it with a counted vmcnt before the barrier that precedes the
+// ds_reads of that image (the builtin form makes hipcc assume every later LDS
+// read may alias it and drain vmcnt to 0 before them).  No VGPR destination,
+// so no register hazard.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+
 __device__ __forceinline__ float sel16(const f32x16& v, int i) {
   float r = v[0];
 #pragma unroll
@@ -277,6 +294,254 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The deep-pipeline form (default): K-steps of 32 elements (64 B per row), NBUF
+// LDS images of 32 KB (both operand tiles of one step), NBUF-1 steps in flight.
+// Each wave issues the 4 LDS-DMA pieces of step s+NBUF-1 before computing step
+// s, then retires step s+1 with a COUNTED vmcnt (the younger NBUF-2 steps stay
+// in flight across the raw s_barrier; cdna_hip_programming.md "Pipelining
+// across barriers").  Loads past the last step re-read it (unconditional
+// loads keep the count fixed; nothing reads those images).  64-B LDS rows:
+// chunk c of row r at c ^ ((r >> 2) & 3) — conflict-free ds_read_b128 for the
+// 32x32x16 fragments, and one per-lane source offset for every 16-row group.
+//
+// XCD blocking (a 256-workgroup grid, one per CU): the 32 workgroups of an XCD
+// take QG query tiles x DG database splits (QG = min(nqt, 4)), so each XCD's L2
+// serves a query tile to DG workgroups and a database tile to QG of them.
+template <int KR, int MODE, int NBUF>
+__global__ __launch_bounds__(512, 1) void gemm_topk_x1d(
+    const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
+    const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
+    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
+    int KP, float* __restrict__ pkey, int* __restrict__ pid) {
+  constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int c32 = lane & 31;
+  const int wr = w & 1;
+  const int wq = w >> 1;
+
+  int qt, sp;
+  {
+    const int nblk = gridDim.x;
+    const int b = blockIdx.x;
+    const int QG = nqt < 4 ? nqt : 4;
+    const int G = nqt / QG;
+    if (nblk == 256 && nqt * nsplit == 256 && nqt % QG == 0 && G <= 8 && 8 % G == 0) {
+      const int xcd = b & 7, slot = b >> 3, DG = 32 / QG;
+      qt = (xcd % G) * QG + slot % QG;
+      sp = (xcd / G) * DG + slot / QG;
+    } else {  // bijective remap: the workgroups of a split on one XCD
+      const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
+      const int lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+      qt = lb % nqt;
+      sp = lb / nqt;
+    }
+  }
+  const int s0 = (int)((int64_t)sp * ntiles / nsplit);
+  const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
+  const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
+  const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
+
+  int gq[2], selfrow[2];
+  float qa[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    gq[qb] = qt * kT + 64 * wq + 32 * qb + c32;
+    qa[qb] = 0.0f;
+    if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
+    selfrow[qb] = self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
+  }
+  const int P = nsplit * 4;
+  const int pl = sp * 4 + wr * 2 + h;
+  float lk[2][KR];
+  int li[2][KR];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+    if (chunk == 0) {
+      list_init<KR, int>(lk[qb], li[qb]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < KR; ++e) {
+        lk[qb][e] = pkey[o + e];
+        li[qb][e] = pid[o + e];
+      }
+    }
+  }
+
+  // Settle the loads above (resumed lists, query aux) before the pipeline: an
+  // asm use makes hipcc wait for them here, once, instead of inside the loop,
+  // where its vmcnt would drain the LDS-DMA steps in flight.
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
+    asm volatile("" ::"v"(qa[qb]));
+  }
+
+  if (t1 > t0) {  // uniform over the workgroup
+    const uint32_t ldb = (uint32_t)ld * 2u;
+    // lane L of an instruction moves 16 B of row L>>2 of a 16-row group into slot
+    // L&3 of that 64-B LDS row; source chunk = slot ^ ((row >> 2) & 3) =
+    // (L & 3) ^ (L >> 4) for every group
+    const uint32_t soff = (uint32_t)(lane >> 2) * ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
+    const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld);
+    const int fsw = (c32 >> 2) & 3;
+    const int nsteps = (t1 - t0) * nksteps;
+
+    // wave w stages row groups 2w, 2w+1 (rows 32w .. 32w+31) of both tiles
+    auto stage = [&](int s) {
+      s = s < nsteps ? s : nsteps - 1;  // past the end: re-read the last step
+      const int t = t0 + s / nksteps, ks = s % nksteps;
+      char* dX = smem + (s % NBUF) * 2 * kStepB;
+      char* dQ = dX + kStepB;
+      const char* xs = (const char*)(XH + (int64_t)t * kT * ld) + ks * 64;
+      const char* qs = qtile + ks * 64;
+      const uint32_t lx = (uint32_t)(uintptr_t)VS_LDS(dX) + (uint32_t)(2 * w) * 1024u;
+      const uint32_t lq = (uint32_t)(uintptr_t)VS_LDS(dQ) + (uint32_t)(2 * w) * 1024u;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t o = soff + (uint32_t)(32 * w + 16 * i) * ldb;
+        glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + i * 1024u));
+        glds16(qs + o, __builtin_amdgcn_readfirstlane(lq + i * 1024u));
+      }
+    };
+
+    f32x16 acc[4][2];
+    auto zero = [&]() {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[rb][qb][r] = 0.0f;
+    };
+    auto mma = [&](int s) {
+      const char* base = smem + (s % NBUF) * 2 * kStepB;
+      const char* cX = base + (128 * wr + c32) * 64;
+      const char* cQ = base + kStepB + (64 * wq + c32) * 64;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int co = ((2 * s2 + h) ^ fsw) * 16;
+        const uint4 b0 = *(const uint4*)(cQ + co);
+        const uint4 b1 = *(const uint4*)(cQ + 32 * 64 + co);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const uint4 a = *(const uint4*)(cX + rb * 32 * 64 + co);
+          acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b0), acc[rb][0], 0, 0, 0);
+          acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b1), acc[rb][1], 0, 0, 0);
+        }
+      }
+    };
+    auto epilogue = [&](int t) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int r0 = t * kT + 128 * wr + 32 * rb;
+        f32x4 xa[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
+            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          f32x16 key;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = acc[rb][qb][jj * 4 + e];
+              float kk;
+              if constexpr (MODE == MODE_IP) {
+                kk = -v;
+              } else if constexpr (MODE == MODE_L2) {
+                kk = l2_from_ip(qa[qb], xa[jj][e], v);
+              } else {
+                kk = -(v * (qa[qb] * xa[jj][e]));
+              }
+              key[jj * 4 + e] = kk;
+            }
+          }
+          float m = key[0];
+#pragma unroll
+          for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
+          if (m <= lk[qb][KR - 1]) {
+            uint32_t cm = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              const bool c = row < ntotal && row != selfrow[qb] &&
+                             lex_less(key[r], row, lk[qb][KR - 1], li[qb][KR - 1]);
+              cm |= (uint32_t)c << r;
+            }
+            while (cm) {
+              const int bi = __builtin_ctz(cm);
+              cm &= cm - 1;
+              const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+              list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+            }
+          }
+        }
+      }
+    };
+
+    if (VS_X1_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
+
+    // prologue: steps 0 .. NBUF-2 in flight, retire step 0
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s) stage(s);
+    if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    zero();
+    for (int s = 0; s < nsteps; ++s) {
+      stage(s + NBUF - 1);  // into the image step s-1 used (every wave is past it)
+      mma(s);
+      if ((s + 1) % nksteps == 0) {
+        epilogue(t0 + s / nksteps);
+        zero();
+      }
+      // retire step s+1 (this wave's pieces), keep the younger steps in flight
+      if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
+  }
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+#pragma unroll
+    for (int e = 0; e < KR; ++e) {
+      pkey[o + e] = lk[qb][e];
+      pid[o + e] = li[qb][e];
+    }
+    for (int e = KR; e < KP; ++e) {
+      pkey[o + e] = FLT_MAX;
+      pid[o + e] = -1;
+    }
+  }
+}
+
+// Pipeline form: VS_X1_PIPE=2 (64-element steps, 2 images), 4 or 5 (32-element
+// steps, that many images); default 4.
+static int x1_pipe() {
+  static const int v = [] {
+    const char* e = getenv("VS_X1_PIPE");
+    const int p = e ? atoi(e) : 0;
+    return p == 2 || p == 4 || p == 5 ? p : 4;
+  }();
+  return v;
+}
+
 template <int KR, int MODE>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
@@ -288,11 +553,20 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
-  const int nksteps = (int)(a.ld / 64);
+  const int pipe = x1_pipe();
   for (int c = 0; c < nchunk; ++c) {
-    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE>), dim3(nqt * a.nsplit), dim3(512), 0, st, a.XH,
-                       a.xaux, a.QH, a.qaux, a.nqa, a.ld, nksteps, a.ntotal, ntiles, a.nsplit, nqt,
-                       a.self0, c, nchunk, part.KP, part.key, part.id);
+    if (pipe == 2)
+      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE>), dim3(nqt * a.nsplit), dim3(512), 0, st, a.XH,
+                         a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 64), a.ntotal, ntiles,
+                         a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    else if (pipe == 5)
+      hipLaunchKernelGGL((gemm_topk_x1d<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
+                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    else
+      hipLaunchKernelGGL((gemm_topk_x1d<KR, MODE, 4>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
+                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
