@@ -531,13 +531,263 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1d(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The split-step form (default): as gemm_topk_x1d, but each 32-element step is
+// cut at its middle by the barrier, and the fragment reads run one half-step
+// ahead of the MFMAs:
+//     MFMAs of sub-step 0 (fragments read during the previous step)
+//     ds_read the sub-step 1 fragments
+//     wait for this wave's pieces of step s+1, s_barrier
+//     LDS-DMA of step s+NBUF-1 into the image step s-1 used (every wave has
+//       passed this barrier, so every read of that image is done)
+//     MFMAs of sub-step 1, then ds_read sub-step 0 of step s+1 (its image is
+//       complete: every wave's pieces were retired before this barrier)
+// so the LDS read latency after a barrier hides under MFMAs instead of
+// stalling both waves of a SIMD at every step.  Load and position cursors are
+// incremental (no divisions in the loop).
+template <int KR, int MODE, int NBUF>
+__global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
+    const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
+    const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
+    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
+    int KP, float* __restrict__ pkey, int* __restrict__ pid) {
+  constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
+  constexpr int D = NBUF - 1;      // steps in flight
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int c32 = lane & 31;
+  const int wr = w & 1;
+  const int wq = w >> 1;
+
+  int qt, sp;
+  {
+    const int nblk = gridDim.x;
+    const int b = blockIdx.x;
+    const int QG = nqt < 4 ? nqt : 4;
+    const int G = nqt / QG;
+    if (nblk == 256 && nqt * nsplit == 256 && nqt % QG == 0 && G <= 8 && 8 % G == 0) {
+      const int xcd = b & 7, slot = b >> 3, DG = 32 / QG;
+      qt = (xcd % G) * QG + slot % QG;
+      sp = (xcd / G) * DG + slot / QG;
+    } else {
+      const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
+      const int lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+      qt = lb % nqt;
+      sp = lb / nqt;
+    }
+  }
+  const int s0 = (int)((int64_t)sp * ntiles / nsplit);
+  const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
+  const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
+  const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
+
+  int gq[2], selfrow[2];
+  float qa[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    gq[qb] = qt * kT + 64 * wq + 32 * qb + c32;
+    qa[qb] = 0.0f;
+    if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
+    selfrow[qb] = self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
+  }
+  const int P = nsplit * 4;
+  const int pl = sp * 4 + wr * 2 + h;
+  float lk[2][KR];
+  int li[2][KR];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+    if (chunk == 0) {
+      list_init<KR, int>(lk[qb], li[qb]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < KR; ++e) {
+        lk[qb][e] = pkey[o + e];
+        li[qb][e] = pid[o + e];
+      }
+    }
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
+    asm volatile("" ::"v"(qa[qb]));
+  }
+
+  if (t1 > t0) {  // uniform over the workgroup
+    const uint32_t ldb = (uint32_t)ld * 2u;
+    const uint32_t soff = (uint32_t)(lane >> 2) * ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
+    const int fsw = (c32 >> 2) & 3;
+    const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld) + (uint32_t)(32 * w) * ldb;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
+    const int nsteps = (t1 - t0) * nksteps;
+
+    // load cursor: the step it issues next (clamped to the last one)
+    int ls = 0, lt = t0, lk_ = 0, lbuf = 0;
+    auto stage_next = [&]() {
+      const char* xs = (const char*)(XH + (int64_t)lt * kT * ld) + (uint32_t)(32 * w) * ldb +
+                       lk_ * 64;
+      const char* qs = qtile + lk_ * 64;
+      const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t o = soff + (uint32_t)(16 * i) * ldb;
+        glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + i * 1024u));
+        glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + i * 1024u));
+      }
+      if (ls + 1 < nsteps) {  // advance (past the end: keep re-reading the last step)
+        ++ls;
+        if (++lk_ == nksteps) {
+          lk_ = 0;
+          ++lt;
+        }
+      }
+      lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
+    };
+
+    f32x16 acc[4][2];
+    auto zero = [&]() {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[rb][qb][r] = 0.0f;
+    };
+    // fragments of one sub-step: A (database rows) x4, B (queries) x2
+    uint4 fa0[4], fb0[2], fa1[4], fb1[2];
+    auto rd = [&](int buf, int s2, uint4 (&fa)[4], uint4 (&fb)[2]) {
+      const char* base = smem + buf * 2 * kStepB;
+      const int co = ((2 * s2 + h) ^ fsw) * 16;
+      const char* cX = base + (128 * wr + c32) * 64 + co;
+      const char* cQ = base + kStepB + (64 * wq + c32) * 64 + co;
+      fb[0] = *(const uint4*)cQ;
+      fb[1] = *(const uint4*)(cQ + 32 * 64);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
+    };
+    auto mfma = [&](const uint4 (&fa)[4], const uint4 (&fb)[2]) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
+        acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
+      }
+    };
+    auto epilogue = [&](int t) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int r0 = t * kT + 128 * wr + 32 * rb;
+        f32x4 xa[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
+            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          f32x16 key;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = acc[rb][qb][jj * 4 + e];
+              float kk;
+              if constexpr (MODE == MODE_IP) {
+                kk = -v;
+              } else if constexpr (MODE == MODE_L2) {
+                kk = l2_from_ip(qa[qb], xa[jj][e], v);
+              } else {
+                kk = -(v * (qa[qb] * xa[jj][e]));
+              }
+              key[jj * 4 + e] = kk;
+            }
+          }
+          float m = key[0];
+#pragma unroll
+          for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
+          if (m <= lk[qb][KR - 1]) {
+            uint32_t cm = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              const bool c = row < ntotal && row != selfrow[qb] &&
+                             lex_less(key[r], row, lk[qb][KR - 1], li[qb][KR - 1]);
+              cm |= (uint32_t)c << r;
+            }
+            while (cm) {
+              const int bi = __builtin_ctz(cm);
+              cm &= cm - 1;
+              const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+              list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+            }
+          }
+        }
+      }
+    };
+
+    if (VS_X1_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
+
+    // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
+#pragma unroll
+    for (int i = 0; i < D; ++i) stage_next();
+    if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    zero();
+    rd(0, 0, fa0, fb0);
+    int buf = 0, t = t0, ks = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      mfma(fa0, fb0);
+      rd(buf, 1, fa1, fb1);
+      // retire step s+1 (this wave's pieces); the younger D-2 steps stay in flight
+      if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      stage_next();  // step s+D into the image of step s-1
+      mfma(fa1, fb1);
+      const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+      if (++ks == nksteps) {
+        ks = 0;
+        epilogue(t);
+        zero();
+        ++t;
+      }
+      rd(nbuf, 0, fa0, fb0);  // past the end: a harmless read of a stale image
+      buf = nbuf;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
+  }
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+#pragma unroll
+    for (int e = 0; e < KR; ++e) {
+      pkey[o + e] = lk[qb][e];
+      pid[o + e] = li[qb][e];
+    }
+    for (int e = KR; e < KP; ++e) {
+      pkey[o + e] = FLT_MAX;
+      pid[o + e] = -1;
+    }
+  }
+}
+
 // Pipeline form: VS_X1_PIPE=2 (64-element steps, 2 images), 4 or 5 (32-element
-// steps, that many images); default 4.
+// steps, that many images, one barrier per step), 14 / 15 (the split-step form
+// with 4 / 5 images); default 14.
 static int x1_pipe() {
   static const int v = [] {
     const char* e = getenv("VS_X1_PIPE");
     const int p = e ? atoi(e) : 0;
-    return p == 2 || p == 4 || p == 5 ? p : 4;
+    return p == 2 || p == 4 || p == 5 || p == 14 || p == 15 ? p : 14;
   }();
   return v;
 }
@@ -559,6 +809,14 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
       hipLaunchKernelGGL((gemm_topk_x1<KR, MODE>), dim3(nqt * a.nsplit), dim3(512), 0, st, a.XH,
                          a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 64), a.ntotal, ntiles,
                          a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    else if (pipe == 14)
+      hipLaunchKernelGGL((gemm_topk_x1e<KR, MODE, 4>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
+                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    else if (pipe == 15)
+      hipLaunchKernelGGL((gemm_topk_x1e<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
+                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     else if (pipe == 5)
       hipLaunchKernelGGL((gemm_topk_x1d<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                          a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,

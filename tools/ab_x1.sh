@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/ab_${TAG}
 mkdir -p "$OUT"
 for round in 1 2; do
-  for p in 2 4 5; do
+  for p in ${PIPES:-2 4 5}; do
     VS_X1_PIPE=$p timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --batch1-steps 0 \
       --no-cpu-baseline "$@" > "$OUT/pipe${p}_r${round}.log" 2>&1 || { echo "pipe $p failed"; exit 1; }
     python3 - "$OUT/pipe${p}_r${round}.log" "$p" <<'PY'
