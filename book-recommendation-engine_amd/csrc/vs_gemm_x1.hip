@@ -626,28 +626,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
     const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
     const int nsteps = (t1 - t0) * nksteps;
 
-    // load cursor: the step it issues next (clamped to the last one)
+    // load cursor: the step it issues next (past the end it keeps re-reading
+    // the last step: unconditional loads keep the vmcnt counts fixed)
     int ls = 0, lt = t0, lk_ = 0, lbuf = 0;
-    auto stage_next = [&]() {
-      const char* xs = (const char*)(XH + (int64_t)lt * kT * ld) + (uint32_t)(32 * w) * ldb +
-                       lk_ * 64;
-      const char* qs = qtile + lk_ * 64;
-      const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t o = soff + (uint32_t)(16 * i) * ldb;
-        glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + i * 1024u));
-        glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + i * 1024u));
-      }
-      if (ls + 1 < nsteps) {  // advance (past the end: keep re-reading the last step)
-        ++ls;
-        if (++lk_ == nksteps) {
-          lk_ = 0;
-          ++lt;
-        }
-      }
-      lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
-    };
 
     f32x16 acc[4][2];
     auto zero = [&]() {
@@ -676,6 +657,30 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
         acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
         acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
       }
+    };
+    auto mfma_rb = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
+      acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
+      acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
+    };
+    // the four LDS-DMA pieces of the load cursor's step, one at a time
+    auto stage_piece = [&](int i) {
+      const char* xs = (const char*)(XH + (int64_t)lt * kT * ld) + (uint32_t)(32 * w) * ldb +
+                       lk_ * 64;
+      const char* qs = qtile + lk_ * 64;
+      const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
+      const uint32_t o = soff + (uint32_t)(16 * (i >> 1)) * ldb;
+      if ((i & 1) == 0) glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
+      else glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
+    };
+    auto advance_cursor = [&]() {
+      if (ls + 1 < nsteps) {
+        ++ls;
+        if (++lk_ == nksteps) {
+          lk_ = 0;
+          ++lt;
+        }
+      }
+      lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
     };
     auto epilogue = [&](int t) {
 #pragma unroll
@@ -734,7 +739,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
 #pragma unroll
-    for (int i = 0; i < D; ++i) stage_next();
+    for (int i = 0; i < D; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stage_piece(j);
+      advance_cursor();
+    }
     if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -742,24 +751,45 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
     zero();
     rd(0, 0, fa0, fb0);
     int buf = 0, t = t0, ks = 0;
+    // The instruction order inside a step is pinned with sched_barrier(0): hipcc
+    // would otherwise move the MFMAs across the barrier and the fragment reads
+    // next to their first use, undoing the half-step lookahead.
     for (int s = 0; s < nsteps; ++s) {
-      mfma(fa0, fb0);
+      const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+      // first half: sub-step 0 (fragments read during the previous step), with
+      // the sub-step 1 reads of this step's image issued behind two MFMAs
+      mfma_rb(0, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
       rd(buf, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_rb(1, fa0, fb0);
+      mfma_rb(2, fa0, fb0);
+      mfma_rb(3, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
       // retire step s+1 (this wave's pieces); the younger D-2 steps stay in flight
       if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      stage_next();  // step s+D into the image of step s-1
-      mfma(fa1, fb1);
-      const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+      __builtin_amdgcn_sched_barrier(0);
+      // second half: next step's sub-step 0 reads first (their latency hides under
+      // this half's MFMAs), then sub-step 1's MFMAs with the LDS-DMA of step s+D
+      // (into the image of step s-1, which every wave has finished) between them
+      rd(nbuf, 0, fa0, fb0);  // past the end: a harmless read of a stale image
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        mfma_rb(i, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_piece(i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      advance_cursor();
       if (++ks == nksteps) {
         ks = 0;
         epilogue(t);
         zero();
         ++t;
       }
-      rd(nbuf, 0, fa0, fb0);  // past the end: a harmless read of a stale image
       buf = nbuf;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
