@@ -651,13 +651,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
     };
-    auto mfma = [&](const uint4 (&fa)[4], const uint4 (&fb)[2]) {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
-        acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
-      }
-    };
     auto mfma_rb = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
       acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
       acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
