@@ -13,17 +13,14 @@
 // whether the candidate set must contain the exact top-M.
 //
 // Tile: 256 database rows x 256 queries per workgroup of 8 waves (two per SIMD,
-// one workgroup per CU; 128 KB of LDS).  Wave w owns rows [128 (w&1), +128) and
-// queries [64 (w>>1), +64): 4 x 2 accumulators of 32x32 (128 registers); lane l
-// sees queries c = l&31 of its two 32-query blocks and keeps one sorted list of
-// KR entries per query (lanes l and l+32 hold disjoint rows of the same query).
-// K advances 64 elements (128 B per row) per step: both operand tiles (32 KB
-// each) are staged by global_load_lds_dwordx4 into the step's LDS image — eight
-// 1-KiB instructions per wave, whole 128-B lines per row — double-buffered, one
-// barrier per step.  16-B chunk c of LDS row r sits at c ^ ((r >> 1) & 7): every
-// 16-lane ds_read_b128 group of a fragment read hits 16 distinct bank slots
-// (the swizzle is applied to the per-lane GLOBAL source address, as LDS-DMA
-// writes LDS lane-linearly).
+// one workgroup per CU).  Wave w owns rows [128 (w&1), +128) and queries
+// [64 (w>>1), +64): 4 x 2 accumulators of 32x32 (128 registers); lane l sees
+// queries c = l&31 of its two 32-query blocks and keeps one sorted list of KR
+// entries per query (lanes l and l+32 hold disjoint rows of the same query).
+// K advances 32 elements (64 B per row) per step through a ring of NBUF LDS
+// images (both operand tiles of one step, 32 KB), filled by
+// global_load_lds_dwordx4 (LDS-DMA) NBUF-1 steps ahead; see gemm_topk_x1
+// below for the step schedule.
 //
 // Epilogue per 256-row tile (rare work after the first tiles): the keys of a
 // lane's 16 rows of one 32-row block are reduced to their minimum; only when it
@@ -35,10 +32,34 @@
 
 #include "vs_device.h"
 
-// waves 4-7 share their SIMDs with waves 0-3 and lose VALU arbitration on age:
-// one static priority for that half (MI355X_MICROARCH.md, "Two waves per SIMD" 4)
+// Static priority of one half of the waves (MI355X_MICROARCH.md, "Two waves
+// per SIMD" 4): 0 none, 1 waves 4-7, 2 waves 0-3.  With the stagger below none
+// measured fastest (profiles/r02h_ab_stagger.txt).
 #ifndef VS_X1_PRIO
-#define VS_X1_PRIO 1
+#define VS_X1_PRIO 0
+#endif
+#ifndef VS_X1_STAGGER
+#define VS_X1_STAGGER 1
+#endif
+// Diagnostic builds only (tools/x1_probe.sh; wrong results by design): drop the
+// LDS-DMA, the fragment reads, the mid-step barrier or the epilogue.
+#ifndef VS_X1_P_NODMA
+#define VS_X1_P_NODMA 0
+#endif
+#ifndef VS_X1_P_NOLDS
+#define VS_X1_P_NOLDS 0
+#endif
+#ifndef VS_X1_P_NOBAR
+#define VS_X1_P_NOBAR 0
+#endif
+#ifndef VS_X1_P_NOEPI
+#define VS_X1_P_NOEPI 0
+#endif
+#ifndef VS_X1_P_NOWAIT  // no vmcnt wait in the loop (the DMA still issued)
+#define VS_X1_P_NOWAIT 0
+#endif
+#ifndef VS_X1_P_FULLLINE  // DMA pieces of 8 rows x 128 B instead of 16 rows x 64 B
+#define VS_X1_P_FULLLINE 0
 #endif
 
 namespace vs {
@@ -46,7 +67,6 @@ namespace vs {
 namespace {
 
 constexpr int kT = 256;               // rows (and queries) per tile
-constexpr int kTileB = kT * 128;      // one operand tile of one K-step: 32 KB
 constexpr int kX1ChunkTiles = 16;     // database tiles per workgroup per launch
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
@@ -77,464 +97,10 @@ __device__ __forceinline__ float sel16(const f32x16& v, int i) {
 
 }  // namespace
 
-template <int KR, int MODE>
-__global__ __launch_bounds__(512, 1) void gemm_topk_x1(
-    const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
-    const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
-    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
-    int KP, float* __restrict__ pkey, int* __restrict__ pid) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * kTileB];  // [buf][X|Q][256][128 B]
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5;
-  const int c32 = lane & 31;
-  const int wr = w & 1;   // row half
-  const int wq = w >> 1;  // query quarter
-
-  // Bijective XCD remap: the workgroups of one database split run on one XCD,
-  // so each database tile is fetched into that XCD's L2 once for all query tiles.
-  const int nblk = gridDim.x;
-  const int b = blockIdx.x;
-  int lb;
-  {
-    const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
-    lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
-  }
-  const int qt = lb % nqt;
-  const int sp = lb / nqt;
-  const int s0 = (int)((int64_t)sp * ntiles / nsplit);
-  const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
-  const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
-  const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
-
-  int gq[2], selfrow[2];
-  float qa[2];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    gq[qb] = qt * kT + 64 * wq + 32 * qb + c32;
-    qa[qb] = 0.0f;
-    if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
-    selfrow[qb] = self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
-  }
-
-  // list (sp, wr, h) of each query
-  const int P = nsplit * 4;
-  const int pl = sp * 4 + wr * 2 + h;
-  float lk[2][KR];
-  int li[2][KR];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
-    if (chunk == 0) {
-      list_init<KR, int>(lk[qb], li[qb]);
-    } else {  // resume the list the previous launch wrote
-#pragma unroll
-      for (int e = 0; e < KR; ++e) {
-        lk[qb][e] = pkey[o + e];
-        li[qb][e] = pid[o + e];
-      }
-    }
-  }
-
-  if (t1 > t0) {  // uniform over the workgroup
-    const uint32_t ldb = (uint32_t)ld * 2u;  // row stride in bytes
-    // LDS-DMA geometry: lane L of an instruction moves 16 B of row L>>3 of an
-    // 8-row group into slot L&7 of that LDS row; the source chunk is the slot
-    // XOR the row's swizzle, which depends on the group only through its parity.
-    const int srow = lane >> 3;
-    uint32_t soff[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-      const int row = par * 8 + srow;
-      soff[par] = (uint32_t)srow * ldb + (uint32_t)((lane & 7) ^ ((row >> 1) & 7)) * 16u;
-    }
-    const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld);
-    const int fsw = (c32 >> 1) & 7;  // fragment rows 32i + c32 share (row >> 1) & 7
-
-    // wave w stages row groups 4w .. 4w+3 (rows 32w .. 32w+31) of both tiles
-    auto stage = [&](int buf, int t, int ks) {
-      char* dX = smem + buf * 2 * kTileB;
-      char* dQ = dX + kTileB;
-      const char* xs = (const char*)(XH + (int64_t)t * kT * ld) + ks * 128;
-      const char* qs = qtile + ks * 128;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t o = soff[i & 1] + (uint32_t)(32 * w + 8 * i) * ldb;
-        __builtin_amdgcn_global_load_lds(xs + o, VS_LDS(dX + (4 * w + i) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(qs + o, VS_LDS(dQ + (4 * w + i) * 1024), 16, 0, 0);
-      }
-    };
-
-    f32x16 acc[4][2];
-    auto zero = [&]() {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[rb][qb][r] = 0.0f;
-    };
-
-    // one K-step: 4 sub-steps of 16 elements; lane (c32, h) reads chunk 2s+h of
-    // its fragment rows (A: database rows 128wr + 32rb + c32; B: queries
-    // 64wq + 32qb + c32) — the same k order on both operands
-    auto mma = [&](int buf) {
-      const char* cX = smem + buf * 2 * kTileB + (128 * wr + c32) * 128;
-      const char* cQ = smem + buf * 2 * kTileB + kTileB + (64 * wq + c32) * 128;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int co = ((2 * s4 + h) ^ fsw) * 16;
-        const uint4 b0 = *(const uint4*)(cQ + co);
-        const uint4 b1 = *(const uint4*)(cQ + 32 * 128 + co);
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-          const uint4 a = *(const uint4*)(cX + rb * 32 * 128 + co);
-          acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b0), acc[rb][0], 0, 0, 0);
-          acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b1), acc[rb][1], 0, 0, 0);
-        }
-      }
-    };
-
-    // Keys of the lane's 16 rows of a block (row r0 + 8jj + 4h + e in register
-    // 4jj + e); their minimum against the list's last entry decides whether any
-    // can enter (lexicographic admission: a key equal to the last one may).
-    auto epilogue = [&](int t) {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const int r0 = t * kT + 128 * wr + 32 * rb;
-        f32x4 xa[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
-            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
-        }
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          f32x16 key;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = acc[rb][qb][jj * 4 + e];
-              float kk;
-              if constexpr (MODE == MODE_IP) {
-                kk = -v;
-              } else if constexpr (MODE == MODE_L2) {
-                kk = l2_from_ip(qa[qb], xa[jj][e], v);
-              } else {
-                kk = -(v * (qa[qb] * xa[jj][e]));
-              }
-              key[jj * 4 + e] = kk;
-            }
-          }
-          float m = key[0];
-#pragma unroll
-          for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
-          if (m <= lk[qb][KR - 1]) {  // rare after the first tiles
-            uint32_t cm = 0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              const bool c = row < ntotal && row != selfrow[qb] &&
-                             lex_less(key[r], row, lk[qb][KR - 1], li[qb][KR - 1]);
-              cm |= (uint32_t)c << r;
-            }
-            while (cm) {
-              const int bi = __builtin_ctz(cm);
-              cm &= cm - 1;
-              const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
-              list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
-            }
-          }
-        }
-      }
-    };
-
-    if (VS_X1_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
-
-    int t = t0, ks = 0, buf = 0;
-    stage(0, t, 0);
-    __syncthreads();
-    zero();
-    for (;;) {
-      int nt = t, nk = ks + 1;
-      if (nk == nksteps) {
-        nk = 0;
-        ++nt;
-      }
-      if (nt < t1) stage(buf ^ 1, nt, nk);
-      mma(buf);
-      if (nk == 0) {
-        epilogue(t);
-        zero();
-      }
-      if (nt >= t1) break;
-      __syncthreads();  // this wave's next-step loads landed; everyone is done with `buf`
-      buf ^= 1;
-      t = nt;
-      ks = nk;
-    }
-  }
-
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
-#pragma unroll
-    for (int e = 0; e < KR; ++e) {
-      pkey[o + e] = lk[qb][e];
-      pid[o + e] = li[qb][e];
-    }
-    for (int e = KR; e < KP; ++e) {  // the merge reads KP entries per list
-      pkey[o + e] = FLT_MAX;
-      pid[o + e] = -1;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// The deep-pipeline form (default): K-steps of 32 elements (64 B per row), NBUF
-// LDS images of 32 KB (both operand tiles of one step), NBUF-1 steps in flight.
-// Each wave issues the 4 LDS-DMA pieces of step s+NBUF-1 before computing step
-// s, then retires step s+1 with a COUNTED vmcnt (the younger NBUF-2 steps stay
-// in flight across the raw s_barrier; cdna_hip_programming.md "Pipelining
-// across barriers").  Loads past the last step re-read it (unconditional
-// loads keep the count fixed; nothing reads those images).  64-B LDS rows:
-// chunk c of row r at c ^ ((r >> 2) & 3) — conflict-free ds_read_b128 for the
-// 32x32x16 fragments, and one per-lane source offset for every 16-row group.
-//
-// XCD blocking (a 256-workgroup grid, one per CU): the 32 workgroups of an XCD
-// take QG query tiles x DG database splits (QG = min(nqt, 4)), so each XCD's L2
-// serves a query tile to DG workgroups and a database tile to QG of them.
-template <int KR, int MODE, int NBUF>
-__global__ __launch_bounds__(512, 1) void gemm_topk_x1d(
-    const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
-    const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
-    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
-    int KP, float* __restrict__ pkey, int* __restrict__ pid) {
-  constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5;
-  const int c32 = lane & 31;
-  const int wr = w & 1;
-  const int wq = w >> 1;
-
-  int qt, sp;
-  {
-    const int nblk = gridDim.x;
-    const int b = blockIdx.x;
-    const int QG = nqt < 4 ? nqt : 4;
-    const int G = nqt / QG;
-    if (nblk == 256 && nqt * nsplit == 256 && nqt % QG == 0 && G <= 8 && 8 % G == 0) {
-      const int xcd = b & 7, slot = b >> 3, DG = 32 / QG;
-      qt = (xcd % G) * QG + slot % QG;
-      sp = (xcd / G) * DG + slot / QG;
-    } else {  // bijective remap: the workgroups of a split on one XCD
-      const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
-      const int lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
-      qt = lb % nqt;
-      sp = lb / nqt;
-    }
-  }
-  const int s0 = (int)((int64_t)sp * ntiles / nsplit);
-  const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
-  const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
-  const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
-
-  int gq[2], selfrow[2];
-  float qa[2];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    gq[qb] = qt * kT + 64 * wq + 32 * qb + c32;
-    qa[qb] = 0.0f;
-    if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
-    selfrow[qb] = self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
-  }
-  const int P = nsplit * 4;
-  const int pl = sp * 4 + wr * 2 + h;
-  float lk[2][KR];
-  int li[2][KR];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
-    if (chunk == 0) {
-      list_init<KR, int>(lk[qb], li[qb]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < KR; ++e) {
-        lk[qb][e] = pkey[o + e];
-        li[qb][e] = pid[o + e];
-      }
-    }
-  }
-
-  // Settle the loads above (resumed lists, query aux) before the pipeline: an
-  // asm use makes hipcc wait for them here, once, instead of inside the loop,
-  // where its vmcnt would drain the LDS-DMA steps in flight.
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-#pragma unroll
-    for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
-    asm volatile("" ::"v"(qa[qb]));
-  }
-
-  if (t1 > t0) {  // uniform over the workgroup
-    const uint32_t ldb = (uint32_t)ld * 2u;
-    // lane L of an instruction moves 16 B of row L>>2 of a 16-row group into slot
-    // L&3 of that 64-B LDS row; source chunk = slot ^ ((row >> 2) & 3) =
-    // (L & 3) ^ (L >> 4) for every group
-    const uint32_t soff = (uint32_t)(lane >> 2) * ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
-    const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld);
-    const int fsw = (c32 >> 2) & 3;
-    const int nsteps = (t1 - t0) * nksteps;
-
-    // wave w stages row groups 2w, 2w+1 (rows 32w .. 32w+31) of both tiles
-    auto stage = [&](int s) {
-      s = s < nsteps ? s : nsteps - 1;  // past the end: re-read the last step
-      const int t = t0 + s / nksteps, ks = s % nksteps;
-      char* dX = smem + (s % NBUF) * 2 * kStepB;
-      char* dQ = dX + kStepB;
-      const char* xs = (const char*)(XH + (int64_t)t * kT * ld) + ks * 64;
-      const char* qs = qtile + ks * 64;
-      const uint32_t lx = (uint32_t)(uintptr_t)VS_LDS(dX) + (uint32_t)(2 * w) * 1024u;
-      const uint32_t lq = (uint32_t)(uintptr_t)VS_LDS(dQ) + (uint32_t)(2 * w) * 1024u;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t o = soff + (uint32_t)(32 * w + 16 * i) * ldb;
-        glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + i * 1024u));
-        glds16(qs + o, __builtin_amdgcn_readfirstlane(lq + i * 1024u));
-      }
-    };
-
-    f32x16 acc[4][2];
-    auto zero = [&]() {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[rb][qb][r] = 0.0f;
-    };
-    auto mma = [&](int s) {
-      const char* base = smem + (s % NBUF) * 2 * kStepB;
-      const char* cX = base + (128 * wr + c32) * 64;
-      const char* cQ = base + kStepB + (64 * wq + c32) * 64;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int co = ((2 * s2 + h) ^ fsw) * 16;
-        const uint4 b0 = *(const uint4*)(cQ + co);
-        const uint4 b1 = *(const uint4*)(cQ + 32 * 64 + co);
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-          const uint4 a = *(const uint4*)(cX + rb * 32 * 64 + co);
-          acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b0), acc[rb][0], 0, 0, 0);
-          acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b1), acc[rb][1], 0, 0, 0);
-        }
-      }
-    };
-    auto epilogue = [&](int t) {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const int r0 = t * kT + 128 * wr + 32 * rb;
-        f32x4 xa[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
-            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
-        }
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          f32x16 key;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = acc[rb][qb][jj * 4 + e];
-              float kk;
-              if constexpr (MODE == MODE_IP) {
-                kk = -v;
-              } else if constexpr (MODE == MODE_L2) {
-                kk = l2_from_ip(qa[qb], xa[jj][e], v);
-              } else {
-                kk = -(v * (qa[qb] * xa[jj][e]));
-              }
-              key[jj * 4 + e] = kk;
-            }
-          }
-          float m = key[0];
-#pragma unroll
-          for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
-          if (m <= lk[qb][KR - 1]) {
-            uint32_t cm = 0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              const bool c = row < ntotal && row != selfrow[qb] &&
-                             lex_less(key[r], row, lk[qb][KR - 1], li[qb][KR - 1]);
-              cm |= (uint32_t)c << r;
-            }
-            while (cm) {
-              const int bi = __builtin_ctz(cm);
-              cm &= cm - 1;
-              const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
-              list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
-            }
-          }
-        }
-      }
-    };
-
-    if (VS_X1_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
-
-    // prologue: steps 0 .. NBUF-2 in flight, retire step 0
-#pragma unroll
-    for (int s = 0; s < NBUF - 1; ++s) stage(s);
-    if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    zero();
-    for (int s = 0; s < nsteps; ++s) {
-      stage(s + NBUF - 1);  // into the image step s-1 used (every wave is past it)
-      mma(s);
-      if ((s + 1) % nksteps == 0) {
-        epilogue(t0 + s / nksteps);
-        zero();
-      }
-      // retire step s+1 (this wave's pieces), keep the younger steps in flight
-      if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
-  }
-
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
-#pragma unroll
-    for (int e = 0; e < KR; ++e) {
-      pkey[o + e] = lk[qb][e];
-      pid[o + e] = li[qb][e];
-    }
-    for (int e = KR; e < KP; ++e) {
-      pkey[o + e] = FLT_MAX;
-      pid[o + e] = -1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// The split-step form (default): as gemm_topk_x1d, but each 32-element step is
-// cut at its middle by the barrier, and the fragment reads run one half-step
-// ahead of the MFMAs:
+// The step schedule.  Each 32-element step is two sub-steps of 16 (8 MFMAs per
+// wave each), cut at its middle by the one barrier of the step, and the
+// fragment reads run one half-step ahead of the MFMAs:
 //     MFMAs of sub-step 0 (fragments read during the previous step)
 //     ds_read the sub-step 1 fragments
 //     wait for this wave's pieces of step s+1, s_barrier
@@ -543,10 +109,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1d(
 //     MFMAs of sub-step 1, then ds_read sub-step 0 of step s+1 (its image is
 //       complete: every wave's pieces were retired before this barrier)
 // so the LDS read latency after a barrier hides under MFMAs instead of
-// stalling both waves of a SIMD at every step.  Load and position cursors are
-// incremental (no divisions in the loop).
+// stalling both waves of a SIMD at every step.  The LDS-DMA steps are retired
+// with a COUNTED vmcnt (the younger NBUF-2 steps stay in flight across the raw
+// s_barrier; cdna_hip_programming.md "Pipelining across barriers"); loads past
+// the last step re-read it (unconditional loads keep the count fixed).  64-B
+// LDS rows: chunk c of row r at c ^ ((r >> 2) & 3) — conflict-free ds_read_b128
+// for the 32x32x16 fragments, and one per-lane source offset for every 16-row
+// group.  The first sub-step of every tile multiplies into a zero accumulator
+// (the MFMA's inline-constant C), so no register clearing between tiles.  Load
+// and position cursors are incremental (no divisions in the loop).
+//
+// XCD blocking (a 256-workgroup grid, one per CU): the 32 workgroups of an XCD
+// take QG query tiles x DG database splits (QG = min(nqt, 4)), so each XCD's L2
+// serves a query tile to DG workgroups and a database tile to QG of them.
 template <int KR, int MODE, int NBUF>
-__global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
+__global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
     const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
     int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
@@ -620,7 +197,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
 
   if (t1 > t0) {  // uniform over the workgroup
     const uint32_t ldb = (uint32_t)ld * 2u;
+#if !VS_X1_P_FULLLINE
     const uint32_t soff = (uint32_t)(lane >> 2) * ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
+#else
+    const uint32_t soff = (uint32_t)(lane >> 3) * ldb + (uint32_t)(lane & 7) * 16u;
+#endif
     const int fsw = (c32 >> 2) & 3;
     const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld) + (uint32_t)(32 * w) * ldb;
     const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
@@ -631,14 +212,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
     int ls = 0, lt = t0, lk_ = 0, lbuf = 0;
 
     f32x16 acc[4][2];
-    auto zero = [&]() {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[rb][qb][r] = 0.0f;
-    };
     // fragments of one sub-step: A (database rows) x4, B (queries) x2
     uint4 fa0[4], fb0[2], fa1[4], fb1[2];
     auto rd = [&](int buf, int s2, uint4 (&fa)[4], uint4 (&fb)[2]) {
@@ -646,14 +219,29 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
       const int co = ((2 * s2 + h) ^ fsw) * 16;
       const char* cX = base + (128 * wr + c32) * 64 + co;
       const char* cQ = base + kStepB + (64 * wq + c32) * 64 + co;
+#if !VS_X1_P_NOLDS
       fb[0] = *(const uint4*)cQ;
       fb[1] = *(const uint4*)(cQ + 32 * 64);
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
+#else
+      auto opq = [](uint4& u) { asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w)); };
+      asm volatile("" ::"v"(cX), "v"(cQ));
+      opq(fb[0]);
+      opq(fb[1]);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) opq(fa[rb]);
+#endif
     };
     auto mfma_rb = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
       acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
       acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
+    };
+    // the first sub-step of a tile: C = 0 (inline constant), no clearing pass
+    auto mfma_rb_first = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
+      const f32x16 z = {};
+      acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), z, 0, 0, 0);
+      acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), z, 0, 0, 0);
     };
     // the four LDS-DMA pieces of the load cursor's step, one at a time
     auto stage_piece = [&](int i) {
@@ -662,8 +250,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
       const char* qs = qtile + lk_ * 64;
       const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
       const uint32_t o = soff + (uint32_t)(16 * (i >> 1)) * ldb;
+#if !VS_X1_P_NODMA
       if ((i & 1) == 0) glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
       else glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
+#else
+      asm volatile("" ::"v"(xs + o), "v"(qs + o), "s"(lx));
+#endif
     };
     auto advance_cursor = [&]() {
       if (ls + 1 < nsteps) {
@@ -676,6 +268,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
       lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
     };
     auto epilogue = [&](int t) {
+      // uniform: every row of the tile exists and none is excluded
+      const bool plain = self0 < 0 && (t + 1) * kT <= ntotal;
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const int r0 = t * kT + 128 * wr + 32 * rb;
@@ -705,17 +299,26 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
               key[jj * 4 + e] = kk;
             }
           }
+          // A list only ever sees rows in increasing order (tiles ascend within a
+          // split, blocks ascend within a tile, resumed lists hold earlier
+          // tiles), so against the entries present before this block the
+          // lexicographic admission (key, row) < (last key, last row) is just
+          // key < last key; list_insert keeps the full rule within the block.
           float m = key[0];
 #pragma unroll
           for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
-          if (m <= lk[qb][KR - 1]) {
+          const float last = lk[qb][KR - 1];
+          if (m < last) {  // rare after the first tiles
             uint32_t cm = 0;
+            if (plain) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              const bool c = row < ntotal && row != selfrow[qb] &&
-                             lex_less(key[r], row, lk[qb][KR - 1], li[qb][KR - 1]);
-              cm |= (uint32_t)c << r;
+              for (int r = 0; r < 16; ++r) cm |= (uint32_t)(key[r] < last) << r;
+            } else {
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                cm |= (uint32_t)(row < ntotal && row != selfrow[qb] && key[r] < last) << r;
+              }
             }
             while (cm) {
               const int bi = __builtin_ctz(cm);
@@ -728,7 +331,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
       }
     };
 
-    if (VS_X1_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
+    if ((VS_X1_PRIO == 1 && w >= 4) || (VS_X1_PRIO == 2 && w < 4)) __builtin_amdgcn_s_setprio(1);
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
 #pragma unroll
@@ -741,28 +344,57 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
     else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    zero();
     rd(0, 0, fa0, fb0);
     int buf = 0, t = t0, ks = 0;
     // The instruction order inside a step is pinned with sched_barrier(0): hipcc
     // would otherwise move the MFMAs across the barrier and the fragment reads
     // next to their first use, undoing the half-step lookahead.
+    // Stagger (VS_X1_STAGGER): waves 4-7 take the step's barrier at its start
+    // instead of its middle, so they run half a step behind their SIMD
+    // partners (the LDS-DMA issue of one wave beside the other's MFMAs).
+    // Every condition above still holds for them: they retire DMA(s+1) before
+    // barrier s and read image s+1 only after it, and their last reads of
+    // image s-1 are consumed before barrier s, after which DMA(s+D) may
+    // overwrite it.
+    const bool lag = VS_X1_STAGGER && w >= 4;
     for (int s = 0; s < nsteps; ++s) {
       const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+      if (lag) {  // uniform
+        if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      __builtin_amdgcn_sched_barrier(0);
       // first half: sub-step 0 (fragments read during the previous step), with
       // the sub-step 1 reads of this step's image issued behind two MFMAs
-      mfma_rb(0, fa0, fb0);
-      __builtin_amdgcn_sched_barrier(0);
-      rd(buf, 1, fa1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_rb(1, fa0, fb0);
-      mfma_rb(2, fa0, fb0);
-      mfma_rb(3, fa0, fb0);
+      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
+        mfma_rb_first(0, fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(buf, 1, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_rb_first(1, fa0, fb0);
+        mfma_rb_first(2, fa0, fb0);
+        mfma_rb_first(3, fa0, fb0);
+      } else {
+        mfma_rb(0, fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(buf, 1, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_rb(1, fa0, fb0);
+        mfma_rb(2, fa0, fb0);
+        mfma_rb(3, fa0, fb0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       // retire step s+1 (this wave's pieces); the younger D-2 steps stay in flight
-      if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if (!lag) {  // uniform
+#if !VS_X1_P_NOWAIT
+        if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#endif
+#if !VS_X1_P_NOBAR
+        __builtin_amdgcn_s_barrier();
+#endif
+      }
       __builtin_amdgcn_sched_barrier(0);
       // second half: next step's sub-step 0 reads first (their latency hides under
       // this half's MFMAs), then sub-step 1's MFMAs with the LDS-DMA of step s+D
@@ -779,8 +411,14 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
       advance_cursor();
       if (++ks == nksteps) {
         ks = 0;
+#if !VS_X1_P_NOEPI
         epilogue(t);
-        zero();
+#else
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+#endif
         ++t;
       }
       buf = nbuf;
@@ -788,9 +426,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
   }
 
+  // the list offsets are recomputed from the lane id here (not kept live
+  // across the main loop: registers)
+  const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int pl0 = sp * 4 + wr * 2 + (ln >> 5);
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+    const int64_t o = ((int64_t)(qt * kT + 64 * wq + 32 * qb + (ln & 31)) * P + pl0) * KP;
 #pragma unroll
     for (int e = 0; e < KR; ++e) {
       pkey[o + e] = lk[qb][e];
@@ -803,14 +445,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1e(
   }
 }
 
-// Pipeline form: VS_X1_PIPE=2 (64-element steps, 2 images), 4 or 5 (32-element
-// steps, that many images, one barrier per step), 14 / 15 (the split-step form
-// with 4 / 5 images); default 14.
-static int x1_pipe() {
+// LDS ring depth: VS_X1_NBUF=5 selects five images (A/B); default four.
+static int x1_nbuf() {
   static const int v = [] {
-    const char* e = getenv("VS_X1_PIPE");
-    const int p = e ? atoi(e) : 0;
-    return p == 2 || p == 4 || p == 5 || p == 14 || p == 15 ? p : 14;
+    const char* e = getenv("VS_X1_NBUF");
+    return e && atoi(e) == 5 ? 5 : 4;
   }();
   return v;
 }
@@ -826,26 +465,14 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
-  const int pipe = x1_pipe();
+  const bool five = x1_nbuf() == 5;
   for (int c = 0; c < nchunk; ++c) {
-    if (pipe == 2)
-      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE>), dim3(nqt * a.nsplit), dim3(512), 0, st, a.XH,
-                         a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 64), a.ntotal, ntiles,
-                         a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
-    else if (pipe == 14)
-      hipLaunchKernelGGL((gemm_topk_x1e<KR, MODE, 4>), dim3(nqt * a.nsplit), dim3(512), 0, st,
-                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
-                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
-    else if (pipe == 15)
-      hipLaunchKernelGGL((gemm_topk_x1e<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
-                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
-                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
-    else if (pipe == 5)
-      hipLaunchKernelGGL((gemm_topk_x1d<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+    if (five)
+      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                          a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
                          ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     else
-      hipLaunchKernelGGL((gemm_topk_x1d<KR, MODE, 4>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 4>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                          a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
                          ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
     hipError_t e = hipGetLastError();
@@ -859,8 +486,8 @@ int x1_lane_len() { return 8; }
 
 hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStream_t st,
                                int* ndispatch) {
-  // 64-element K-steps of 128-B rows; 256-query tiles; the lists of a query
-  // are (split, row half, lane half)
+  // 32-element K-steps of plane rows padded to 128 B; 256-query tiles; the
+  // lists of a query are (split, row half, lane half)
   if (a.nq_pad % kT != 0 || a.ld % 64 != 0 || a.ld <= 0 || part.KP < x1_lane_len() ||
       part.P != 4 * a.nsplit || a.nsplit < 1 || a.ntotal <= 0)
     return hipErrorInvalidValue;
