@@ -141,7 +141,10 @@ struct KernelTimer {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;
   int dispatches = 1;  // kernel launches between the two events
+  // name == nullptr: untimed (the filter engine's exact redo, which is not the
+  // kernel the roofline is quoted on)
   KernelTimer(hipStream_t s, const char* name) : st(s) {
+    if (!name) return;
     std::lock_guard<std::mutex> g(g_timer_mu);
     g_timer_kernel = name;
     if (!g_timer_on) return;
@@ -317,7 +320,7 @@ int run_gemm(vs_index* idx, const SearchArgs& a, int need, hipStream_t st,
   VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
   const void* qmat = a.qb16 ? a.qb16 : (const void*)a.qbuf;
   {
-    KernelTimer tm(st, "gemm_topk");
+    KernelTimer tm(st, qlist ? nullptr : "gemm_topk");
     VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, qmat, a.qaux, idx->ld, idx->esize,
                             ntotal, a.nq_pad, nsplit, a.self0, part, st, qlist, qcount),
            "vs: gemm_topk launch");
@@ -432,20 +435,12 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(launch_merge_partials(mode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
                                a.raw),
          "vs: merge");
-  {
-    std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_kernel = "gemm_topk_x1";
-  }
-  // the exact redo of what is still flagged (usually nothing: every tile exits)
+  // the exact redo of what is still flagged (usually nothing: every tile exits;
+  // untimed, so the kernel timer holds the filter pass alone)
   SearchArgs ex = a;
   ex.qbuf = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
   ex.nq_pad = (int)round_up(nq, kBQ);
-  int rc = run_gemm(idx, ex, need, st, qlist, qcount + 1);
-  {
-    std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_kernel = "gemm_topk_x1";  // the redo is part of this engine's search
-  }
-  return rc;
+  return run_gemm(idx, ex, need, st, qlist, qcount + 1);
 }
 
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,

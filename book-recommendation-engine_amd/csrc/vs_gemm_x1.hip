@@ -55,6 +55,12 @@
 #ifndef VS_X1_P_NOEPI
 #define VS_X1_P_NOEPI 0
 #endif
+#ifndef VS_X1_P_NODMA_X  // drop only the database (X) pieces
+#define VS_X1_P_NODMA_X 0
+#endif
+#ifndef VS_X1_P_NODMA_Q  // drop only the query (Q) pieces
+#define VS_X1_P_NODMA_Q 0
+#endif
 #ifndef VS_X1_P_NOWAIT  // no vmcnt wait in the loop (the DMA still issued)
 #define VS_X1_P_NOWAIT 0
 #endif
@@ -251,8 +257,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
       const uint32_t o = soff + (uint32_t)(16 * (i >> 1)) * ldb;
 #if !VS_X1_P_NODMA
-      if ((i & 1) == 0) glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
-      else glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
+      if ((i & 1) == 0) {
+        if (!(VS_X1_P_NODMA_X)) glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
+      } else {
+        if (!(VS_X1_P_NODMA_Q))
+          glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
+      }
 #else
       asm volatile("" ::"v"(xs + o), "v"(qs + o), "s"(lx));
 #endif
