@@ -53,14 +53,49 @@ sys.path.insert(0, ROOT)
 METRIC_NAME = "exact top-10 queries/sec at 10M×1536 fp32 (1/8 GPU) + % HBM/MFMA roofline"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA (dense)
+# MI355X_MICROARCH.md, MFMA table: I8 32x32x32 takes the cycles of BF16 32x32x16
+# (2x K), so the dense int8 MFMA rate is twice the bf16 one
+I8_MFMA_PEAK_TOPS = 2.0 * BF16_MFMA_PEAK_TFLOPS
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak (spec)
 HBM_KERNELS = ("gemv_topk", "skinny_topk")
 
 
 def mfma_kind(kname: str, esz: int) -> str:
+    if kname == "gemm_topk_x1_i8":  # one int8 MFMA product per fp32 product
+        return "mfma_x1_i8"
     if kname == "gemm_topk_x1":  # one bf16 MFMA product per fp32 product
         return "mfma_x1"
     return "mfma32" if esz == 4 else "mfma16"
+
+
+def is_x1(kname: str) -> bool:
+    return kname.startswith("gemm_topk_x1")
+
+
+def x1_dominant(ctx, work_total, kms, nl):
+    """The filter engine's first stage runs on the int8 or the bf16 plane per
+    search (the library's adaptive order).  Returns the plane that took most of
+    the timed kernel time: (timer name, its share of the algorithmic work, its
+    kernel ms, its dispatches, per-plane record).  Both planes' launches are the
+    same grid over the same batch, so the work per dispatch is the same."""
+    mi, ni = ctx.lib.timer_read_kernel("gemm_topk_x1_i8")
+    mb, nb = ctx.lib.timer_read_kernel("gemm_topk_x1")
+    per = work_total / max(1, ni + nb)
+    split = {"i8": {"dispatches": ni, "kernel_ms": round(mi, 3)},
+             "bf16": {"dispatches": nb, "kernel_ms": round(mb, 3)}}
+    if mi >= mb:
+        return "gemm_topk_x1_i8", per * ni, mi, ni, split
+    return "gemm_topk_x1", per * nb, mb, nb, split
+
+
+def rocprof_prefix(kname: str):
+    """rocprof's name of a timed kernel: gemm_topk_x1<KR, MODE, NBUF, EL> with EL
+    1 = int8, 0 = bf16 (the plane is the last template argument)."""
+    if kname == "gemm_topk_x1_i8":
+        return "void vs::gemm_topk_x1<", ", 1>("
+    if kname == "gemm_topk_x1":
+        return "void vs::gemm_topk_x1<", ", 0>("
+    return "void vs::" + kname + "<", ""
 
 DEFAULTS = {
     "c3": dict(ntotal=10_000_000, batch=4096, k=10, metric="ip", dtype="f32"),
@@ -104,8 +139,9 @@ def parse(argv=None):
     return a
 
 
-def pmc_traffic(workload: str, kernel_prefix: str):
-    """HBM bytes per launch of `kernel_prefix` from the newest PMC summary in profiles/."""
+def pmc_traffic(workload: str, kernel_prefix: str, must_contain: str = ""):
+    """HBM bytes per launch of `kernel_prefix` from the newest PMC summary in profiles/
+    (names containing `must_contain`: the x1 kernel's plane)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{workload}.json")))
     if not files:
         return None, None
@@ -113,7 +149,7 @@ def pmc_traffic(workload: str, kernel_prefix: str):
         with open(path, encoding="utf-8") as f:
             summ = json.load(f)
         for name, rec in summ.get("kernels", {}).items():
-            if name.startswith(kernel_prefix):
+            if name.startswith(kernel_prefix) and must_contain in name:
                 return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
@@ -331,6 +367,8 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
         peak, unit, bound, scale = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma", 1e12
     elif kind == "mfma_x1":
         peak, unit, bound, scale = BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma", 1e12
+    elif kind == "mfma_x1_i8":
+        peak, unit, bound, scale = I8_MFMA_PEAK_TOPS, "TFLOP/s", "mfma", 1e12
     else:
         peak, unit, bound, scale = HBM_PEAK_GBS, "GB/s", "hbm", 1e9
     secs = kms / 1e3
@@ -350,6 +388,13 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
                           "per fp32 product (bf16 copies of rows and queries), against the dense "
                           "bf16 peak; candidates are then rescored exactly in fp64 and a "
                           "rigorous error bound proves the exact top-k is among them")
+    if kind == "mfma_x1_i8":
+        r["peak_note"] = ("filter pass of the filter-and-verify engine: one int8 MFMA product "
+                          "per fp32 product (int8 codes of rows and queries, one fp32 scale per "
+                          "row; 2*N*d int8 multiply-adds per query, counted as FLOP) against the "
+                          "dense int8 MFMA peak (2x bf16, MI355X_MICROARCH.md); candidates are "
+                          "then rescored exactly in fp64 and a rigorous error bound proves the "
+                          "exact top-k is among them")
     if traffic_src:
         r["traffic_source"] = traffic_src
     return r
@@ -406,6 +451,7 @@ def run_knn(args, ctx):
     elapsed, kms, nl, (D, I) = ctx.timed(
         lambda i: index.search_device(xq, k, stream=ctx.stream), args.steps, args.warmup)
     fw = ctx.lib.filter_wide_stats()
+    f2 = ctx.lib.filter_second_stats()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
@@ -415,7 +461,7 @@ def run_knn(args, ctx):
     esz = 4 if args.dtype == "f32" else 2
     kname = ctx.lib.timer_kernel()
     exact_check = None
-    if kname == "gemm_topk_x1":
+    if is_x1(kname):
         # the same queries through the exact fp32 MFMA engine: ids must agree up to
         # exact fp32 near-ties (the verify step makes the filter engine exact; this
         # re-checks it live; the two round their fp32 scores differently)
@@ -435,16 +481,23 @@ def run_knn(args, ctx):
         sane &= beyond == 0
     gemv = kname in HBM_KERNELS  # the small-batch kernels are HBM-bound
     # PMC summaries are single-GPU profiles: per-dispatch bytes of a 1/N shard differ
-    traffic, tsrc = (pmc_traffic(args.workload, "void vs::" + kname + "<") if ctx.world == 1
-                     else (None, None))
+    work = flops * args.steps
+    split = None
+    if is_x1(kname):
+        kname, work, kms, nl, split = x1_dominant(ctx, work, kms, nl)
+    plane = {"gemm_topk_x1_i8": "i8", "gemm_topk_x1": "bf16"}.get(kname)
+    traffic, tsrc = (pmc_traffic(args.workload, *rocprof_prefix(kname))
+                     if ctx.world == 1 else (None, None))
     if gemv:
         rf = roofline("hbm", n_shard * d * esz * args.steps, kms, nl,
                       f"{n_shard}*{d}*{esz} B per search (batch {B} over the rank's shard)",
                       kname, traffic, tsrc)
     else:
-        rf = roofline(mfma_kind(kname, esz), flops * args.steps, kms, nl,
+        rf = roofline(mfma_kind(kname, esz), work, kms, nl,
                       f"2*{n_shard}*{d}*{B} FLOP per search (whole batch over the rank's shard)",
                       kname, traffic, tsrc)
+        if split:
+            rf["first_stage_planes"] = split
 
     batch1 = None
     if args.batch1_steps > 0 and not gemv:
@@ -476,7 +529,9 @@ def run_knn(args, ctx):
             "kernel": kname}
         res["roofline"] = rf
         if fq:
-            res["filter_verify"] = {"queries": fq, "wide_checked": fw, "fallback_queries": ff,
+            res["filter_verify"] = {"plane": plane, "queries": fq, "wide_checked": fw,
+                                    "to_bf16_stage": f2,
+                                    "fallback_queries": ff,
                                     "fallback_rate": round(ff / fq, 6), "exact_check": exact_check}
         res["batch1"] = batch1
         res["cpu_baseline"] = cpu
@@ -518,6 +573,7 @@ def run_selfjoin(args, ctx):
     ctx.lib.filter_stats(reset=True)
     elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
     fw = ctx.lib.filter_wide_stats()
+    f2 = ctx.lib.filter_second_stats()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Ih = I.cpu()
     sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
@@ -525,7 +581,7 @@ def run_selfjoin(args, ctx):
     flops_step = 2.0 * N * d * nq
     kname = ctx.lib.timer_kernel()
     exact_check = None
-    if kname == "gemm_topk_x1":
+    if is_x1(kname):
         # the first 256 students again through the fp32 MFMA engine: ids must agree
         nchk = min(nq, 256)
         De = torch.empty((nchk, k), dtype=torch.float32, device="cuda")
@@ -544,11 +600,18 @@ def run_selfjoin(args, ctx):
                        "rows_beyond_tie_tolerance": beyond,
                        "max_abs_sim_diff": float(dsim.max())}
         sane &= beyond == 0
-    traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
+    work = flops_step * args.steps
+    split = None
+    if is_x1(kname):
+        kname, work, kms, nl, split = x1_dominant(ctx, work, kms, nl)
+    plane = {"gemm_topk_x1_i8": "i8", "gemm_topk_x1": "bf16"}.get(kname)
+    traffic, tsrc = pmc_traffic(args.workload, *rocprof_prefix(kname))
     esz = 4 if args.dtype == "f32" else 2
-    rf = roofline(mfma_kind(kname, esz), flops_step * args.steps, kms, nl,
+    rf = roofline(mfma_kind(kname, esz), work, kms, nl,
                   f"2*{N}*{d}*{nq} FLOP per step ({nq} query rows per rank)",
                   kname, traffic, tsrc)
+    if split:
+        rf["first_stage_planes"] = split
     if ctx.rank == 0:
         # the writer's rows: (a, b, sim) with sim >= threshold (main.py:350-354),
         # counted from the gathered arrays of the last step (not timed)
@@ -570,7 +633,9 @@ def run_selfjoin(args, ctx):
         res["writer"] = writer
         res["roofline"] = rf
         if fq:
-            res["filter_verify"] = {"students": fq, "wide_checked": fw, "fallback_students": ff,
+            res["filter_verify"] = {"plane": plane, "students": fq, "wide_checked": fw,
+                                    "to_bf16_stage": f2,
+                                    "fallback_students": ff,
                                     "fallback_rate": round(ff / fq, 6),
                                     "exact_check": exact_check}
         res["result_sane"] = sane

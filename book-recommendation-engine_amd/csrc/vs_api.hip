@@ -37,13 +37,35 @@ struct vs_index {
   int64_t rowbytes() const { return ld * esize; }
   char* row(int64_t r) const { return codes + r * rowbytes(); }
   float* norms = nullptr;  // [capacity] squared L2 norms
-  // fp32 indexes: the bf16 (round-to-nearest-even) copy of every row that the
-  // filter pass multiplies ([capacity][ld] uint16, kept in step with the rows by
-  // add / remove_ids / growth) and |x - hi(x)|^2 per row, for the bound.
-  // bf16 indexes: the rows themselves are the plane.
-  uint16_t* hplane = nullptr;
-  float* rn2 = nullptr;
-  const uint16_t* plane() const { return esize == 2 ? (const uint16_t*)codes : hplane; }
+  // fp32 indexes: the filter planes the filter passes multiply ([capacity][ld]
+  // each, kept in step with the rows by add / remove_ids / growth) and
+  // |x - plane(x)|^2 per row for the bound: [FILTER_I8] int8 codes + a per-row
+  // scale (inner-product indexes), [FILTER_BF16] bf16 (round-to-nearest-even)
+  // copies.  bf16 indexes use the exact bf16 engine, no plane.
+  bool plane_on[2] = {false, false};
+  char* fplane[2] = {nullptr, nullptr};
+  float* rn2[2] = {nullptr, nullptr};
+  float* fscale = nullptr;  // int8 plane: s = max|x| / 127 per row
+  // per plane: max |x|^2, max |x - plane(x)|^2, max of their ratio over the
+  // rows (the bound's index maxima; grown by add, recomputed by remove_ids)
+  unsigned* bstats[2] = {nullptr, nullptr};
+  int64_t planebytes(int p) const { return ld * filter_bytes(p); }
+  // Adaptive plane order: the int8 stage pays off while it settles most
+  // queries; on data where it hands most of them to bf16 (clustered
+  // embeddings) the searches go to bf16 directly, re-probing int8 with an
+  // exponential backoff.  Device counters [i8 queries, handed to bf16], read
+  // through a pinned mirror when the copy's event has completed (no host wait).
+  struct Adaptive {
+    std::mutex mu;
+    unsigned long long* dcount = nullptr;
+    unsigned long long* hmirror = nullptr;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    unsigned long long seen_q = 0, seen_h = 0;
+    double ema = 0.0;
+    bool have = false;
+    int skip_left = 0, backoff = 1;
+  } ad;
   int engine = VS_ENGINE_AUTO;
   std::shared_mutex mu;
 };
@@ -106,6 +128,7 @@ bool g_timer_on = false;
 struct TimedSpan {
   hipEvent_t a, b;
   int dispatches;
+  const char* name;
 };
 std::vector<TimedSpan> g_timer_events;
 const char* g_timer_kernel = "";
@@ -140,10 +163,11 @@ bool wide_enabled() {
 struct KernelTimer {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;
+  const char* name = nullptr;
   int dispatches = 1;  // kernel launches between the two events
   // name == nullptr: untimed (the filter engine's exact redo, which is not the
   // kernel the roofline is quoted on)
-  KernelTimer(hipStream_t s, const char* name) : st(s) {
+  KernelTimer(hipStream_t s, const char* nm) : st(s), name(nm) {
     if (!name) return;
     std::lock_guard<std::mutex> g(g_timer_mu);
     g_timer_kernel = name;
@@ -158,7 +182,7 @@ struct KernelTimer {
     if (!a) return;
     (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_events.push_back({a, b, dispatches});
+    g_timer_events.push_back({a, b, dispatches, name});
     a = b = nullptr;
   }
 };
@@ -172,49 +196,87 @@ int engine_from_env() {
   if (!e) return VS_ENGINE_AUTO;
   if (strcmp(e, "fp32") == 0) return VS_ENGINE_FP32_MFMA;
   if (strcmp(e, "bf16v") == 0) return VS_ENGINE_BF16_VERIFY;
+  if (strcmp(e, "i8v") == 0) return VS_ENGINE_I8_VERIFY;
   return VS_ENGINE_AUTO;
+}
+
+// Filter planes of a new fp32 index: inner product holds int8 + bf16 (the
+// staged engine), L2 bf16 only (the int8 filter has no L2 form).  Env
+// VS_FILTER=bf16 | i8 keeps only that plane (A/B; i8 only for inner product).
+void planes_for(vs_index* idx) {
+  const char* e = getenv("VS_FILTER");
+  const bool ip = idx->metric == VS_METRIC_INNER_PRODUCT && idx->esize == 4;
+  idx->plane_on[FILTER_BF16] = idx->esize == 4 && !(ip && e && strcmp(e, "i8") == 0);
+  idx->plane_on[FILTER_I8] = ip && !(e && strcmp(e, "bf16") == 0);
 }
 
 // The filter plane and residual norms of fp32 rows [r0, r0+n) (after the rows
 // and their norms are in place).
 int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
   if (idx->esize != 4 || n <= 0) return VS_OK;
-  VS_HIP(launch_f32_to_bf16((const float*)idx->row(r0), idx->ld, idx->hplane + r0 * idx->ld,
-                            idx->ld, n, idx->ld, st),
-         "vs: filter plane");
-  VS_HIP(launch_resid_norms((const float*)idx->codes, idx->ld, r0, n, idx->rn2, st),
-         "vs: residual norms");
+  for (int p = 0; p < 2; ++p) {
+    if (!idx->plane_on[p] || idx->bstats[p]) continue;
+    VS_HIP(hipMalloc(&idx->bstats[p], 4 * sizeof(unsigned)), "vs: bound maxima");
+    VS_HIP(hipMemsetAsync(idx->bstats[p], 0, 4 * sizeof(unsigned), st), "vs: bound maxima");
+  }
+  if (idx->plane_on[FILTER_I8])
+    VS_HIP(launch_quantize_i8((const float*)idx->codes, idx->ld, r0, n,
+                              (int8_t*)idx->fplane[FILTER_I8], idx->fscale, idx->rn2[FILTER_I8], st),
+           "vs: int8 filter plane");
+  if (idx->plane_on[FILTER_BF16]) {
+    VS_HIP(launch_f32_to_bf16((const float*)idx->row(r0), idx->ld,
+                              (uint16_t*)idx->fplane[FILTER_BF16] + r0 * idx->ld, idx->ld, n,
+                              idx->ld, st),
+           "vs: bf16 filter plane");
+    VS_HIP(launch_resid_norms((const float*)idx->codes, idx->ld, r0, n, idx->rn2[FILTER_BF16], st),
+           "vs: residual norms");
+  }
+  // the new rows' maxima fold into the index's (they only grow on add)
+  for (int p = 0; p < 2; ++p)
+    if (idx->plane_on[p])
+      VS_HIP(launch_bound_stats(idx->norms + r0, idx->rn2[p] + r0, n, idx->bstats[p], st, true),
+             "vs: bound maxima");
   return VS_OK;
 }
+
+void free_storage(vs_index* idx);
 
 // Grows storage to hold `rows` rows (plus the tile slack), preserving content.
 int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   const int64_t need = round_up(rows + 256, kRowPad);  // 256-row query tiles of self-joins
   if (need <= idx->capacity) return VS_OK;
   int64_t cap = std::max(need, round_up(idx->capacity + idx->capacity / 2, kRowPad));
-  const bool f32 = idx->esize == 4;
+  const bool i8 = idx->plane_on[FILTER_I8];
   char* codes = nullptr;
   float* norms = nullptr;
-  uint16_t* hplane = nullptr;
-  float* rn2 = nullptr;
+  char* fplane[2] = {nullptr, nullptr};
+  float* rn2[2] = {nullptr, nullptr};
+  float* fscale = nullptr;
   auto release = [&]() {
     if (codes) (void)hipFree(codes);
     if (norms) (void)hipFree(norms);
-    if (hplane) (void)hipFree(hplane);
-    if (rn2) (void)hipFree(rn2);
+    for (int p = 0; p < 2; ++p) {
+      if (fplane[p]) (void)hipFree(fplane[p]);
+      if (rn2[p]) (void)hipFree(rn2[p]);
+      fplane[p] = nullptr;
+      rn2[p] = nullptr;
+    }
+    if (fscale) (void)hipFree(fscale);
+    codes = nullptr;
+    norms = nullptr;
+    fscale = nullptr;
   };
   auto allocate = [&](int64_t c) -> hipError_t {
     hipError_t e = hipMalloc(&codes, (size_t)c * idx->rowbytes());
     if (e == hipSuccess) e = hipMalloc(&norms, (size_t)c * sizeof(float));
-    if (e == hipSuccess && f32) e = hipMalloc(&hplane, (size_t)c * idx->ld * sizeof(uint16_t));
-    if (e == hipSuccess && f32) e = hipMalloc(&rn2, (size_t)c * sizeof(float));
+    for (int p = 0; p < 2; ++p) {
+      if (e == hipSuccess && idx->plane_on[p]) e = hipMalloc(&fplane[p], (size_t)c * idx->planebytes(p));
+      if (e == hipSuccess && idx->plane_on[p]) e = hipMalloc(&rn2[p], (size_t)c * sizeof(float));
+    }
+    if (e == hipSuccess && i8) e = hipMalloc(&fscale, (size_t)c * sizeof(float));
     if (e != hipSuccess) {
       (void)hipGetLastError();
       release();
-      codes = nullptr;
-      norms = nullptr;
-      hplane = nullptr;
-      rn2 = nullptr;
     }
     return e;
   };
@@ -231,13 +293,17 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
          "vs: zeroing storage");
   VS_HIP(hipMemsetAsync(norms + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
          "vs: zeroing norms");
-  if (f32) {
-    VS_HIP(hipMemsetAsync(hplane + keep * idx->ld, 0,
-                          (size_t)(cap - keep) * idx->ld * sizeof(uint16_t), st),
+  for (int p = 0; p < 2; ++p) {
+    if (!idx->plane_on[p]) continue;
+    const int64_t pb = idx->planebytes(p);
+    VS_HIP(hipMemsetAsync(fplane[p] + keep * pb, 0, (size_t)(cap - keep) * pb, st),
            "vs: zeroing plane");
-    VS_HIP(hipMemsetAsync(rn2 + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
+    VS_HIP(hipMemsetAsync(rn2[p] + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
            "vs: zeroing residual norms");
   }
+  if (i8)
+    VS_HIP(hipMemsetAsync(fscale + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
+           "vs: zeroing scales");
   if (idx->codes && keep > 0) {
     VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->rowbytes(),
                           hipMemcpyDeviceToDevice, st),
@@ -245,25 +311,30 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     VS_HIP(hipMemcpyAsync(norms, idx->norms, (size_t)keep * sizeof(float),
                           hipMemcpyDeviceToDevice, st),
            "vs: copying norms");
-    if (f32) {
-      VS_HIP(hipMemcpyAsync(hplane, idx->hplane, (size_t)keep * idx->ld * sizeof(uint16_t),
+    for (int p = 0; p < 2; ++p) {
+      if (!idx->plane_on[p]) continue;
+      VS_HIP(hipMemcpyAsync(fplane[p], idx->fplane[p], (size_t)keep * idx->planebytes(p),
                             hipMemcpyDeviceToDevice, st),
              "vs: copying plane");
-      VS_HIP(hipMemcpyAsync(rn2, idx->rn2, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
-                            st),
+      VS_HIP(hipMemcpyAsync(rn2[p], idx->rn2[p], (size_t)keep * sizeof(float),
+                            hipMemcpyDeviceToDevice, st),
              "vs: copying residual norms");
     }
+    if (i8)
+      VS_HIP(hipMemcpyAsync(fscale, idx->fscale, (size_t)keep * sizeof(float),
+                            hipMemcpyDeviceToDevice, st),
+             "vs: copying scales");
   }
   // In-flight searches (any stream) may still read the old storage.
   VS_HIP(hipDeviceSynchronize(), "vs: storage growth");
-  if (idx->codes) (void)hipFree(idx->codes);
-  if (idx->norms) (void)hipFree(idx->norms);
-  if (idx->hplane) (void)hipFree(idx->hplane);
-  if (idx->rn2) (void)hipFree(idx->rn2);
+  free_storage(idx);
   idx->codes = codes;
   idx->norms = norms;
-  idx->hplane = hplane;
-  idx->rn2 = rn2;
+  for (int p = 0; p < 2; ++p) {
+    idx->fplane[p] = fplane[p];
+    idx->rn2[p] = rn2[p];
+  }
+  idx->fscale = fscale;
   idx->capacity = cap;
   return VS_OK;
 }
@@ -271,12 +342,16 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
 void free_storage(vs_index* idx) {
   if (idx->codes) (void)hipFree(idx->codes);
   if (idx->norms) (void)hipFree(idx->norms);
-  if (idx->hplane) (void)hipFree(idx->hplane);
-  if (idx->rn2) (void)hipFree(idx->rn2);
+  for (int p = 0; p < 2; ++p) {
+    if (idx->fplane[p]) (void)hipFree(idx->fplane[p]);
+    if (idx->rn2[p]) (void)hipFree(idx->rn2[p]);
+    idx->fplane[p] = nullptr;
+    idx->rn2[p] = nullptr;
+  }
+  if (idx->fscale) (void)hipFree(idx->fscale);
   idx->codes = nullptr;
   idx->norms = nullptr;
-  idx->hplane = nullptr;
-  idx->rn2 = nullptr;
+  idx->fscale = nullptr;
   idx->capacity = 0;
 }
 
@@ -332,67 +407,139 @@ int run_gemm(vs_index* idx, const SearchArgs& a, int need, hipStream_t st,
   return VS_OK;
 }
 
-// The filter-and-verify engine (vs_gemm_x1.hip), entirely stream-ordered:
-//  1. split the queries to bf16; the x1 pass keeps 8-entry lane lists per query;
+int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st);
+
+// The filter-and-verify engine (vs_gemm_x1.hip), entirely stream-ordered, as a
+// chain of stages over the planes the index holds (int8, then bf16):
+//  1. convert the stage's queries to its plane (int8 codes + scales, or bf16);
+//     the x1 pass keeps 8-entry lane lists per query;
 //  2. merge them to the KF best approximate candidates;
 //  3. verify_rescore: exact keys of the candidates + the bound check (fail[]);
 //  4. the flagged queries are compacted on the device and re-checked by the
 //     wide verification (every lane-list entry below the list floors);
-//  5. those still flagged are redone by the exact fp32 engine over the gathered
-//     rows (a launch whose tiles past the device-side count exit at once);
-//  6. the merges emit (D, I): all queries, then the redone rows over theirs.
-// The host never waits: counts live in device memory.
-int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st) {
+//  5. the merges emit (D, I) of the stage's queries;
+//  6. the queries still flagged go to the next stage as a gathered batch
+//     (device-side list and count: the int8 plane's wider bound leaves
+//     clustered data to the bf16 plane), and after the last plane to the exact
+//     fp32 engine (a launch whose tiles past the device-side count exit at
+//     once), whose rows overwrite theirs.
+// The host never waits: counts live in device memory.  `gl` / `gc` (stages
+// after the first): the batch is queries gl[0 .. *gc) of `a`.
+int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
+                      int plane, bool last_plane, const int* gl = nullptr,
+                      const int* gc = nullptr) {
   const int ntotal = (int)idx->ntotal;
-  const int nq = a.nq;
   const int mode = a.mode;
+  const bool gathered = gl != nullptr;
   Scratch scr(st);
   X1Args x;
   x.nq_pad = (int)round_up(a.nq_pad, kX1Q);
+  const int nq = gathered ? x.nq_pad : a.nq;  // slots of this stage
   const int nqt = x.nq_pad / kX1Q;
   const int ntiles = (ntotal + kX1Q - 1) / kX1Q;
   const int L = x1_lane_len();
-  // enough lists that their 4*nsplit*L entries cover 4*KF candidates, and one
-  // workgroup per CU on 256 CUs
-  x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, (KF + L - 1) / L),
-                                    std::min<int64_t>(ntiles, (256 + nqt - 1) / nqt));
+  // enough lists that their 4*nsplit*L entries cover 8*KF candidates, and two
+  // workgroups per CU on 256 CUs: 128 lists per query at C3.  More lists put
+  // the wide check's floor T (the best last entry of a full list) deeper
+  // behind the top-M, which the bound needs on clustered data and on the int8
+  // plane (profiles/r02l_ab_split.txt; one workgroup per CU left 0.7 % of the
+  // C3 queries to the exact engine on int8)
+  x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, 2 * ((KF + L - 1) / L)),
+                                    std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
   x.nsplit = std::max(x.nsplit, 1);
+  {  // A/B: more (shorter) database splits = more lane lists per query
+    static const int mult = [] {
+      const char* e = getenv("VS_X1_SPLIT_MULT");
+      return e && atoi(e) > 1 ? atoi(e) : 1;
+    }();
+    x.nsplit = (int)std::min<int64_t>(ntiles, (int64_t)x.nsplit * mult);
+  }
   Partials part;  // lane lists: L entries each
   part.KP = L;
   part.P = 4 * x.nsplit;
   const size_t np_ = (size_t)x.nq_pad * part.P * part.KP;
   VS_HIP(scr.alloc((void**)&part.key, np_ * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&part.id, np_ * sizeof(int)), "vs: scratch");
-  // bf16 query plane: a split of the staged queries, or the stored rows' plane
-  const uint16_t* QH = nullptr;
-  const float* Q = a.qbuf;  // fp32 query rows for the rescoring
-  if (a.self0 >= 0) {
-    QH = idx->hplane + a.self0 * idx->ld;
-    Q = (const float*)idx->row(a.self0);
+  // this stage's fp32 query rows and aux values: the staged batch, the stored
+  // rows (self-joins), or a gathered copy of the flagged ones
+  const float* Q = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
+  const float* qaux = a.qaux;
+  int* qrow = nullptr;
+  if (gathered) {
+    float *qc = nullptr, *ac = nullptr;
+    VS_HIP(scr.alloc((void**)&qc, (size_t)x.nq_pad * idx->ld * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&ac, (size_t)x.nq_pad * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&qrow, (size_t)x.nq_pad * sizeof(int)), "vs: scratch");
+    VS_HIP(launch_gather_queries(Q, idx->ld, a.qaux, gl, gc, x.nq_pad, a.self0, qc, ac, qrow, st),
+           "vs: gathered queries");
+    Q = qc;
+    qaux = ac;
+  }
+  const bool self_rows = a.self0 >= 0 && !gathered;  // queries are stored rows in place
+  const int qa_rows = gathered ? x.nq_pad : a.nq_pad;  // rows of Q / qaux
+  // query plane: a conversion of the stage's queries, or the stored rows' plane
+  const bool i8 = plane == FILTER_I8;
+  const int64_t pb = idx->planebytes(plane);
+  const char* QH = nullptr;
+  const float* qs = nullptr;    // int8: query scales
+  const float* qr2 = nullptr;   // int8: query residual norms (for the bound)
+  if (self_rows) {
+    QH = idx->fplane[plane] + a.self0 * pb;
+    if (i8) {
+      qs = idx->fscale + a.self0;
+      qr2 = idx->rn2[FILTER_I8] + a.self0;
+    }
   } else {
-    uint16_t* qh = nullptr;
-    VS_HIP(scr.alloc((void**)&qh, (size_t)x.nq_pad * idx->ld * sizeof(uint16_t)), "vs: scratch");
-    VS_HIP(launch_f32_to_bf16(a.qbuf, idx->ld, qh, idx->ld, a.nq_pad, idx->ld, st),
-           "vs: query plane");
-    if (x.nq_pad > a.nq_pad)
-      VS_HIP(hipMemsetAsync(qh + (size_t)a.nq_pad * idx->ld, 0,
-                            (size_t)(x.nq_pad - a.nq_pad) * idx->ld * sizeof(uint16_t), st),
+    char* qh = nullptr;
+    VS_HIP(scr.alloc((void**)&qh, (size_t)x.nq_pad * pb), "vs: scratch");
+    if (i8) {
+      float *sc = nullptr, *r = nullptr;
+      VS_HIP(scr.alloc((void**)&sc, (size_t)qa_rows * sizeof(float)), "vs: scratch");
+      VS_HIP(scr.alloc((void**)&r, (size_t)qa_rows * sizeof(float)), "vs: scratch");
+      VS_HIP(launch_quantize_i8(Q, idx->ld, 0, qa_rows, (int8_t*)qh, sc, r, st), "vs: query plane");
+      qs = sc;
+      qr2 = r;
+    } else {
+      VS_HIP(launch_f32_to_bf16(Q, idx->ld, (uint16_t*)qh, idx->ld, qa_rows, idx->ld, st),
+             "vs: query plane");
+    }
+    if (x.nq_pad > qa_rows)
+      VS_HIP(hipMemsetAsync(qh + (size_t)qa_rows * pb, 0, (size_t)(x.nq_pad - qa_rows) * pb, st),
              "vs: query plane");
     QH = qh;
   }
-  unsigned* stats = nullptr;
-  VS_HIP(scr.alloc((void**)&stats, 4 * sizeof(unsigned)), "vs: scratch");
-  VS_HIP(launch_bound_stats(idx->norms, idx->rn2, ntotal, stats, st), "vs: bound stats");
-  x.XH = idx->hplane;
+  const unsigned* stats = idx->bstats[plane];  // the index's maxima (kept by add / remove)
+  x.filter = plane;
+  x.XH = idx->fplane[plane];
+  x.xs = idx->fscale;
+  if (i8 && mode == MODE_COS) {
+    // the cosine folds the inverse norms into the int8 factors: s_x / |x| per
+    // row (capacity rows: tiles read past ntotal), s_q / |q| per query
+    float* cx = nullptr;
+    VS_HIP(scr.alloc((void**)&cx, (size_t)idx->capacity * sizeof(float)), "vs: scratch");
+    VS_HIP(launch_mul_arrays(idx->fscale, a.xaux, idx->capacity, cx, st), "vs: cosine factors");
+    x.xs = cx;
+    if (self_rows) {
+      qs = cx + a.self0;
+    } else {
+      float* cq = nullptr;
+      VS_HIP(scr.alloc((void**)&cq, (size_t)qa_rows * sizeof(float)), "vs: scratch");
+      VS_HIP(launch_mul_arrays(qs, qaux, qa_rows, cq, st), "vs: cosine factors");
+      qs = cq;
+    }
+  }
   x.xaux = a.xaux;
   x.QH = QH;
-  x.qaux = a.qaux;
-  x.nqa = a.nq_pad;
+  x.qs = qs;
+  x.qaux = qaux;
+  x.nqa = qa_rows;
   x.ld = idx->ld;
   x.ntotal = ntotal;
-  x.self0 = a.self0;
+  x.self0 = self_rows ? a.self0 : -1;
+  x.qrow = qrow;
+  x.qcount = gc;
   {
-    KernelTimer tm(st, "gemm_topk_x1");
+    KernelTimer tm(st, gathered ? nullptr : i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1");
     VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &tm.dispatches), "vs: gemm_topk_x1 launch");
     tm.stop();
   }
@@ -404,7 +551,8 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   Partials mp = part;
   mp.KP = kp_for(KF);
   mp.KL = L;
-  VS_HIP(launch_merge_partials(MODE_L2, mp, nq, KF, 0, 0.0f, Dk, Ik, KF, st), "vs: merge");
+  VS_HIP(launch_merge_partials(MODE_L2, mp, nq, KF, 0, 0.0f, Dk, Ik, KF, st, 0, nullptr, gc),
+         "vs: merge");
   Partials vp;
   vp.KP = kp_for(KF);
   vp.P = 1;
@@ -414,33 +562,116 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(scr.alloc((void**)&vp.key, (size_t)nq * vp.KP * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&vp.id, (size_t)nq * vp.KP * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&flags, (size_t)nq * sizeof(int)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&qlist, (size_t)a.nq_pad * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qlist, (size_t)x.nq_pad * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&qcount, 2 * sizeof(int)), "vs: scratch");
-  const BoundArgs ba = make_bound_args(idx->ld);
-  const float* qinv = mode == MODE_COS ? a.qaux : nullptr;
+  const BoundArgs ba = make_bound_args(idx->ld, plane);
+  const float* qinv = mode == MODE_COS ? qaux : nullptr;
   const float* xinv = mode == MODE_COS ? a.xaux : nullptr;
   VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
-                               Q, a.qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
-                               st, qinv, xinv),
+                               Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
+                               st, qinv, xinv, qr2, gc),
          "vs: verify");
   unsigned long long* dst = device_stats(idx->device);
   if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
-  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, dst + 0, st), "vs: flags");
+  // statistics: [0] queries (first stage), [1] flagged by a first check, [2]
+  // redone by the exact engine, [3] handed to a second filter stage
+  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, gathered ? nullptr : dst + 0, st),
+         "vs: flags");
   if (wide_enabled())
     VS_HIP(launch_verify_wide(mode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
-                              idx->norms, Q, a.qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
-                              vp.KP, flags, st, qinv, xinv),
+                              idx->norms, Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
+                              vp.KP, flags, st, qinv, xinv, qr2),
            "vs: verify wide");
-  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, dst + 2, nullptr, st), "vs: flags");
+  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, last_plane ? dst + 2 : dst + 3,
+                              nullptr, st),
+         "vs: flags");
   VS_HIP(launch_merge_partials(mode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
-                               a.raw),
+                               a.raw, gl, gc),
          "vs: merge");
-  // the exact redo of what is still flagged (usually nothing: every tile exits;
-  // untimed, so the kernel timer holds the filter pass alone)
+  // what is still flagged (usually nothing: every tile exits), as query ids of `a`
+  const int* next = qlist;
+  if (gathered) {
+    int* composed = nullptr;
+    VS_HIP(scr.alloc((void**)&composed, (size_t)x.nq_pad * sizeof(int)), "vs: scratch");
+    VS_HIP(launch_compose_list(gl, qlist, qcount + 1, x.nq_pad, composed, st), "vs: flags");
+    next = composed;
+  }
+  if (!last_plane) {
+    if (!gathered && plane == FILTER_I8) {
+      int rc = adaptive_record(idx, qcount + 1, nq, st);
+      if (rc) return rc;
+    }
+    return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, true, next, qcount + 1);
+  }
+  // the exact redo (untimed: the kernel timer holds the first filter pass)
   SearchArgs ex = a;
   ex.qbuf = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
-  ex.nq_pad = (int)round_up(nq, kBQ);
-  return run_gemm(idx, ex, need, st, qlist, qcount + 1);
+  ex.nq_pad = (int)round_up(a.nq, kBQ);
+  return run_gemm(idx, ex, need, st, next, qcount + 1);
+}
+
+// Fraction of int8-stage queries handed on to bf16 above which the int8 stage
+// costs more than it saves (stage costs ~0.58 and 1 of a bf16-only search:
+// break-even ~0.42).
+constexpr double kI8HandOffMax = 0.3;
+
+// Whether this search starts on the int8 plane (see vs_index::Adaptive).  While
+// the int8 stage hands on too much, searches start on bf16, with an int8 probe
+// after 1, 2, 4 .. 64 of them (each probe's counters arrive with a later search).
+bool adaptive_use_i8(vs_index* idx) {
+  auto& A = idx->ad;
+  std::lock_guard<std::mutex> g(A.mu);
+  bool fresh = false;
+  if (A.pending && hipEventQuery(A.ev) == hipSuccess) {
+    const unsigned long long q = A.hmirror[0], h = A.hmirror[1];
+    if (q > A.seen_q) {
+      const double f = (double)(h - A.seen_h) / (double)(q - A.seen_q);
+      A.ema = A.have ? 0.5 * A.ema + 0.5 * f : f;
+      A.have = true;
+      fresh = true;
+    }
+    A.seen_q = q;
+    A.seen_h = h;
+    A.pending = false;
+  }
+  if (!A.have || A.ema <= kI8HandOffMax) {
+    A.backoff = 1;
+    A.skip_left = 0;
+    return true;
+  }
+  if (fresh) {
+    A.skip_left = A.backoff;
+    A.backoff = std::min(2 * A.backoff, 64);
+  }
+  if (A.skip_left > 0) {
+    --A.skip_left;
+    return false;
+  }
+  A.skip_left = A.backoff;  // a probe; bf16 until its counters arrive
+  return true;
+}
+
+// The per-index counters of an int8-first search: what the int8 stage saw
+// and handed on, then an async copy to the pinned mirror (one in flight).
+int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st) {
+  auto& A = idx->ad;
+  std::lock_guard<std::mutex> g(A.mu);
+  if (!A.dcount) {
+    VS_HIP(hipMalloc(&A.dcount, 2 * sizeof(unsigned long long)), "vs: adaptive counters");
+    VS_HIP(hipMemset(A.dcount, 0, 2 * sizeof(unsigned long long)), "vs: adaptive counters");
+    VS_HIP(hipHostMalloc(&A.hmirror, 2 * sizeof(unsigned long long)), "vs: adaptive counters");
+    A.hmirror[0] = A.hmirror[1] = 0;
+    VS_HIP(hipEventCreateWithFlags(&A.ev, hipEventDisableTiming), "vs: adaptive counters");
+  }
+  VS_HIP(launch_add_counts(handed, n, A.dcount, st), "vs: adaptive counters");
+  if (!A.pending) {
+    VS_HIP(hipMemcpyAsync(A.hmirror, A.dcount, 2 * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, st),
+           "vs: adaptive counters");
+    VS_HIP(hipEventRecord(A.ev, st), "vs: adaptive counters");
+    A.pending = true;
+  }
+  return VS_OK;
 }
 
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
@@ -526,8 +757,17 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
                : idx->engine != VS_ENGINE_AUTO ? idx->engine
                                                : engine_from_env();
   const int KF = x1_list_len(need);
-  if (idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0)
-    return run_filter_verify(idx, a, need, KF, st);
+  if (idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0) {
+    // the planes this search runs through: int8 first (inner product and
+    // cosine), then bf16; a forced *_VERIFY engine runs its plane alone
+    bool i8_ok = idx->plane_on[FILTER_I8] && idx->ld <= kI8MaxLd && mode != MODE_L2 &&
+                 engine != VS_ENGINE_BF16_VERIFY;
+    const bool b16_ok = idx->plane_on[FILTER_BF16] && engine != VS_ENGINE_I8_VERIFY;
+    // the automatic order adapts to how much the int8 stage settles
+    if (i8_ok && b16_ok && engine == VS_ENGINE_AUTO) i8_ok = adaptive_use_i8(idx);
+    if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
+    if (b16_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, true);
+  }
   return run_gemm(idx, a, need, st);
 }
 
@@ -578,6 +818,7 @@ int vs_create(int d, int metric, int dtype, int device, vs_index** out) {
   idx->dtype = dtype;
   idx->device = device;
   idx->esize = dtype == VS_DTYPE_BF16 ? 2 : 4;
+  planes_for(idx);
   idx->ld = round_up(d, 64);  // 64-element K-steps of the filter pass (128-B plane rows)
   *out = idx;
   return VS_OK;
@@ -589,6 +830,11 @@ int vs_destroy(vs_index* idx) {
     DeviceGuard g(idx->device);
     (void)hipDeviceSynchronize();
     free_storage(idx);
+    for (int p = 0; p < 2; ++p)
+      if (idx->bstats[p]) (void)hipFree(idx->bstats[p]);
+    if (idx->ad.dcount) (void)hipFree(idx->ad.dcount);
+    if (idx->ad.hmirror) (void)hipHostFree(idx->ad.hmirror);
+    if (idx->ad.ev) (void)hipEventDestroy(idx->ad.ev);
   }
   delete idx;
   return VS_OK;
@@ -706,6 +952,8 @@ int vs_reset(vs_index* idx) {
   DeviceGuard g(idx->device);
   VS_HIP(hipDeviceSynchronize(), "vs_reset");
   free_storage(idx);
+  for (int p = 0; p < 2; ++p)
+    if (idx->bstats[p]) VS_HIP(hipMemset(idx->bstats[p], 0, 4 * sizeof(unsigned)), "vs_reset");
   idx->ntotal = 0;
   return VS_OK;
 }
@@ -737,10 +985,22 @@ int vs_dtype(const vs_index* idx, int* out) {
 int vs_set_engine(vs_index* idx, int engine) {
   if (!idx) return fail(VS_E_INVALID, "vs_set_engine: null index");
   if (engine != VS_ENGINE_AUTO && engine != VS_ENGINE_FP32_MFMA &&
-      engine != VS_ENGINE_BF16_VERIFY)
+      engine != VS_ENGINE_BF16_VERIFY && engine != VS_ENGINE_I8_VERIFY)
     return fail(VS_E_INVALID, "vs_set_engine: unknown engine");
   std::unique_lock<std::shared_mutex> lk(idx->mu);
+  if (idx->esize == 4 && engine == VS_ENGINE_I8_VERIFY && !idx->plane_on[FILTER_I8])
+    return fail(VS_E_UNSUPPORTED,
+                "vs_set_engine: no int8 filter plane (it serves inner-product indexes)");
+  if (idx->esize == 4 && engine == VS_ENGINE_BF16_VERIFY && !idx->plane_on[FILTER_BF16])
+    return fail(VS_E_UNSUPPORTED, "vs_set_engine: no bf16 filter plane (VS_FILTER=i8)");
   idx->engine = engine;
+  return VS_OK;
+}
+
+int vs_filter_plane(const vs_index* idx, int* out) {
+  if (!idx || !out) return fail(VS_E_INVALID, "vs_filter_plane: null argument");
+  *out = (idx->plane_on[FILTER_I8] ? VS_FILTER_I8 : 0) |
+         (idx->plane_on[FILTER_BF16] ? VS_FILTER_BF16 : 0);
   return VS_OK;
 }
 
@@ -937,32 +1197,32 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
                             hipMemcpyDeviceToDevice, st),
              "vs_remove_ids: move norms");
     }
-    if (idx->hplane) {  // the filter plane and residual norms move with their rows
-      const int64_t pb = idx->ld * (int64_t)sizeof(uint16_t);
-      VS_HIP(launch_gather_kept(idx->hplane, idx->rn2, pb, s0, cn, drm, nrem, tmp, tmpn, st),
-             "vs_remove_ids: gather plane");
-      if (kept > 0) {
-        VS_HIP(hipMemcpyAsync(idx->hplane + dst * idx->ld, tmp, (size_t)kept * pb,
-                              hipMemcpyDeviceToDevice, st),
-               "vs_remove_ids: move plane");
-        VS_HIP(hipMemcpyAsync(idx->rn2 + dst, tmpn, (size_t)kept * sizeof(float),
-                              hipMemcpyDeviceToDevice, st),
-               "vs_remove_ids: move residual norms");
-      }
-    }
   }
   const int64_t nt = idx->ntotal - nrem;
   VS_HIP(hipMemsetAsync(idx->row(nt), 0, (size_t)nrem * idx->rowbytes(), st),
          "vs_remove_ids: zero tail");
   VS_HIP(hipMemsetAsync(idx->norms + nt, 0, (size_t)nrem * sizeof(float), st),
          "vs_remove_ids: zero tail");
-  if (idx->hplane) {
-    VS_HIP(hipMemsetAsync(idx->hplane + nt * idx->ld, 0,
-                          (size_t)nrem * idx->ld * sizeof(uint16_t), st),
+  // the filter planes are re-derived from the moved rows (one pass over
+  // them), and their tails zeroed like the rows'; the bound maxima are
+  // recomputed over the remaining rows (a removal can lower them)
+  int rc = derive_plane(idx, first, nt - first, st);
+  if (rc) return rc;
+  for (int p = 0; p < 2; ++p)
+    if (idx->plane_on[p] && idx->bstats[p])
+      VS_HIP(launch_bound_stats(idx->norms, idx->rn2[p], nt, idx->bstats[p], st),
+             "vs_remove_ids: bound maxima");
+  for (int p = 0; p < 2; ++p) {
+    if (!idx->plane_on[p]) continue;
+    const int64_t pb = idx->planebytes(p);
+    VS_HIP(hipMemsetAsync(idx->fplane[p] + nt * pb, 0, (size_t)nrem * pb, st),
            "vs_remove_ids: zero tail");
-    VS_HIP(hipMemsetAsync(idx->rn2 + nt, 0, (size_t)nrem * sizeof(float), st),
+    VS_HIP(hipMemsetAsync(idx->rn2[p] + nt, 0, (size_t)nrem * sizeof(float), st),
            "vs_remove_ids: zero tail");
   }
+  if (idx->fscale)
+    VS_HIP(hipMemsetAsync(idx->fscale + nt, 0, (size_t)nrem * sizeof(float), st),
+           "vs_remove_ids: zero tail");
   VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
   idx->ntotal = nt;
   if (nremoved) *nremoved = nrem;
@@ -1052,8 +1312,8 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
 
 // The counters live on the devices (written by the searches' own kernels); reading
 // them waits for every search already queued on those devices.
-static int read_filter_stats(unsigned long long out[3], int reset) {
-  out[0] = out[1] = out[2] = 0;
+static int read_filter_stats(unsigned long long out[4], int reset) {
+  out[0] = out[1] = out[2] = out[3] = 0;
   std::lock_guard<std::mutex> g(g_stats_mu);
   for (int dev = 0; dev < (int)g_dev_stats.size(); ++dev) {
     if (!g_dev_stats[dev]) continue;
@@ -1061,7 +1321,7 @@ static int read_filter_stats(unsigned long long out[3], int reset) {
     unsigned long long h[4] = {0, 0, 0, 0};
     VS_HIP(hipDeviceSynchronize(), "vs_filter_stats");
     VS_HIP(hipMemcpy(h, g_dev_stats[dev], sizeof(h), hipMemcpyDeviceToHost), "vs_filter_stats");
-    for (int i = 0; i < 3; ++i) out[i] += h[i];
+    for (int i = 0; i < 4; ++i) out[i] += h[i];
     if (reset) VS_HIP(hipMemset(g_dev_stats[dev], 0, sizeof(h)), "vs_filter_stats");
   }
   return VS_OK;
@@ -1069,7 +1329,7 @@ static int read_filter_stats(unsigned long long out[3], int reset) {
 
 int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
   if (!queries || !fallbacks) return fail(VS_E_INVALID, "vs_filter_stats: null output");
-  unsigned long long c[3];
+  unsigned long long c[4];
   int rc = read_filter_stats(c, reset);
   if (rc) return rc;
   *queries = (int64_t)c[0];
@@ -1079,10 +1339,19 @@ int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
 
 int vs_filter_wide_stats(int64_t* wide) {
   if (!wide) return fail(VS_E_INVALID, "vs_filter_wide_stats: null output");
-  unsigned long long c[3];
+  unsigned long long c[4];
   int rc = read_filter_stats(c, 0);
   if (rc) return rc;
   *wide = (int64_t)c[1];
+  return VS_OK;
+}
+
+int vs_filter_second_stats(int64_t* second) {
+  if (!second) return fail(VS_E_INVALID, "vs_filter_second_stats: null output");
+  unsigned long long c[4];
+  int rc = read_filter_stats(c, 0);
+  if (rc) return rc;
+  *second = (int64_t)c[3];
   return VS_OK;
 }
 
@@ -1108,11 +1377,16 @@ const char* vs_timer_kernel(void) {
 }
 
 int vs_timer_read(double* total_ms, int64_t* launches) {
+  return vs_timer_read_kernel(nullptr, total_ms, launches);
+}
+
+int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches) {
   if (!total_ms || !launches) return fail(VS_E_INVALID, "vs_timer_read: null output");
   std::lock_guard<std::mutex> g(g_timer_mu);
   double tot = 0.0;
   int64_t n = 0;
   for (auto& p : g_timer_events) {
+    if (kernel && strcmp(kernel, p.name) != 0) continue;
     VS_HIP(hipEventSynchronize(p.b), "vs_timer_read: synchronise");
     float ms = 0.0f;
     VS_HIP(hipEventElapsedTime(&ms, p.a, p.b), "vs_timer_read: elapsed");

@@ -8,6 +8,8 @@ namespace vs {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define VS_LDS(p) ((__attribute__((address_space(3))) void*)(p))
 
 // ---------------------------------------------------------------------------

@@ -1,11 +1,17 @@
-// vs_gemm_x1.hip — the filter pass of the filter-and-verify engine: one bf16
-// MFMA product per fp32 product, fused with per-lane candidate lists.
+// vs_gemm_x1.hip — the filter pass of the filter-and-verify engine: one
+// low-precision MFMA product per fp32 product, fused with per-lane candidate
+// lists.
 //
-// Every fp32 index keeps, beside its fp32 rows, the bf16 (round-to-nearest-even)
-// copy of every row ("hi plane", [capacity][ld] uint16, row-major) and the
-// squared norm of each row's residual x - hi.  A search splits its queries the
-// same way and the kernel below scores every (query, row) pair with the single
-// product hi(q) . hi(x) on v_mfma_f32_32x32x16_bf16 — a plain bf16 GEMM over
+// Every fp32 index keeps, beside its fp32 rows, a "filter plane" copy of every
+// row ([capacity][ld], row-major) and the squared norm of each row's residual
+// x - plane(x).  Two planes exist (vs_internal.h, Filter):
+//   int8 (default): code = rint(x / s) with one scale s = max|x| / 127 per row;
+//     the kernel multiplies codes on v_mfma_i32_32x32x32_i8 (exact int32 sums,
+//     twice the bf16 MFMA rate, 64 elements per 64-B step) and scales the sum
+//     by s_q * s_x in the epilogue;
+//   bf16: round-to-nearest-even copies on v_mfma_f32_32x32x16_bf16.
+// A search converts its queries the same way and the kernel below scores every
+// (query, row) pair with the one product plane(q) . plane(x) — a plain GEMM over
 // Q (nq x d) and X (N x d) whose output never leaves the chip: each lane keeps
 // the best approximate keys of its queries.  The exact answer is then proved and
 // produced by verify_rescore_kernel (below): the candidates are rescored in
@@ -17,7 +23,7 @@
 // [64 (w>>1), +64): 4 x 2 accumulators of 32x32 (128 registers); lane l sees
 // queries c = l&31 of its two 32-query blocks and keeps one sorted list of KR
 // entries per query (lanes l and l+32 hold disjoint rows of the same query).
-// K advances 32 elements (64 B per row) per step through a ring of NBUF LDS
+// K advances 64 B per row per step (32 bf16 / 64 int8 elements) through a ring of NBUF LDS
 // images (both operand tiles of one step, 32 KB), filled by
 // global_load_lds_dwordx4 (LDS-DMA) NBUF-1 steps ahead; see gemm_topk_x1
 // below for the step schedule.
@@ -29,6 +35,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "vs_device.h"
 
@@ -64,9 +71,6 @@
 #ifndef VS_X1_P_NOWAIT  // no vmcnt wait in the loop (the DMA still issued)
 #define VS_X1_P_NOWAIT 0
 #endif
-#ifndef VS_X1_P_FULLLINE  // DMA pieces of 8 rows x 128 B instead of 16 rows x 64 B
-#define VS_X1_P_FULLLINE 0
-#endif
 
 namespace vs {
 
@@ -76,6 +80,18 @@ constexpr int kT = 256;               // rows (and queries) per tile
 constexpr int kX1ChunkTiles = 16;     // database tiles per workgroup per launch
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
+__device__ __forceinline__ i32x4 as_i4(const uint4& u) { return __builtin_bit_cast(i32x4, u); }
+
+// One 32x32 block of one 64-B sub-step: C (+)= A . B on the plane's MFMA.
+template <int EL>
+using AccT = typename std::conditional<EL == FILTER_I8, i32x16, f32x16>::type;
+template <int EL>
+__device__ __forceinline__ AccT<EL> mfma_blk(const uint4& a, const uint4& b, const AccT<EL>& c) {
+  if constexpr (EL == FILTER_I8)
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(a), as_i4(b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), as_bf(b), c, 0, 0, 0);
+}
 
 // LDS-DMA of 16 B per lane into the wave-uniform LDS byte address `lds` (M0 is
 // written and restored inside the statement; cdna_hip_programming.md §5.7).
@@ -84,14 +100,26 @@ __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_c
 // ds_reads of that image (the builtin form makes hipcc assume every later LDS
 // read may alias it and drain vmcnt to 0 before them).  No VGPR destination,
 // so no register hazard.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+// The source is a uniform base (SGPR pair) plus a 32-bit per-lane offset: no
+// 64-bit address VGPRs beside the accumulators.
+__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gsrc), "s"(lds)
+      : "v"(voff), "s"(sbase), "s"(lds)
       : "memory");
+}
+
+// Row order inside database tile t: LDS slot s holds tile row s ^ tile_perm(t)
+// (bits 2..7, so 4-row groups stay contiguous).  The slot decides which lane
+// list sees a row; without the permutation a row's list would depend only on
+// row % 256, and data laid out periodically (rows of one cluster every 1024
+// rows, say) would crowd a quarter of a query's lists, pulling the wide
+// check's floor T toward the top and failing its bound.
+__device__ __forceinline__ int tile_perm(int t) {
+  return (int)(((uint32_t)t * 2654435761u) >> 24) & 0xFC;
 }
 
 __device__ __forceinline__ float sel16(const f32x16& v, int i) {
@@ -128,12 +156,13 @@ __device__ __forceinline__ float sel16(const f32x16& v, int i) {
 // XCD blocking (a 256-workgroup grid, one per CU): the 32 workgroups of an XCD
 // take QG query tiles x DG database splits (QG = min(nqt, 4)), so each XCD's L2
 // serves a query tile to DG workgroups and a database tile to QG of them.
-template <int KR, int MODE, int NBUF>
+template <int KR, int MODE, int NBUF, int EL>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
-    const uint16_t* __restrict__ XH, const float* __restrict__ xaux,
-    const uint16_t* __restrict__ QH, const float* __restrict__ qaux, int nqa, int64_t ld,
-    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0, int chunk, int nchunk,
-    int KP, float* __restrict__ pkey, int* __restrict__ pid) {
+    const char* __restrict__ XH, const float* __restrict__ xs, const float* __restrict__ xaux,
+    const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
+    int nqa, int64_t ldb, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0,
+    const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
+    float* __restrict__ pkey, int* __restrict__ pid) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
   constexpr int D = NBUF - 1;      // steps in flight
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
@@ -163,19 +192,24 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       sp = lb / nqt;
     }
   }
+  // a gathered batch (device-side count): query tiles past it have nothing to do
+  if (qcount && qt * kT >= *qcount) return;  // uniform
   const int s0 = (int)((int64_t)sp * ntiles / nsplit);
   const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
   const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
   const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
 
   int gq[2], selfrow[2];
-  float qa[2];
+  float qa[2], qsc[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     gq[qb] = qt * kT + 64 * wq + 32 * qb + c32;
     qa[qb] = 0.0f;
-    if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
-    selfrow[qb] = self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
+    if constexpr (MODE == MODE_L2 || (MODE == MODE_COS && EL != FILTER_I8))
+      qa[qb] = gq[qb] < nqa ? qaux[gq[qb]] : 0.0f;
+    qsc[qb] = 0.0f;
+    if constexpr (EL == FILTER_I8) qsc[qb] = gq[qb] < nqa ? qs[gq[qb]] : 0.0f;
+    selfrow[qb] = qrow ? (gq[qb] < nqa ? qrow[gq[qb]] : -1) : self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
   }
   const int P = nsplit * 4;
   const int pl = sp * 4 + wr * 2 + h;
@@ -199,25 +233,37 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
     for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
     asm volatile("" ::"v"(qa[qb]));
+    if constexpr (EL == FILTER_I8) asm volatile("" ::"v"(qsc[qb]));
   }
 
   if (t1 > t0) {  // uniform over the workgroup
-    const uint32_t ldb = (uint32_t)ld * 2u;
-#if !VS_X1_P_FULLLINE
-    const uint32_t soff = (uint32_t)(lane >> 2) * ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
-#else
-    const uint32_t soff = (uint32_t)(lane >> 3) * ldb + (uint32_t)(lane & 7) * 16u;
-#endif
+    // per-lane DMA source: row (lane >> 2) of a 16-row piece, 16-B chunk
+    // swizzled by the LDS slot (c ^ ((slot >> 2) & 3))
+    const uint32_t soff =
+        (uint32_t)(lane >> 2) * (uint32_t)ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
     const int fsw = (c32 >> 2) & 3;
-    const char* qtile = (const char*)(QH + (int64_t)qt * kT * ld) + (uint32_t)(32 * w) * ldb;
+    const char* qtile = QH + (int64_t)qt * kT * ldb + (uint32_t)(32 * w) * (uint32_t)ldb;
     const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
     const int nsteps = (t1 - t0) * nksteps;
 
     // load cursor: the step it issues next (past the end it keeps re-reading
     // the last step: unconditional loads keep the vmcnt counts fixed)
     int ls = 0, lt = t0, lk_ = 0, lbuf = 0;
+    // the load tile's permuted source rows: slot 32 w + 16 p + (lane >> 2) of
+    // piece p reads row (32 w + 16 p) ^ (f & 0xF0) + ((lane >> 2) ^ (f & 0x0C))
+    // (the two parts occupy disjoint bits): one lane offset, a uniform rest
+    uint32_t xlane = 0;
+    int xhi = 0;
+    auto set_xoff = [&](int tt) {  // once per tile; the lane id is re-derived
+      const int f = tile_perm(tt);
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      xhi = f & 0xF0;
+      xlane = (uint32_t)((ln >> 2) ^ (f & 0x0C)) * (uint32_t)ldb +
+              (uint32_t)((ln & 3) ^ (ln >> 4)) * 16u;
+    };
+    set_xoff(t0);
 
-    f32x16 acc[4][2];
+    AccT<EL> acc[4][2];
     // fragments of one sub-step: A (database rows) x4, B (queries) x2
     uint4 fa0[4], fb0[2], fa1[4], fb1[2];
     auto rd = [&](int buf, int s2, uint4 (&fa)[4], uint4 (&fb)[2]) {
@@ -240,31 +286,33 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #endif
     };
     auto mfma_rb = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
-      acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), acc[rb][0], 0, 0, 0);
-      acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), acc[rb][1], 0, 0, 0);
+      acc[rb][0] = mfma_blk<EL>(fa[rb], fb[0], acc[rb][0]);
+      acc[rb][1] = mfma_blk<EL>(fa[rb], fb[1], acc[rb][1]);
     };
     // the first sub-step of a tile: C = 0 (inline constant), no clearing pass
     auto mfma_rb_first = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
-      const f32x16 z = {};
-      acc[rb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[0]), z, 0, 0, 0);
-      acc[rb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(fa[rb]), as_bf(fb[1]), z, 0, 0, 0);
+      const AccT<EL> z = {};
+      acc[rb][0] = mfma_blk<EL>(fa[rb], fb[0], z);
+      acc[rb][1] = mfma_blk<EL>(fa[rb], fb[1], z);
     };
     // the four LDS-DMA pieces of the load cursor's step, one at a time
     auto stage_piece = [&](int i) {
-      const char* xs = (const char*)(XH + (int64_t)lt * kT * ld) + (uint32_t)(32 * w) * ldb +
-                       lk_ * 64;
-      const char* qs = qtile + lk_ * 64;
+      // uniform bases (the piece's permuted 16-row group of the load tile, the
+      // query tile's) + per-lane offsets below 256 rows
+      const char* xbase = XH + (int64_t)lt * kT * ldb + lk_ * 64 +
+                          (uint32_t)((32 * w + 16 * (i >> 1)) ^ xhi) * (uint32_t)ldb;
+      const char* qbase = qtile + lk_ * 64 + (uint32_t)(16 * (i >> 1)) * (uint32_t)ldb;
       const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
-      const uint32_t o = soff + (uint32_t)(16 * (i >> 1)) * ldb;
 #if !VS_X1_P_NODMA
       if ((i & 1) == 0) {
-        if (!(VS_X1_P_NODMA_X)) glds16(xs + o, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
+        if (!(VS_X1_P_NODMA_X))
+          glds16(xbase, xlane, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
       } else {
         if (!(VS_X1_P_NODMA_Q))
-          glds16(qs + o, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
+          glds16(qbase, soff, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
       }
 #else
-      asm volatile("" ::"v"(xs + o), "v"(qs + o), "s"(lx));
+      asm volatile("" ::"v"(xlane), "v"(soff), "s"(xbase), "s"(qbase), "s"(lx));
 #endif
     };
     auto advance_cursor = [&]() {
@@ -272,23 +320,34 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         ++ls;
         if (++lk_ == nksteps) {
           lk_ = 0;
-          ++lt;
+          set_xoff(++lt);
         }
       }
       lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
     };
     auto epilogue = [&](int t) {
       // uniform: every row of the tile exists and none is excluded
-      const bool plain = self0 < 0 && (t + 1) * kT <= ntotal;
+      const bool plain = self0 < 0 && !qrow && (t + 1) * kT <= ntotal;
+      const int f = tile_perm(t);
+      // slot 128 wr + 32 rb + 8 jj + 4 h + e holds row t kT + (slot ^ f) + e; the
+      // slot's fields are disjoint bits, so the XOR splits into a uniform part
+      // (wr, rb, jj) and one lane part (h), and f leaves the low two bits (e)
+      const int fh = (4 * h) ^ (f & 0x04);
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
-        const int r0 = t * kT + 128 * wr + 32 * rb;
-        f32x4 xa[4];
+        auto rowof = [&](int jj) {
+          return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh;
+        };
+        // int8: xs holds s_x (IP) or s_x / |x| (COS), qsc s_q or s_q / |q|
+        f32x4 xa[4], xsv[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (MODE == MODE_L2 || MODE == MODE_COS)
-            xa[jj] = *(const f32x4*)(xaux + r0 + 8 * jj + 4 * h);
+          const int g = rowof(jj);
+          if constexpr ((MODE == MODE_L2 || MODE == MODE_COS) && EL != FILTER_I8)
+            xa[jj] = *(const f32x4*)(xaux + g);
+          xsv[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (EL == FILTER_I8) xsv[jj] = *(const f32x4*)(xs + g);
         }
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
@@ -297,9 +356,15 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
           for (int jj = 0; jj < 4; ++jj) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float v = acc[rb][qb][jj * 4 + e];
+              // int8: the exact int32 sum times the two factors (three fp32
+              // roundings, five with the cosine's folded inverse norms)
+              float v;
+              if constexpr (EL == FILTER_I8)
+                v = (float)acc[rb][qb][jj * 4 + e] * (qsc[qb] * xsv[jj][e]);
+              else
+                v = acc[rb][qb][jj * 4 + e];
               float kk;
-              if constexpr (MODE == MODE_IP) {
+              if constexpr (MODE == MODE_IP || EL == FILTER_I8) {
                 kk = -v;
               } else if constexpr (MODE == MODE_L2) {
                 kk = l2_from_ip(qa[qb], xa[jj][e], v);
@@ -309,11 +374,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               key[jj * 4 + e] = kk;
             }
           }
-          // A list only ever sees rows in increasing order (tiles ascend within a
-          // split, blocks ascend within a tile, resumed lists hold earlier
-          // tiles), so against the entries present before this block the
-          // lexicographic admission (key, row) < (last key, last row) is just
-          // key < last key; list_insert keeps the full rule within the block.
+          // Admission against the list's last entry is key < last key (a row
+          // tied with it is left out even when its label is lower: the lists
+          // are candidate pools, and the verification only needs every row
+          // outside them to have an approximate key >= its list's final last
+          // entry, which this keeps); list_insert orders the admitted rows
+          // lexicographically.
           float m = key[0];
 #pragma unroll
           for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
@@ -326,14 +392,14 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
             } else {
 #pragma unroll
               for (int r = 0; r < 16; ++r) {
-                const int row = r0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int row = rowof(r >> 2) + (r & 3);
                 cm |= (uint32_t)(row < ntotal && row != selfrow[qb] && key[r] < last) << r;
               }
             }
             while (cm) {
               const int bi = __builtin_ctz(cm);
               cm &= cm - 1;
-              const int row = r0 + (bi & 3) + 8 * (bi >> 2) + 4 * h;
+              const int row = rowof(bi >> 2) + (bi & 3);
               list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
             }
           }
@@ -455,16 +521,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 }
 
-// LDS ring depth: VS_X1_NBUF=5 selects five images (A/B); default four.
-static int x1_nbuf() {
-  static const int v = [] {
-    const char* e = getenv("VS_X1_NBUF");
-    return e && atoi(e) == 5 ? 5 : 4;
-  }();
-  return v;
-}
-
-template <int KR, int MODE>
+template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
   const int nqt = a.nq_pad / kT;
@@ -475,16 +532,12 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
-  const bool five = x1_nbuf() == 5;
+  const int64_t ldb = a.ld * filter_bytes(EL);
   for (int c = 0; c < nchunk; ++c) {
-    if (five)
-      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 5>), dim3(nqt * a.nsplit), dim3(512), 0, st,
-                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
-                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
-    else
-      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 4>), dim3(nqt * a.nsplit), dim3(512), 0, st,
-                         a.XH, a.xaux, a.QH, a.qaux, a.nqa, a.ld, (int)(a.ld / 32), a.ntotal,
-                         ntiles, a.nsplit, nqt, a.self0, c, nchunk, part.KP, part.key, part.id);
+    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 4, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+                       (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
+                       ldb, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.self0, a.qrow,
+                       a.qcount, c, nchunk, part.KP, part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -494,23 +547,36 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
 
 int x1_lane_len() { return 8; }
 
+template <int EL>
+static hipError_t x1_dispatch(int mode, const X1Args& a, Partials part, hipStream_t st,
+                              int* ndispatch) {
+  switch (mode) {
+    case MODE_IP:
+      return x1_launch<8, MODE_IP, EL>(a, part, st, ndispatch);
+    case MODE_L2:
+      // int8: no L2 form (its key needs two per-row factors, which do not fit
+      // the registers beside the accumulators); L2 indexes hold the bf16 plane
+      if constexpr (EL == FILTER_I8) return hipErrorInvalidValue;
+      else return x1_launch<8, MODE_L2, EL>(a, part, st, ndispatch);
+    case MODE_COS:
+      return x1_launch<8, MODE_COS, EL>(a, part, st, ndispatch);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStream_t st,
                                int* ndispatch) {
-  // 32-element K-steps of plane rows padded to 128 B; 256-query tiles; the
+  // 64-B K-steps of plane rows padded to 64 elements; 256-query tiles; the
   // lists of a query are (split, row half, lane half)
   if (a.nq_pad % kT != 0 || a.ld % 64 != 0 || a.ld <= 0 || part.KP < x1_lane_len() ||
       part.P != 4 * a.nsplit || a.nsplit < 1 || a.ntotal <= 0)
     return hipErrorInvalidValue;
-  switch (mode) {
-    case MODE_IP:
-      return x1_launch<8, MODE_IP>(a, part, st, ndispatch);
-    case MODE_L2:
-      return x1_launch<8, MODE_L2>(a, part, st, ndispatch);
-    case MODE_COS:
-      return x1_launch<8, MODE_COS>(a, part, st, ndispatch);
-    default:
-      return hipErrorInvalidValue;
+  if (a.filter == FILTER_I8) {
+    if (!a.xs || !a.qs || a.ld > kI8MaxLd) return hipErrorInvalidValue;
+    return x1_dispatch<FILTER_I8>(mode, a, part, st, ndispatch);
   }
+  return x1_dispatch<FILTER_BF16>(mode, a, part, st, ndispatch);
 }
 
 // Filter-pass candidate count: the merged approximate candidates for `need`
@@ -547,9 +613,12 @@ __global__ __launch_bounds__(256) void bound_stats_kernel(const float* __restric
 }
 
 hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, unsigned* out,
-                              hipStream_t st) {
-  hipError_t e = hipMemsetAsync(out, 0, 3 * sizeof(unsigned), st);
-  if (e != hipSuccess || n <= 0) return e;
+                              hipStream_t st, bool accumulate) {
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(out, 0, 3 * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+  }
+  if (n <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>(1024, (n + 255) / 256);
   hipLaunchKernelGGL(bound_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, st, norms, rn2, n,
                      out);
@@ -592,8 +661,139 @@ hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n,
   return hipGetLastError();
 }
 
+// int8 plane: code = rint(x / s), s = max|x| / 127 per row, clamped to +-127
+// (a zero row has s = 0 and zero codes).  One wave per row: the row's maximum
+// and finiteness, then the codes (4 per lane-store) and, when rn2 is given, the
+// residual |x - s code|^2 in fp64 (s * code and x - s * code are exact there),
+// rounded up to float; a non-finite row gets rn2 = +inf, which makes every
+// bound non-finite (every query then goes to the exact engine).
+__global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restrict__ X, int64_t ld,
+                                                          int64_t r0, int64_t n,
+                                                          int8_t* __restrict__ codes,
+                                                          float* __restrict__ scale,
+                                                          float* __restrict__ rn2) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* xr = X + (r0 + row) * ld;
+  float m = 0.0f;
+  bool bad = false;
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bad |= !isfinite(v[i]);
+      m = fmaxf(m, fabsf(v[i]));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  bad = __any(bad);
+  const float s = bad ? 0.0f : m / 127.0f;
+  double acc = 0.0;
+  uint32_t* out = (uint32_t*)(codes + (r0 + row) * ld);
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int code = 0;
+      if (s > 0.0f) code = (int)fminf(fmaxf(rintf(v[i] / s), -127.0f), 127.0f);
+      packed |= (uint32_t)(code & 0xFF) << (8 * i);
+      const double r = (double)v[i] - (double)s * (double)code;
+      acc += r * r;
+    }
+    out[c >> 2] = packed;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) {
+    scale[r0 + row] = s;
+    if (rn2) {
+      float f = (float)acc;
+      if ((double)f < acc) f = nextafterf(f, INFINITY);
+      rn2[r0 + row] = bad ? INFINITY : f;
+    }
+  }
+}
+
+// Gathered batch of a later filter stage: slot s < *count takes query gl[s]
+// (its fp32 row of `src`, stride ld, and its aux value; self row self0 + gl[s]
+// when self0 >= 0); slots past the count are zero rows (aux 0, no self row).
+// One wave per slot.
+__global__ __launch_bounds__(256) void gather_queries_kernel(
+    const float* __restrict__ src, int64_t ld, const float* __restrict__ aux,
+    const int* __restrict__ gl, const int* __restrict__ count, int nslot, int64_t self0,
+    float* __restrict__ dst, float* __restrict__ daux, int* __restrict__ drow) {
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslot) return;
+  const bool on = s < *count;
+  const int q = on ? gl[s] : 0;
+  const f32x4* in = (const f32x4*)(src + (int64_t)q * ld);
+  f32x4* out = (f32x4*)(dst + (int64_t)s * ld);
+  for (int64_t c = lane; c < ld / 4; c += 64) out[c] = on ? in[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (lane == 0) {
+    if (daux) daux[s] = on && aux ? aux[q] : 0.0f;
+    if (drow) drow[s] = on && self0 >= 0 ? (int)(self0 + q) : -1;
+  }
+}
+
+hipError_t launch_gather_queries(const float* src, int64_t ld, const float* aux, const int* gl,
+                                 const int* count, int nslot, int64_t self0, float* dst,
+                                 float* daux, int* drow, hipStream_t st) {
+  if (nslot <= 0) return hipSuccess;
+  if (ld % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_queries_kernel, dim3((unsigned)((nslot + 3) / 4)), dim3(256), 0, st,
+                     src, ld, aux, gl, count, nslot, self0, dst, daux, drow);
+  return hipGetLastError();
+}
+
+// out[j] = outer[inner[j]] for j < *count (query ids of a gathered batch's
+// flagged slots), one thread per slot of a fixed grid.
+__global__ __launch_bounds__(256) void compose_list_kernel(const int* __restrict__ outer,
+                                                           const int* __restrict__ inner,
+                                                           const int* __restrict__ count, int n,
+                                                           int* __restrict__ out) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < n && j < *count) out[j] = outer[inner[j]];
+}
+
+hipError_t launch_compose_list(const int* outer, const int* inner, const int* count, int n,
+                               int* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(compose_list_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     outer, inner, count, n, out);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void mul_arrays_kernel(const float* __restrict__ a,
+                                                         const float* __restrict__ b, int64_t n,
+                                                         float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = a[i] * b[i];
+}
+
+hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* out,
+                             hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mul_arrays_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, b,
+                     n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
+                              float* scale, float* rn2, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ld % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(quantize_i8_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, ld, r0,
+                     n, codes, scale, rn2);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
-// Verification (engine VS_ENGINE_BF16_VERIFY).  With x = hi(x) + r(x) and
+// Verification (engines VS_ENGINE_I8_VERIFY / VS_ENGINE_BF16_VERIFY).  Written
+// for the bf16 plane; the int8 plane is the same argument with hi(.) the
+// dequantized row s * code and gam its three scaling roundings (the int32 sum is
+// exact), see make_bound_args.  With x = hi(x) + r(x) and
 // q = hi(q) + r(q) (bf16 round-to-nearest-even, residuals exact in fp32):
 //   x.q - hi(x).hi(q) = hi(x).r(q) + r(x).hi(q) + r(x).r(q)
 // and the MFMA sums ld exact products in fp32 (each add off by <= 1 ulp), so
@@ -624,21 +824,23 @@ __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, doubl
     b = 2.0 * b + 8.0 * ldexp(1.0, -24) * (qn2 + xm2);
   } else if (mode == MODE_COS) {
     // keys -(s qinv xinv) with qinv, xinv from the stored norms (relative error
-    // ~gam); |s_a - s_e| / (|x||q|) <= gam (1+rho)^2 + 2 rho (1+rho) + rho^2 +
-    // 2^-23, rho = max |r(x)| / |x| (the queries are stored rows); two roundings
+    // ~gam(ld) each, 1.5 norm_inf together); |s_a - s_e| / (|x||q|) <=
+    // gam (1+rho)^2 + 2 rho (1+rho) + rho^2 + 2^-23, rho = max |r(x)| / |x| (the queries are stored rows); two roundings
     // of a key of magnitude <= 1 add 2^-22
     const double rho = sqrt((double)__uint_as_float(stats[2]) * (1.0 + ba.norm_inf));
     const double rel = ba.gam * (1 + rho) * (1 + rho) + 2 * rho * (1 + rho) + rho * rho +
                        ldexp(1.0, -23);
-    b = (rel * (1.0 + 3.0 * ba.gam) + ldexp(1.0, -22)) * (1.0 + 1e-6);
+    b = (rel * (1.0 + 1.5 * ba.norm_inf) + ldexp(1.0, -22)) * (1.0 + 1e-6);
   }
   return b;
 }
 
-// the query's split norms |hi(q)|^2, |r(q)|^2, |q|^2 (fp64, across the wave)
+// the query's split norms |hi(q)|^2, |r(q)|^2, |q|^2 (fp64, across the wave);
+// int8 plane (qr2i8 = the query's stored residual norm, rounded up):
+// |hi(q)| <= |q| + |r(q)|
 __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow, int64_t ld,
-                                                  int lane, double& qh2, double& qr2,
-                                                  double& qn2) {
+                                                  int lane, const float* __restrict__ qr2i8,
+                                                  double& qh2, double& qr2, double& qn2) {
   double a = 0.0, r = 0.0, n = 0.0;
   for (int64_t c = lane * 4; c < ld; c += 256) {
     const f32x4 v = *(const f32x4*)(qrow + c);
@@ -660,6 +862,11 @@ __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow
   qh2 = a;
   qr2 = r;
   qn2 = n;
+  if (qr2i8) {
+    qr2 = (double)*qr2i8;
+    const double hq = sqrt(n) + sqrt(qr2);
+    qh2 = hq * hq;
+  }
 }
 
 // exact dot product of two fp32 rows (fp64 accumulation across the wave)
@@ -676,6 +883,50 @@ __device__ __forceinline__ double wave_dot(const float* __restrict__ x, const fl
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   return acc;
+}
+
+// The same sums for two rows at once against a query whose slice of this lane
+// sits in registers (ld <= 256 kQV): every load of both rows is issued before
+// the first FMA (one memory round trip per pair instead of one per 1 KB), and
+// each row's terms are added in wave_dot's order (identical results).
+constexpr int kQV = 8;
+struct QSlice {
+  f32x4 v[kQV];
+};
+__device__ __forceinline__ void load_qslice(const float* __restrict__ q, int64_t ld, int lane,
+                                            QSlice& qs) {
+#pragma unroll
+  for (int i = 0; i < kQV; ++i) {
+    const int64_t c = lane * 4 + 256 * i;
+    qs.v[i] = c < ld ? *(const f32x4*)(q + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+__device__ __forceinline__ void wave_dot2(const float* __restrict__ xa, const float* __restrict__ xb,
+                                          const QSlice& qs, int64_t ld, int lane, double& ra,
+                                          double& rb) {
+  f32x4 va[kQV], vb[kQV];
+#pragma unroll
+  for (int i = 0; i < kQV; ++i) {
+    const int64_t c = lane * 4 + 256 * i;
+    va[i] = c < ld ? *(const f32x4*)(xa + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    vb[i] = c < ld ? *(const f32x4*)(xb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int i = 0; i < kQV; ++i) {
+    if (lane * 4 + 256 * i >= ld) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a = fma((double)va[i][e], (double)qs.v[i][e], a);
+      b = fma((double)vb[i][e], (double)qs.v[i][e], b);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+  }
+  ra = a;
+  rb = b;
 }
 
 template <int MODE>
@@ -699,10 +950,15 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
-    const float* __restrict__ qinv, const float* __restrict__ xinv) {
+    const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8,
+    const int* __restrict__ qcount) {
   __shared__ float ek[64];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
+  if (qcount && q >= *qcount) {  // gathered batch: slots past the count are not flagged
+    if (lane == 0) fail[q] = 0;
+    return;
+  }
   const float a = lane < KF ? Dk[(int64_t)q * KF + lane] : FLT_MAX;
   const int id = lane < KF ? (int)Ik[(int64_t)q * KF + lane] : -1;
   const float aK = __shfl(a, KF - 1);
@@ -724,15 +980,29 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
 
   const float* qrow = Q + (int64_t)q * ld;
   double qh2, qr2, qn2;
-  query_split_norms(qrow, ld, lane, qh2, qr2, qn2);
-  for (int j = 0; j < KF; ++j) {
-    const int r = __shfl(id, j);
-    if (r < 0) {
-      if (lane == 0) ek[j] = FLT_MAX;
-      continue;
+  query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2);
+  if (ld <= 256 * kQV) {  // two candidates per step, the query in registers
+    QSlice qsl;
+    load_qslice(qrow, ld, lane, qsl);
+    for (int j = 0; j < KF; j += 2) {
+      const int ra = __shfl(id, j), rb = j + 1 < KF ? __shfl(id, j + 1) : -1;
+      double da, db;
+      wave_dot2(X + (int64_t)max(ra, 0) * ld, X + (int64_t)max(rb, 0) * ld, qsl, ld, lane, da, db);
+      if (lane == 0) {
+        ek[j] = ra < 0 ? FLT_MAX : exact_key<MODE>((float)da, q, ra, qn, xn, qinv, xinv);
+        if (j + 1 < KF) ek[j + 1] = rb < 0 ? FLT_MAX : exact_key<MODE>((float)db, q, rb, qn, xn, qinv, xinv);
+      }
     }
-    const double acc = wave_dot(X + (int64_t)r * ld, qrow, ld, lane);
-    if (lane == 0) ek[j] = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
+  } else {
+    for (int j = 0; j < KF; ++j) {
+      const int r = __shfl(id, j);
+      if (r < 0) {
+        if (lane == 0) ek[j] = FLT_MAX;
+        continue;
+      }
+      const double acc = wave_dot(X + (int64_t)r * ld, qrow, ld, lane);
+      if (lane == 0) ek[j] = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
+    }
   }
   __syncthreads();
   // rank sort of (key, row); empty slots last, in lane order among themselves
@@ -768,7 +1038,7 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
                                  const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st, const float* qinv,
-                                 const float* xinv) {
+                                 const float* xinv, const float* qr2i8, const int* qcount) {
   if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
       L > lists.KP)
     return hipErrorInvalidValue;
@@ -776,7 +1046,7 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
 #define VS_VERIFY(MD)                                                                             \
   hipLaunchKernelGGL(verify_rescore_kernel<MD>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, X, xn, \
                      Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey, oid,  \
-                     KP, fail, qinv, xinv)
+                     KP, fail, qinv, xinv, qr2i8, qcount)
   if (mode == MODE_IP)
     VS_VERIFY(MODE_IP);
   else if (mode == MODE_L2)
@@ -827,6 +1097,18 @@ __global__ __launch_bounds__(1024) void compact_flags_kernel(const int* __restri
   }
 }
 
+// acc[0] += n, acc[1] += *count (one thread; a per-index record of a stage)
+__global__ void add_counts_kernel(const int* __restrict__ count, int n,
+                                  unsigned long long* __restrict__ acc) {
+  acc[0] += (unsigned long long)n;
+  acc[1] += (unsigned long long)*count;
+}
+
+hipError_t launch_add_counts(const int* count, int n, unsigned long long* acc, hipStream_t st) {
+  hipLaunchKernelGGL(add_counts_kernel, dim3(1), dim3(1), 0, st, count, n, acc);
+  return hipGetLastError();
+}
+
 hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
                                 unsigned long long* total, unsigned long long* total_n,
                                 hipStream_t st) {
@@ -852,7 +1134,7 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
-    const float* __restrict__ qinv, const float* __restrict__ xinv) {
+    const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8) {
   __shared__ float ck[kWideCap];
   __shared__ int cid[kWideCap];
   __shared__ float wT[4];
@@ -888,7 +1170,7 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     const float* qrow = Q + (int64_t)q * ld;
     if (wv == 0) {
       double a, b, c;
-      query_split_norms(qrow, ld, lane, a, b, c);
+      query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, a, b, c);
       if (lane == 0) {
         qs[0] = a;
         qs[1] = b;
@@ -910,13 +1192,27 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     __syncthreads();
     const int n = cnt;
     if (!(n > kWideCap || n < M || !isfinite(T))) {  // uniform
-      for (int j = wv; j < n; j += 4) {
-        const int r = cid[j];
-        const double acc = wave_dot(X + (int64_t)r * ld, qrow, ld, lane);
+      auto put = [&](int j, int r, double acc) {
         if (lane == 0) {
           const float key = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
           ck[j] = key;
           if (!isfinite(key)) bad = 1;
+        }
+      };
+      if (ld <= 256 * kQV) {  // two rows per wave step, the query in registers
+        QSlice qsl;
+        load_qslice(qrow, ld, lane, qsl);
+        for (int j = wv; j < n; j += 8) {
+          const int ra = cid[j], rb = j + 4 < n ? cid[j + 4] : ra;
+          double da, db;
+          wave_dot2(X + (int64_t)ra * ld, X + (int64_t)rb * ld, qsl, ld, lane, da, db);
+          put(j, ra, da);
+          if (j + 4 < n) put(j + 4, rb, db);
+        }
+      } else {
+        for (int j = wv; j < n; j += 4) {
+          const int r = cid[j];
+          put(j, r, wave_dot(X + (int64_t)r * ld, qrow, ld, lane));
         }
       }
       __syncthreads();
@@ -957,14 +1253,14 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
-                              const float* xinv) {
+                              const float* xinv, const float* qr2i8) {
   if (KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
   if (nq_max <= 0) return hipSuccess;
-  const int grid = std::min(nq_max, 512);
+  const int grid = std::min(nq_max, 2048);
 #define VS_WIDE(MD)                                                                               \
   hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(grid), dim3(256), 0, st, qlist, count, KF, M, X, \
                      xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey,   \
-                     oid, KP, fail, qinv, xinv)
+                     oid, KP, fail, qinv, xinv, qr2i8)
   if (mode == MODE_IP)
     VS_WIDE(MODE_IP);
   else if (mode == MODE_L2)
@@ -977,13 +1273,22 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
   return hipGetLastError();
 }
 
-// Bound constants for `ld` K elements (see above).
-BoundArgs make_bound_args(int64_t ld) {
+// Bound constants for `ld` K elements (see above).  bf16: the MFMA's fp32
+// accumulation.  int8: the int32 sum is exact (|code| <= 127, ld <= kI8MaxLd),
+// and the approximate score fl(fl(float(sum)) * fl(f_q * f_x)) carries three
+// roundings for IP (f = s), five for the cosine (f = fl(s * inverse norm)), so
+// approx = hi(x).hi(q) (1 + d), |d| <= (1 + 2^-24)^5 - 1 < 6 * 2^-24; for the
+// cosine the key then needs no further rounding term (the 2^-22 kept below is
+// slack).
+BoundArgs make_bound_args(int64_t ld, int filter) {
   BoundArgs ba;
+  ba.filter = filter;
   const double u = std::ldexp(1.0, -23);
   const double n = (double)ld + 1.0;
-  ba.gam = n * u / (1.0 - n * u);
-  ba.norm_inf = 2.0 * ba.gam;  // fp32 norm sums undercount by at most ~gam(ld) u/2-based
+  ba.gam = filter == FILTER_I8 ? 6.0 * std::ldexp(1.0, -24) : n * u / (1.0 - n * u);
+  // the stored norms are fp32 sums of ld squares: they undercount by at most
+  // ~gam(ld), whatever the plane
+  ba.norm_inf = 2.0 * (n * u / (1.0 - n * u));
   return ba;
 }
 

@@ -72,12 +72,20 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,
                               int ntotal, int nblocks, Partials part, hipStream_t st);
-// The filter pass of the filter-and-verify engine (vs_gemm_x1.hip): one bf16
-// MFMA product per fp32 product over the bf16 (RNE) planes of rows and queries.
+// The filter pass of the filter-and-verify engine (vs_gemm_x1.hip): one MFMA
+// product per fp32 product over a low-precision "filter plane" of rows and
+// queries: bf16 (RNE) on v_mfma_f32_32x32x16_bf16, or int8 with one fp32 scale
+// per row (code = rint(x / s), s = max|x| / 127) on v_mfma_i32_32x32x32_i8
+// (twice the bf16 rate, exact int32 sums, half the bytes per element).
+enum Filter : int { FILTER_BF16 = 0, FILTER_I8 = 1 };
+inline int filter_bytes(int filter) { return filter == FILTER_I8 ? 1 : 2; }
 struct X1Args {
-  const uint16_t* XH = nullptr;  // database hi plane [capacity][ld] (row-major)
+  int filter = FILTER_BF16;
+  const void* XH = nullptr;      // database plane [capacity][ld] (row-major)
+  const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
-  const uint16_t* QH = nullptr;  // query hi plane [nq_pad][ld] (self-join: stored rows)
+  const void* QH = nullptr;      // query plane [nq_pad][ld] (self-join: stored rows)
+  const float* qs = nullptr;     // int8: per-query factor s_q (IP) or s_q / |q| (COS)
   const float* qaux = nullptr;   // per-query aux, nqa entries (padding queries read 0)
   int nqa = 0;
   int64_t ld = 0;                // elements per row, a multiple of 64
@@ -85,8 +93,12 @@ struct X1Args {
   int nq_pad = 0;                // multiple of kX1Q
   int nsplit = 1;
   int64_t self0 = -1;
+  const int* qrow = nullptr;     // per-query excluded row (-1 none), else self0 + q
+  const int* qcount = nullptr;   // gathered batch: device-side query count
 };
 constexpr int kX1Q = 256;  // queries (and database rows) per x1 tile
+// int8 sums stay exact in int32 up to this many elements per row.
+constexpr int64_t kI8MaxLd = 131072;
 // Candidates merged from the lane lists for `need` exact entries (24, 32 or 64;
 // 0 = not served by the filter engine).
 int x1_list_len(int need);
@@ -98,26 +110,51 @@ hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStre
                                int* ndispatch);
 // Bound constants of the verification (vs_gemm_x1.hip).
 struct BoundArgs {
-  double gam = 0.0;       // fp32 accumulation of ld + 1 terms: n u / (1 - n u), u = 2^-23
+  int filter = FILTER_BF16;
+  double gam = 0.0;       // relative error of the filter's own arithmetic (bf16: fp32
+                          // accumulation of ld + 1 terms, n u / (1 - n u), u = 2^-23;
+                          // int8: exact int32 sum, three fp32 roundings of the scaling)
   double norm_inf = 0.0;  // relative undercount of the stored fp32 norms
 };
-BoundArgs make_bound_args(int64_t ld);
+BoundArgs make_bound_args(int64_t ld, int filter);
 // out[0..3) = bits of max norms, max rn2, max rn2/norms over rows [0, n).
+// accumulate: fold rows [0, n) into the maxima already in out (no reset).
 hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, unsigned* out,
-                              hipStream_t st);
+                              hipStream_t st, bool accumulate = false);
 // rn2[r] = |x_r - bf16_rne(x_r)|^2 (rounded up) for fp32 rows [r0, r0+n).
 hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
                               hipStream_t st);
+// int8 filter plane of fp32 rows [r0, r0+n) (stride ld): codes (int8, stride
+// ld), scale[r] = max|x_r| / 127 and, when rn2 != nullptr, rn2[r] = |x_r - scale
+// * code_r|^2 rounded up (+inf for a row with a non-finite element).
+hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
+                              float* scale, float* rn2, hipStream_t st);
+// A later filter stage's gathered batch: dst[s] = src[gl[s]] (rows of stride
+// ld), daux[s] = aux[gl[s]], drow[s] = self0 + gl[s] (or -1) for s < *count,
+// zero rows / 0 / -1 for the other slots of [0, nslot).
+hipError_t launch_gather_queries(const float* src, int64_t ld, const float* aux, const int* gl,
+                                 const int* count, int nslot, int64_t self0, float* dst,
+                                 float* daux, int* drow, hipStream_t st);
+// acc[0] += n, acc[1] += *count.
+hipError_t launch_add_counts(const int* count, int n, unsigned long long* acc, hipStream_t st);
+// out[j] = outer[inner[j]] for j < *count (j < n).
+hipError_t launch_compose_list(const int* outer, const int* inner, const int* count, int n,
+                               int* out, hipStream_t st);
+// out[i] = a[i] * b[i] (the int8 cosine's folded factors s / |x|).
+hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* out,
+                             hipStream_t st);
 // Checks and rescores the filter candidates: Dk/Ik hold the KF best approximate
 // keys of each query (ascending, local rows), `lists` the filter pass's lane
 // lists (L entries each) for their floors; writes sorted exact lists of KP
 // entries (okey/oid) and fail[q] = 1 where the exact engine must redo query q.
+// qsc: the queries' int8 scales (int8 filter; null for bf16).
 hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
                                  const int64_t* Ik, const float* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
                                  const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st,
-                                 const float* qinv = nullptr, const float* xinv = nullptr);
+                                 const float* qinv, const float* xinv, const float* qsc,
+                                 const int* qcount = nullptr);
 // Flagged queries (flags[i] != 0) -> ascending qlist[0 .. *count), all on the
 // device; *total += count and *total_n += n when not null.
 hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
@@ -127,13 +164,13 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // grid): every lane-list entry below the smallest full-list floor is rescored
 // exactly (up to kWideCap per query) and the condition re-checked on that wider
 // set; passing queries get their sorted exact list in okey/oid and fail[q] = 0.
-constexpr int kWideCap = 1024;
+constexpr int kWideCap = 2048;
 hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
                               int M, const float* X, const float* xn, const float* Q,
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
-                              int KP, int* fail, hipStream_t st, const float* qinv = nullptr,
-                              const float* xinv = nullptr);
+                              int KP, int* fail, hipStream_t st, const float* qinv,
+                              const float* xinv, const float* qsc);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
 // (key, label) order, the per-shard half of an exact sharded merge).  With

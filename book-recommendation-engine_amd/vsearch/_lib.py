@@ -26,6 +26,7 @@ MAX_K = 64
 ENGINE_AUTO = 0
 ENGINE_FP32_MFMA = 1
 ENGINE_BF16_VERIFY = 3
+ENGINE_I8_VERIFY = 4
 
 E_INVALID = -1
 E_HIP = -2
@@ -56,6 +57,7 @@ SIGNATURES = {
     "vs_dtype": (_c_int, [_vp, ctypes.POINTER(_c_int)]),
     "vs_set_id_base": (_c_int, [_vp, _c_i64]),
     "vs_set_engine": (_c_int, [_vp, _c_int]),
+    "vs_filter_plane": (_c_int, [_vp, ctypes.POINTER(_c_int)]),
     "vs_search": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
     "vs_reconstruct_n": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp]),
     "vs_remove_ids": (_c_int, [_vp, _vp, _c_i64, _i64p]),
@@ -72,8 +74,10 @@ SIGNATURES = {
     "vs_timer_reset": (_c_int, []),
     "vs_timer_read": (_c_int, [ctypes.POINTER(ctypes.c_double), _i64p]),
     "vs_timer_kernel": (ctypes.c_char_p, []),
+    "vs_timer_read_kernel": (_c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i64p]),
     "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
     "vs_filter_wide_stats": (_c_int, [_i64p]),
+    "vs_filter_second_stats": (_c_int, [_i64p]),
 }
 
 _lock = threading.Lock()
@@ -177,6 +181,14 @@ def timer_read():
     return ms.value, n.value
 
 
+def timer_read_kernel(name: str):
+    """(summed kernel ms, launches) of the timed spans named `name`."""
+    ms = ctypes.c_double(0.0)
+    n = ctypes.c_int64(0)
+    check(load().vs_timer_read_kernel(name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value
+
+
 def filter_stats(reset: bool = False):
     """(queries searched by the filter-and-verify engine, queries the exact
     engine redid) since the last reset."""
@@ -192,3 +204,11 @@ def filter_wide_stats() -> int:
     w = ctypes.c_int64(0)
     check(load().vs_filter_wide_stats(ctypes.byref(w)))
     return w.value
+
+
+def filter_second_stats() -> int:
+    """Queries handed from the int8 plane to the bf16 plane by the staged
+    filter engine since the last filter_stats reset (read it before that reset)."""
+    v = ctypes.c_int64(0)
+    check(load().vs_filter_second_stats(ctypes.byref(v)))
+    return v.value

@@ -190,12 +190,22 @@ class IndexFlat(Index):
         return int(nrem.value)
 
     def set_engine(self, engine: str) -> None:
-        """Large-batch arithmetic of fp32 indexes: "auto", "fp32" (the exact fp32
-        MFMA engine) or "bf16v" (one-product bf16 filter pass + rigorous bound +
-        exact rescoring, the default where it applies)."""
+        """Large-batch arithmetic of fp32 indexes: "auto" (filter and verify in
+        stages: the int8 plane, then the bf16 plane for what int8 cannot settle,
+        then the exact fp32 engine), "fp32" (the exact fp32 MFMA engine), "i8v"
+        or "bf16v" (filter and verify on that plane alone, then fp32)."""
         code = {"auto": _lib.ENGINE_AUTO, "fp32": _lib.ENGINE_FP32_MFMA,
-                "bf16v": _lib.ENGINE_BF16_VERIFY}[engine]
+                "bf16v": _lib.ENGINE_BF16_VERIFY, "i8v": _lib.ENGINE_I8_VERIFY}[engine]
         _lib.check(self._lib.vs_set_engine(self._h, code), "vs_set_engine")
+
+    @property
+    def filter_planes(self):
+        """The filter planes of this index, in the order the staged engine runs
+        them: ("i8", "bf16") for inner-product fp32 indexes, ("bf16",) for L2,
+        () for bf16 indexes (which search their stored values exactly)."""
+        v = ctypes.c_int(0)
+        _lib.check(self._lib.vs_filter_plane(self._h, ctypes.byref(v)), "vs_filter_plane")
+        return tuple(n for bit, n in ((1, "i8"), (2, "bf16")) if v.value & bit)
 
     def set_id_base(self, base: int) -> None:
         _lib.check(self._lib.vs_set_id_base(self._h, int(base)), "vs_set_id_base")

@@ -107,22 +107,39 @@ int vs_metric(const vs_index* idx, int* out);
 int vs_dtype(const vs_index* idx, int* out);
 
 /* Arithmetic engine of the large-batch path of fp32 indexes:
- *   VS_ENGINE_AUTO          library default: BF16_VERIFY where it applies (IP
- *                           k <= 28, L2 / cosine k <= 56), else FP32_MFMA;
- *                           env VS_ENGINE=fp32|bf16v overrides
+ *   VS_ENGINE_AUTO          library default where it applies (IP k <= 28, L2 /
+ *                           cosine k <= 56), else FP32_MFMA: filter and verify
+ *                           in stages over the index's filter planes — int8
+ *                           (inner product and cosine), then bf16 for the
+ *                           queries the int8 bound cannot settle, then the exact
+ *                           FP32_MFMA for what remains;
+ *                           env VS_ENGINE=fp32|bf16v|i8v overrides
  *   VS_ENGINE_FP32_MFMA     v_mfma_f32_32x32x2_f32 on the fp32 rows
- *   VS_ENGINE_BF16_VERIFY   filter and verify: one bf16 MFMA product per fp32
- *                           product (bf16 copies of rows and queries) keeps the
- *                           best candidates of every query, a rigorous error bound
+ *   VS_ENGINE_I8_VERIFY     filter and verify on the int8 plane alone: one int8
+ *                           MFMA product per fp32 product (int8 codes of rows
+ *                           and queries, one scale per row) keeps the best
+ *                           candidates of every query, a rigorous error bound
  *                           proves the exact top-k is among them, the candidates
  *                           are rescored exactly, and queries the bound cannot
  *                           settle are redone by FP32_MFMA — results identical to
  *                           an exact engine
- * bf16 indexes ignore it (bf16 MFMA on the stored values). */
+ *   VS_ENGINE_BF16_VERIFY   the same on the bf16 (round-to-nearest-even) plane
+ * New fp32 indexes hold the int8 plane (inner product) and the bf16 plane;
+ * env VS_FILTER=bf16|i8 at creation keeps one.  bf16 indexes ignore the
+ * setting (bf16 MFMA on the stored values). */
 #define VS_ENGINE_AUTO 0
 #define VS_ENGINE_FP32_MFMA 1
 #define VS_ENGINE_BF16_VERIFY 3
+#define VS_ENGINE_I8_VERIFY 4
 int vs_set_engine(vs_index* idx, int engine);
+
+/* The filter planes an fp32 index holds, a bit set: VS_FILTER_I8 (int8 codes +
+ * per-row scale; inner-product indexes) | VS_FILTER_BF16; 0 for bf16 indexes.
+ * Library-specific (faiss has no counterpart); the benchmark reads it to price
+ * the filter pass. */
+#define VS_FILTER_I8 1
+#define VS_FILTER_BF16 2
+int vs_filter_plane(const vs_index* idx, int* out);
 
 /* Rows [0,ntotal) get labels id_base + row.  Used by the row-sharded multi-GPU
  * index so that per-shard results carry global faiss labels. */
@@ -193,8 +210,14 @@ int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset);
  * lane-list entry below the list floors rescored) examined again, since the last
  * vs_filter_stats reset.  Diagnostic only: no reference interface. */
 int vs_filter_wide_stats(int64_t* wide);
+/* Queries the staged engine handed from the int8 plane to the bf16 plane since
+ * the last vs_filter_stats reset.  Diagnostic only: no reference interface. */
+int vs_filter_second_stats(int64_t* second);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
+/* The same for the spans of one kernel name only (the filter engine's first
+ * stage is "gemm_topk_x1_i8" or "gemm_topk_x1" (bf16) per search). */
+int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches);
 /* Name of the fused search kernel the last search launched ("gemm_topk_x1",
  * "gemm_topk", "skinny_topk" or "gemv_topk"). */
 const char* vs_timer_kernel(void);

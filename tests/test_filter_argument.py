@@ -90,3 +90,89 @@ def test_wide_check_rejects_a_list_full_of_ties():
     wide = [r for r in entries if a[r] < floor]
     ok, _ = _accept(wide, floor, e, B, 19)
     assert not ok
+
+
+# ---------------------------------------------------------------------------
+# The int8 filter plane's bound (vs_gemm_x1.hip quantize_i8_kernel,
+# bound_key, make_bound_args): codes c = rint(x / s) clamped to +-127 with one
+# fp32 scale s = max|x| / 127 per row; the kernel's approximate inner product is
+# fl(fl(float(c_q . c_x)) * fl(s_q * s_x)) (exact int32 sum).  This restates
+# the arithmetic in numpy (fp32 where the kernel is fp32) and checks
+# |approx - x.q| <= B for every (query, row) pair, including rows with outliers,
+# tiny and zero rows, and the cosine form with folded inverse norms.
+
+_U = 2.0 ** -24
+_GAM_I8 = 6.0 * _U
+
+
+def _quantize_i8(x):
+    x = np.asarray(x, np.float32)
+    m = np.abs(x).max(axis=1)
+    s = (m / np.float32(127.0)).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        c = np.where(s[:, None] > 0, np.rint(x / s[:, None]), 0.0)
+    c = np.clip(c, -127, 127).astype(np.int64)
+    r = x.astype(np.float64) - s[:, None].astype(np.float64) * c
+    rn2 = np.nextafter((r * r).sum(axis=1).astype(np.float32), np.float32(np.inf))
+    return c, s, rn2
+
+
+def _rows(rng, n, d):
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    x[1] = 0.0                                     # zero row
+    x[2] *= 1e-30                                  # tiny row
+    x[3, 5] = 40.0                                 # one outlier element
+    x[4] = rng.standard_normal(d).astype(np.float32) / np.sqrt(d)  # embedding-like
+    x[5, :] = 0.0
+    x[5, 0] = 1.0                                  # one-hot
+    return x
+
+
+def test_int8_filter_bound_holds_for_inner_product():
+    rng = np.random.default_rng(11)
+    d = 1536
+    x = _rows(rng, 64, d)
+    q = _rows(rng, 16, d)
+    cx, sx, rx2 = _quantize_i8(x)
+    cq, sq, rq2 = _quantize_i8(q)
+    dot = (cq @ cx.T).astype(np.int64)
+    assert np.abs(dot).max() < 2 ** 31
+    f = (sq[:, None] * sx[None, :]).astype(np.float32)
+    approx = (dot.astype(np.float32) * f).astype(np.float64)
+    exact = q.astype(np.float64) @ x.astype(np.float64).T
+    xn = np.linalg.norm(x.astype(np.float64), axis=1)
+    qn = np.linalg.norm(q.astype(np.float64), axis=1)
+    rx = np.sqrt(rx2.astype(np.float64))
+    rq = np.sqrt(rq2.astype(np.float64))
+    hx = xn + rx
+    hq = qn + rq
+    B = (_GAM_I8 * np.outer(hq, hx) + np.outer(rq, hx) + np.outer(hq, rx) + np.outer(rq, rx)
+         + 2 * _U * np.outer(qn, xn)) * (1 + 1e-6)
+    err = np.abs(approx - exact)
+    assert (err <= B).all(), float((err - B).max())
+    # the bound is not vacuous: for uniform rows it is a few per mille of |x||q|
+    assert np.median(B[6:, 6:] / np.outer(qn[6:], xn[6:])) < 0.01
+
+
+def test_int8_filter_bound_holds_for_cosine():
+    rng = np.random.default_rng(12)
+    d = 768
+    x = _rows(rng, 80, d)
+    # the cosine ranks no zero-norm rows (their inverse norm is infinite)
+    x[1] = rng.uniform(-1, 1, d)
+    x[2] = rng.uniform(-1, 1, d) * 1e-3
+    cx, sx, rx2 = _quantize_i8(x)
+    xn2 = (x.astype(np.float32) ** 2).sum(axis=1, dtype=np.float32)
+    xinv = (1.0 / np.sqrt(xn2.astype(np.float64))).astype(np.float32)
+    fx = (sx * xinv).astype(np.float32)                 # folded s / |x|
+    dot = cx @ cx.T
+    key_a = -((dot.astype(np.float32) * (fx[:, None] * fx[None, :]).astype(np.float32))
+              .astype(np.float32)).astype(np.float64)
+    ip = (x.astype(np.float64) @ x.astype(np.float64).T).astype(np.float32)
+    key_e = -((ip * xinv[:, None]).astype(np.float32) * xinv[None, :]).astype(np.float64)
+    rho = np.sqrt((rx2.astype(np.float64) / xn2.astype(np.float64)).max())
+    gam_ld = (d + 1) * 2.0 ** -23 / (1 - (d + 1) * 2.0 ** -23)
+    norm_inf = 2 * gam_ld
+    rel = _GAM_I8 * (1 + rho) ** 2 + 2 * rho * (1 + rho) + rho ** 2 + 2.0 ** -23
+    b = (rel * (1 + 1.5 * norm_inf) + 2.0 ** -22) * (1 + 1e-6)
+    assert (np.abs(key_a - key_e) <= b).all(), float(np.abs(key_a - key_e).max() - b)

@@ -25,6 +25,11 @@ def vf():
     return vfaiss
 
 
+# Filter-and-verify planes: int8 (the default of inner-product indexes) and
+# bf16; the int8 filter has no L2 form (L2 indexes hold the bf16 plane).
+FILTER_CASES = [(L2, "bf16v"), (IP, "bf16v"), (IP, "i8v")]
+
+
 def _rand(n, d, seed, kind="normal"):
     rng = np.random.default_rng(seed)
     if kind == "normal":
@@ -174,8 +179,9 @@ def test_selfjoin_random(vf, k):
     np.testing.assert_allclose(S[ok], Sr[ok], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("engine", ["i8v", "bf16v"])
 @pytest.mark.parametrize("k", [10, 50])
-def test_selfjoin_filter_fallback_drops_self(vf, k):
+def test_selfjoin_filter_fallback_drops_self(vf, k, engine):
     """Cosine self-join through the filter engine with 40-fold duplicated rows: the
     tied candidates cannot be separated by the bound, those students are redone
     as plain searches for k + 1 and lose their own row; parity with the oracle."""
@@ -184,7 +190,7 @@ def test_selfjoin_filter_fallback_drops_self(vf, k):
     base = _rand(30, 96, 72)
     x = np.concatenate([np.repeat(base, 40, axis=0), _rand(600, 96, 73)])
     index = vf.IndexFlatIP(96)
-    index.set_engine("bf16v")
+    index.set_engine(engine)
     index.add(x)
     _lib.filter_stats(reset=True)
     S, I = index.selfjoin(k)
@@ -391,8 +397,7 @@ def test_small_batch_ragged_rows(vf, metric):
             _check(vf, xb, _rand(nq, 64, 33), 8, metric)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "bf16v"])
-@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("metric,engine", [(L2, "fp32"), (IP, "fp32")] + FILTER_CASES)
 def test_large_batch_engines(vf, engine, metric):
     """Every large-batch engine of fp32 indexes meets the fp32 tolerance."""
     xb = _rand(9000, 1536, 40) * 0.05
@@ -407,16 +412,16 @@ def test_large_batch_engines(vf, engine, metric):
         assert not bad, (engine, k, bad[:5])
 
 
-@pytest.mark.parametrize("metric", [L2, IP])
+@pytest.mark.parametrize("metric,engine", FILTER_CASES)
 @pytest.mark.parametrize("d", [64, 128, 192, 96, 160, 1536])
-def test_filter_step_shapes(vf, metric, d):
+def test_filter_step_shapes(vf, metric, engine, d):
     """The filter pass walks K in 64-element steps of the zero-padded rows (d = 96
     and 160 pad to 128 and 192); several tiles, a ragged last tile and a ragged
     query tile."""
     xb = _rand(1800, d, 46)
     xq = _rand(300, d, 47)
     index = vf.IndexFlat(d, metric)
-    index.set_engine("bf16v")
+    index.set_engine(engine)
     index.add(xb)
     for k in (1, 10):
         D, I = index.search(xq, k)
@@ -425,13 +430,15 @@ def test_filter_step_shapes(vf, metric, d):
         assert not bad, (d, k, bad[:5])
 
 
-def test_filter_plane_follows_mutations(vf):
-    """The bf16 plane and residual norms follow add / remove_ids / reset /
-    storage growth (they are kept in step with the rows, never rebuilt lazily)."""
+@pytest.mark.parametrize("engine", ["i8v", "bf16v"])
+def test_filter_plane_follows_mutations(vf, engine):
+    """The filter plane (codes, scales) and residual norms follow add /
+    remove_ids / reset / storage growth (kept in step with the rows, never
+    rebuilt lazily)."""
     xb = _rand(3000, 96, 42)
     xq = _rand(150, 96, 43)
     index = vf.IndexFlatIP(96)
-    index.set_engine("bf16v")
+    index.set_engine(engine)
     index.add(xb[:2000])
     D, I = index.search(xq, 10)
     for i0 in range(2000, 3000, 250):  # several growths
@@ -452,7 +459,7 @@ def test_filter_plane_follows_mutations(vf):
     assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "bf16v"])
+@pytest.mark.parametrize("engine", ["fp32", "bf16v", "i8v"])
 def test_selfjoin_engines(vf, engine):
     x = _rand(2000, 256, 44)
     index = vf.IndexFlatIP(256)
@@ -466,15 +473,15 @@ def test_selfjoin_engines(vf, engine):
     np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("metric", [L2, IP])
-def test_filter_ragged_shapes(vf, metric):
+@pytest.mark.parametrize("metric,engine", FILTER_CASES)
+def test_filter_ragged_shapes(vf, metric, engine):
     """Odd d (column padding), ragged row tiles, several query tiles per split,
     fewer rows than one tile."""
     for n, d, nq in ((5000, 100, 1000), (257, 1536, 129), (70001, 32, 256), (40, 64, 300)):
         xb = _rand(n, d, 45)
         xq = _rand(nq, d, 46)
         index = vf.IndexFlat(d, metric)
-        index.set_engine("bf16v")
+        index.set_engine(engine)
         index.add(xb)
         for k in (5, 10):
             D, I = index.search(xq, k)
@@ -483,14 +490,15 @@ def test_filter_ragged_shapes(vf, metric):
             assert not bad, (n, d, nq, k, bad[:5])
 
 
-def test_filter_repeatable(vf):
+@pytest.mark.parametrize("engine", ["i8v", "bf16v"])
+def test_filter_repeatable(vf, engine):
     """Race screen for the double-buffered LDS-DMA pipeline and the chunked
     launches: repeated searches over a corpus large enough to keep every CU busy
     give identical, correct lists."""
     xb = _rand(120000, 256, 47)
     xq = _rand(640, 256, 48)
     index = vf.IndexFlatIP(256)
-    index.set_engine("bf16v")
+    index.set_engine(engine)
     index.add(xb)
     D0, I0 = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
@@ -501,12 +509,13 @@ def test_filter_repeatable(vf):
         np.testing.assert_array_equal(D, D0)
 
 
-def test_filter_selfjoin_offsets(vf):
-    """Self-join query tiles taken from the index's own bf16 plane at an offset,
-    with and without self exclusion."""
+@pytest.mark.parametrize("engine", ["i8v", "bf16v"])
+def test_filter_selfjoin_offsets(vf, engine):
+    """Self-join query tiles taken from the index's own filter plane at an
+    offset, with and without self exclusion."""
     x = _rand(3000, 128, 49)
     index = vf.IndexFlatIP(128)
-    index.set_engine("bf16v")
+    index.set_engine(engine)
     index.add(x)
     Sr, Ir = flat.pgvector_cosine_topk(x, 12)
     S, I = index.selfjoin(12, q0=1000, nq=700)
@@ -517,8 +526,8 @@ def test_filter_selfjoin_offsets(vf):
     assert (I2[:, 0] == np.arange(5, 305)).mean() > 0.99  # a row is its own best match
 
 
-@pytest.mark.parametrize("metric", [L2, IP])
-def test_filter_matches_exact_engine(vf, metric):
+@pytest.mark.parametrize("metric,engine", FILTER_CASES)
+def test_filter_matches_exact_engine(vf, metric, engine):
     """The filter-and-verify engine returns the exact lists: oracle parity (ids
     equal except documented ties) and the fp32 engine's ids on (nearly) every row
     — the two round their fp32 scores differently, so an exact near-tie may order
@@ -530,7 +539,7 @@ def test_filter_matches_exact_engine(vf, metric):
     for k in (1, 4, 10, 12, 16, 28):
         index.set_engine("fp32")
         De, Ie = index.search(xq, k)
-        index.set_engine("bf16v")
+        index.set_engine(engine)
         D, I = index.search(xq, k)
         Dr, Ir = flat.knn_exact(xb, xq, k, metric)
         bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
@@ -539,8 +548,8 @@ def test_filter_matches_exact_engine(vf, metric):
         np.testing.assert_allclose(D, De, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("metric", [L2, IP])
-def test_filter_falls_back_on_ties(vf, metric):
+@pytest.mark.parametrize("metric,engine", FILTER_CASES)
+def test_filter_falls_back_on_ties(vf, metric, engine):
     """Duplicated rows tie exactly, so the bound cannot separate the candidates:
     those queries are redone by the exact engine (on the device, gathered by a
     device-side list), and the results keep oracle parity."""
@@ -550,7 +559,7 @@ def test_filter_falls_back_on_ties(vf, metric):
     xb = np.concatenate([np.repeat(base[:20], 40, axis=0), base[20:]])  # 800 dup + 280
     xq = np.concatenate([base[:20] + 0.001 * _rand(20, 64, 65), _rand(300, 64, 66)])
     index = vf.IndexFlat(64, metric)
-    index.set_engine("bf16v")
+    index.set_engine(engine)
     index.add(xb)
     _lib.filter_stats(reset=True)
     D, I = index.search(xq, 10)
@@ -581,7 +590,8 @@ def test_filter_every_query_falls_back(vf):
     assert not bad, bad[:5]
 
 
-def test_filter_wide_check_settles_scattered_near_duplicates(vf):
+@pytest.mark.parametrize("metric,engine", FILTER_CASES)
+def test_filter_wide_check_settles_scattered_near_duplicates(vf, metric, engine):
     """40 near-copies of each base row, scattered over the corpus: the KF merged
     candidates are all copies, so the first check flags those queries; every lane
     list holds only one or two copies, so the wide check (all list entries below
@@ -594,94 +604,79 @@ def test_filter_wide_check_settles_scattered_near_duplicates(vf):
                          _rand(4000, 64, 82)])
     xb = xb[np.random.default_rng(83).permutation(xb.shape[0])]
     xq = np.concatenate([base + 1e-4 * _rand(60, 64, 84), _rand(196, 64, 85)])
-    for metric in (IP, L2):
-        index = vf.IndexFlat(64, metric)
-        index.set_engine("bf16v")
-        index.add(xb)
-        _lib.filter_stats(reset=True)
+    index = vf.IndexFlat(64, metric)
+    index.set_engine(engine)
+    index.add(xb)
+    _lib.filter_stats(reset=True)
+    D, I = index.search(xq, 10)
+    wide = _lib.filter_wide_stats()
+    nq, n_exact = _lib.filter_stats(reset=True)
+    assert nq == xq.shape[0]
+    assert wide >= 60 and n_exact == 0, (metric, wide, n_exact)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
+    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+    assert not bad, bad[:5]
+
+
+def test_filter_engines_agree_and_l2_has_no_int8(vf):
+    """Every filter engine of an inner-product index (the staged default, int8
+    alone, bf16 alone) returns the exact lists; an L2 index holds no int8 plane
+    (the int8 filter has no L2 form) and refuses the int8 engine."""
+    xb = _rand(20000, 192, 86)
+    xq = _rand(300, 192, 87)
+    index = vf.IndexFlatIP(192)
+    assert index.filter_planes == ("i8", "bf16")
+    index.add(xb)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    for engine in ("auto", "bf16v", "i8v", "bf16v", "auto"):
+        index.set_engine(engine)
         D, I = index.search(xq, 10)
-        wide = _lib.filter_wide_stats()
-        nq, n_exact = _lib.filter_stats(reset=True)
-        assert nq == xq.shape[0]
-        assert wide >= 60 and n_exact == 0, (metric, wide, n_exact)
-        Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
-        assert not bad, bad[:5]
+        assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq), engine
+    l2 = vf.IndexFlatL2(192)
+    assert l2.filter_planes == ("bf16",)
+    with pytest.raises(RuntimeError):
+        l2.set_engine("i8v")
 
 
-def test_search_device_is_stream_async(vf):
-    """A device-buffer search queues its work and returns: the host does not
-    wait for the kernels (the filter engine keeps its counts on the device), so
-    enqueueing a search takes far less than running it."""
-    torch = pytest.importorskip("torch")
-    import time
-
-    index = vf.IndexFlatIP(512)
-    index.add_synthetic(3_000_000, seed=7)
-    xq = torch.from_numpy(_rand(4096, 512, 91) * 0.5).cuda()
-    D = torch.empty((4096, 10), dtype=torch.float32, device="cuda")
-    I = torch.empty((4096, 10), dtype=torch.int64, device="cuda")
-    st = torch.cuda.current_stream().cuda_stream
-    index.search_device(xq.data_ptr(), 4096, 10, D.data_ptr(), I.data_ptr(), st)  # warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    index.search_device(xq.data_ptr(), 4096, 10, D.data_ptr(), I.data_ptr(), st)
-    t_enqueue = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    t_total = time.perf_counter() - t0
-    assert t_enqueue < 0.5 * t_total, (t_enqueue, t_total)
-    Dh, Ih = index.search(xq[:64].cpu().numpy(), 10)
-    np.testing.assert_array_equal(I[:64].cpu().numpy(), Ih)
+def _clustered(n, d, ncent, seed, cseed=5):
+    """Unit-norm rows normalize(c[i % ncent] + 0.5 noise / sqrt(d)): clusters laid
+    out periodically, like bench.py's clustered data."""
+    c = np.random.default_rng(cseed).standard_normal((ncent, d))
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    x = c[np.arange(n) % ncent] + 0.5 * np.random.default_rng(seed).standard_normal((n, d)) / d ** 0.5
+    return (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
 
 
-def test_l2_small_calls_use_faiss_sequential_formula(vf):
-    """faiss switches formulas on the call's query count (nq < 20: direct sum of
-    squares; nq >= 20: |q|^2 + |x|^2 - 2 q.x): 9..19-query L2 calls match the C
-    restatement of the sequential branch bit for bit, like 1..8."""
-    xb = _rand(3000, 48, 92)
-    for nq in (1, 8, 9, 13, 19):
-        xq = _rand(nq, 48, 93 + nq)
-        index = vf.IndexFlatL2(48)
-        index.add(xb)
-        D, I = index.search(xq, 10)
-        Dc, Ic = cfaiss.knn_seq(xb, xq, 10, L2)
-        np.testing.assert_array_equal(I, Ic)
-        np.testing.assert_allclose(D, Dc, rtol=2e-6, atol=1e-5)
-
-
-@pytest.mark.parametrize("metric", [L2, IP])
-@pytest.mark.parametrize("nshard", [2, 3, 8])
-def test_sharded_raw_merge_exact_on_ties(vf, metric, nshard):
-    """The multi-GPU search's data flow on one device: shards (id_base = their
-    first label) return their raw lexicographic best min(2k-1, 64) (IP) or k (L2)
-    entries (VS_RAW_ORDER), vs_merge_topk applies faiss's tie rule once — labels
-    and scores equal the C faiss-heap restatement bit for bit on tie-heavy data."""
-    torch = pytest.importorskip("torch")
-    import ctypes
-
+def test_staged_engine_hands_clustered_queries_to_bf16(vf):
+    """Clustered unit-norm rows: the int8 bound cannot separate a query's
+    neighbours inside its cluster, so the staged engine hands (nearly) every
+    query to the bf16 stage as a gathered batch, which settles them; results
+    keep oracle parity, and the cosine self-join takes the same path."""
     from vsearch import _lib
-    from vsearch.sharded import shard_bounds
 
-    xb = _rand(600, 3, 31, "int")
-    for nq in (1, 7, 40):
-        xq = _rand(nq, 3, 32 + nq, "int")
-        for k in (1, 4, 10, 16):
-            kin = min(2 * k - 1, 64) if metric == IP else k
-            parts = []
-            for r in range(nshard):
-                lo, hi = shard_bounds(600, nshard, r)
-                idx = vf.IndexFlat(3, metric)
-                idx.add(xb[lo:hi])
-                idx.set_id_base(lo)
-                parts.append(idx.search(xq, kin, raw=True))
-            Dp = torch.from_numpy(np.stack([p[0] for p in parts])).cuda()
-            Ip = torch.from_numpy(np.stack([p[1] for p in parts])).cuda()
-            D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
-            I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
-            _lib.check(_lib.load().vs_merge_topk(
-                ctypes.c_void_p(Dp.data_ptr()), ctypes.c_void_p(Ip.data_ptr()), nshard, nq, kin,
-                k, metric, ctypes.c_void_p(D.data_ptr()), ctypes.c_void_p(I.data_ptr()), None))
-            torch.cuda.synchronize()
-            Dc, Ic = cfaiss.knn_seq(xb, xq, k, metric)
-            np.testing.assert_array_equal(I.cpu().numpy(), Ic)
-            np.testing.assert_array_equal(D.cpu().numpy(), Dc)
+    xb = _clustered(16384, 1536, 8, 91)
+    xq = _clustered(300, 1536, 8, 92)
+    index = vf.IndexFlatIP(1536)
+    index.add(xb)
+    _lib.filter_stats(reset=True)
+    D, I = index.search(xq, 10)
+    second = _lib.filter_second_stats()
+    nq, n_exact = _lib.filter_stats(reset=True)
+    assert nq == 300 and second > 200 and n_exact < 30, (second, n_exact)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+    assert not bad, bad[:5]
+    # the library has seen the int8 stage hand most queries on: the next search
+    # starts on bf16 (nothing handed over), with the same exact results
+    D2, I2 = index.search(xq, 10)
+    second2 = _lib.filter_second_stats()
+    _lib.filter_stats(reset=True)
+    assert second2 == 0, second2
+    assert not flat.mismatches(D2, I2, Dr, Ir, IP, xb, xq)
+    # the same rows through the cosine self-join (a 1000-student sub-range)
+    S, J = index.selfjoin(15, q0=3000, nq=1000)
+    Sr, Jr = flat.pgvector_cosine_topk(xb, 15, q_rows=np.arange(3000, 4000))
+    diff = J != Jr
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
+    np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
