@@ -580,7 +580,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   if (wide_enabled())
     VS_HIP(launch_verify_wide(mode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
                               idx->norms, Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
-                              vp.KP, flags, st, qinv, xinv, qr2),
+                              vp.KP, flags, st, qinv, xinv, qr2, Dk),
            "vs: verify wide");
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, last_plane ? dst + 2 : dst + 3,
                               nullptr, st),

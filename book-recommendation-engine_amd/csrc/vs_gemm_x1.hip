@@ -531,7 +531,8 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     return v > 0 ? v : kX1ChunkTiles;
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
-  const int nchunk = std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
+  // a gathered later stage (usually empty: its tiles exit at once) is one launch
+  const int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   const int64_t ldb = a.ld * filter_bytes(EL);
   for (int c = 0; c < nchunk; ++c) {
     hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 4, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
@@ -1134,7 +1135,8 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
-    const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8) {
+    const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8,
+    const float* __restrict__ Dk) {
   __shared__ float ck[kWideCap];
   __shared__ int cid[kWideCap];
   __shared__ float wT[4];
@@ -1180,6 +1182,23 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     __syncthreads();
     T = fminf(fminf(wT[0], wT[1]), fminf(wT[2], wT[3]));
     bounded = (wB[0] | wB[1] | wB[2] | wB[3]) != 0;
+    const double bkey =
+        bound_key(MODE, ba, qs[0], qs[1], MODE == MODE_L2 ? (double)qn[q] : qs[2], stats);
+    // Any threshold T' <= T works (every row outside the set still has an
+    // approximate key >= T'): with a_M the M-th smallest approximate key (the
+    // merge's Dk), the M best-approximate rows have exact keys <= a_M + B, so
+    // T' = a_M + 2B passes the check whenever it is below T, and rescoring only
+    // the entries below T' keeps the set small when the lists reach deep (many
+    // lists per query: T far behind the top).
+    if (bounded && Dk) {
+      const float aM = Dk[(int64_t)q * KF + M - 1];
+      const double tp = (double)aM + 2.000001 * bkey;
+      if (isfinite(tp) && tp < (double)T) {
+        float t = (float)tp;
+        if ((double)t < tp) t = nextafterf(t, INFINITY);
+        T = fminf(T, t);
+      }
+    }
     // gather every entry below T (all entries when no list is full)
     for (int j = tid; j < P * L; j += 256) {
       const int64_t o = lbase + (int64_t)(j / L) * LKP + j % L;
@@ -1237,8 +1256,6 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
         }
         __syncthreads();
         const float eM = eMs;
-        const double bkey =
-            bound_key(MODE, ba, qs[0], qs[1], MODE == MODE_L2 ? (double)qn[q] : qs[2], stats);
         const bool pass =
             !bounded || ((double)T - bkey > (double)eM && isfinite(eM) && isfinite(bkey));
         if (tid == 0 && pass) fail[q] = 0;
@@ -1253,14 +1270,14 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
-                              const float* xinv, const float* qr2i8) {
+                              const float* xinv, const float* qr2i8, const float* Dk) {
   if (KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
   if (nq_max <= 0) return hipSuccess;
   const int grid = std::min(nq_max, 2048);
 #define VS_WIDE(MD)                                                                               \
   hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(grid), dim3(256), 0, st, qlist, count, KF, M, X, \
                      xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey,   \
-                     oid, KP, fail, qinv, xinv, qr2i8)
+                     oid, KP, fail, qinv, xinv, qr2i8, Dk)
   if (mode == MODE_IP)
     VS_WIDE(MODE_IP);
   else if (mode == MODE_L2)

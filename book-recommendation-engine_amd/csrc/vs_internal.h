@@ -161,7 +161,9 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
                                 unsigned long long* total, unsigned long long* total_n,
                                 hipStream_t st);
 // Second verification of the queries qlist[0 .. *count) (device count, fixed
-// grid): every lane-list entry below the smallest full-list floor is rescored
+// grid): every lane-list entry below the smallest full-list floor (or below
+// Dk's M-th key + 2 B when that is smaller; Dk = the merged approximate keys,
+// [nq][KF]) is rescored
 // exactly (up to kWideCap per query) and the condition re-checked on that wider
 // set; passing queries get their sorted exact list in okey/oid and fail[q] = 0.
 constexpr int kWideCap = 2048;
@@ -170,7 +172,7 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
-                              const float* xinv, const float* qsc);
+                              const float* xinv, const float* qsc, const float* Dk);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
 // (key, label) order, the per-shard half of an exact sharded merge).  With
