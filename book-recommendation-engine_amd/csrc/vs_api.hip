@@ -426,7 +426,7 @@ int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st);
 // The host never waits: counts live in device memory.  `gl` / `gc` (stages
 // after the first): the batch is queries gl[0 .. *gc) of `a`.
 int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
-                      int plane, bool last_plane, const int* gl = nullptr,
+                      int plane, bool last_plane, bool deep = false, const int* gl = nullptr,
                       const int* gc = nullptr) {
   const int ntotal = (int)idx->ntotal;
   const int mode = a.mode;
@@ -446,6 +446,14 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   // C3 queries to the exact engine on int8)
   x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, 2 * ((KF + L - 1) / L)),
                                     std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
+  // the deep stage (a gathered batch of the few queries an earlier stage could
+  // not settle): as many lists as two workgroups per CU give ONE query tile, so
+  // the floors sit far behind the top (the a_M + 2B threshold keeps the wide
+  // set small)
+  // (lane lists of at most ~1 GB: x.nq_pad slots x 4 nsplit lists x 8 entries x 8 B)
+  if (deep)
+    x.nsplit = (int)std::max<int64_t>(
+        x.nsplit, std::min<int64_t>({ntiles, 512, (1ll << 30) / ((int64_t)x.nq_pad * 4 * 8 * 8)}));
   x.nsplit = std::max(x.nsplit, 1);
   {  // A/B: more (shorter) database splits = more lane lists per query
     static const int mult = [] {
@@ -601,7 +609,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
       int rc = adaptive_record(idx, qcount + 1, nq, st);
       if (rc) return rc;
     }
-    return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, true, next, qcount + 1);
+    return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, true, true, next, qcount + 1);
   }
   // the exact redo (untimed: the kernel timer holds the first filter pass)
   SearchArgs ex = a;
@@ -765,8 +773,9 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
     const bool b16_ok = idx->plane_on[FILTER_BF16] && engine != VS_ENGINE_I8_VERIFY;
     // the automatic order adapts to how much the int8 stage settles
     if (i8_ok && b16_ok && engine == VS_ENGINE_AUTO) i8_ok = adaptive_use_i8(idx);
+    // stages: [int8] -> bf16 with deep lists over what is left -> exact fp32
     if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
-    if (b16_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, true);
+    if (b16_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);
   }
   return run_gemm(idx, a, need, st);
 }
