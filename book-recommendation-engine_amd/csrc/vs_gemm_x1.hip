@@ -349,8 +349,27 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
           xsv[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr (EL == FILTER_I8) xsv[jj] = *(const f32x4*)(xs + g);
         }
+        // int8: a block's scores are fl(fl(float(sum)) * fl(f_q * f_x)), monotone
+        // in the sum and in f_x (both factors >= 0), so the lane's largest
+        // factor over its 16 rows and the largest sum bound every score of the
+        // block from above: when that bound cannot beat the list, the block is
+        // skipped without converting its 16 sums
+        float fmax = 0.0f;
+        if constexpr (EL == FILTER_I8) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fmax = fmaxf(fmax, xsv[jj][e]);
+        }
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
+          if constexpr (EL == FILTER_I8) {
+            int amax = acc[rb][qb][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
+            const float upper = amax > 0 ? (float)amax * (qsc[qb] * fmax) : 0.0f;
+            if (!(upper > -lk[qb][KR - 1])) continue;  // key = -score < last needs score > -last
+          }
           f32x16 key;
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
