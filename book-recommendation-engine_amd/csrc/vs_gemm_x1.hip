@@ -77,7 +77,7 @@ namespace vs {
 namespace {
 
 constexpr int kT = 256;               // rows (and queries) per tile
-constexpr int kX1ChunkTiles = 16;     // database tiles per workgroup per launch
+constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 __device__ __forceinline__ i32x4 as_i4(const uint4& u) { return __builtin_bit_cast(i32x4, u); }
