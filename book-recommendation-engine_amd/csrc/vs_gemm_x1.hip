@@ -153,16 +153,19 @@ __device__ __forceinline__ float sel16(const f32x16& v, int i) {
 // (the MFMA's inline-constant C), so no register clearing between tiles.  Load
 // and position cursors are incremental (no divisions in the loop).
 //
-// XCD blocking (a 256-workgroup grid, one per CU): the 32 workgroups of an XCD
-// take QG query tiles x DG database splits (QG = min(nqt, 4)), so each XCD's L2
-// serves a query tile to DG workgroups and a database tile to QG of them.
+// XCD blocking (grids of 8 S workgroups; workgroup b runs on XCD b % 8, in slot
+// order b / 8 there): the S workgroups of an XCD take QG query tiles x DG
+// database splits (QG = min(nqt, qg)), so each XCD's L2 holds QG query tiles'
+// slices (QG x 16 KB per step) and serves a database tile to QG workgroups;
+// slot / QG orders the splits, so with two rounds of workgroups per CU each
+// round covers its own DG / 2 splits.  Other grids: a plain dealing.
 template <int KR, int MODE, int NBUF, int EL>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ XH, const float* __restrict__ xs, const float* __restrict__ xaux,
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
     int nqa, int64_t ldb, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
-    float* __restrict__ pkey, int* __restrict__ pid) {
+    int qg, float* __restrict__ pkey, int* __restrict__ pid) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
   constexpr int D = NBUF - 1;      // steps in flight
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
@@ -179,10 +182,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   {
     const int nblk = gridDim.x;
     const int b = blockIdx.x;
-    const int QG = nqt < 4 ? nqt : 4;
+    const int QG = nqt < qg ? nqt : qg;
     const int G = nqt / QG;
-    if (nblk == 256 && nqt * nsplit == 256 && nqt % QG == 0 && G <= 8 && 8 % G == 0) {
-      const int xcd = b & 7, slot = b >> 3, DG = 32 / QG;
+    const int S = nblk >> 3;
+    if ((nblk & 7) == 0 && nqt * nsplit == nblk && nqt % QG == 0 && G <= 8 && 8 % G == 0 &&
+        S % QG == 0) {
+      const int xcd = b & 7, slot = b >> 3, DG = S / QG;
       qt = (xcd % G) * QG + slot % QG;
       sp = (xcd / G) * DG + slot / QG;
     } else {
@@ -540,6 +545,16 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 }
 
+// Query tiles per XCD of the blocked grid (env VS_X1_QG for A/B; default 4).
+static int x1_qg() {
+  static const int v = [] {
+    const char* e = getenv("VS_X1_QG");
+    const int q = e ? atoi(e) : 0;
+    return q > 0 ? q : 4;
+  }();
+  return v;
+}
+
 template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
@@ -557,7 +572,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 4, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
                        ldb, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.self0, a.qrow,
-                       a.qcount, c, nchunk, part.KP, part.key, part.id);
+                       a.qcount, c, nchunk, part.KP, x1_qg(), part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
