@@ -246,7 +246,6 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   const int64_t need = round_up(rows + 256, kRowPad);  // 256-row query tiles of self-joins
   if (need <= idx->capacity) return VS_OK;
   int64_t cap = std::max(need, round_up(idx->capacity + idx->capacity / 2, kRowPad));
-  const bool i8 = idx->plane_on[FILTER_I8];
   char* codes = nullptr;
   float* norms = nullptr;
   char* fplane[2] = {nullptr, nullptr};
@@ -273,7 +272,8 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
       if (e == hipSuccess && idx->plane_on[p]) e = hipMalloc(&fplane[p], (size_t)c * idx->planebytes(p));
       if (e == hipSuccess && idx->plane_on[p]) e = hipMalloc(&rn2[p], (size_t)c * sizeof(float));
     }
-    if (e == hipSuccess && i8) e = hipMalloc(&fscale, (size_t)c * sizeof(float));
+    if (e == hipSuccess && idx->plane_on[FILTER_I8])
+      e = hipMalloc(&fscale, (size_t)c * sizeof(float));
     if (e != hipSuccess) {
       (void)hipGetLastError();
       release();
@@ -284,8 +284,21 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   if (e != hipSuccess) {  // retry without the growth headroom
     cap = need;
     e = allocate(cap);
-    if (e != hipSuccess) return hip_fail(e, "vs: allocating row storage");
   }
+  // Still short of HBM: give up filter planes rather than rows (an fp32 inner-
+  // product index holds 10 B per element with both planes, 7 with int8 only,
+  // 4 without; searches then use the plane that remains, or the exact fp32
+  // engine): bf16 first, then every plane.
+  if (e != hipSuccess && idx->plane_on[FILTER_BF16] && idx->plane_on[FILTER_I8]) {
+    idx->plane_on[FILTER_BF16] = false;
+    e = allocate(cap);
+  }
+  if (e != hipSuccess && (idx->plane_on[FILTER_BF16] || idx->plane_on[FILTER_I8])) {
+    idx->plane_on[FILTER_BF16] = idx->plane_on[FILTER_I8] = false;
+    e = allocate(cap);
+  }
+  if (e != hipSuccess) return hip_fail(e, "vs: allocating row storage");
+  const bool i8 = idx->plane_on[FILTER_I8];
   // zero every tail (tile reads past ntotal must see zeros, never NaN garbage)
   const int64_t keep = idx->ntotal;
   VS_HIP(hipMemsetAsync(codes + keep * idx->rowbytes(), 0, (size_t)(cap - keep) * idx->rowbytes(),
