@@ -176,3 +176,39 @@ def test_int8_filter_bound_holds_for_cosine():
     rel = _GAM_I8 * (1 + rho) ** 2 + 2 * rho * (1 + rho) + rho ** 2 + 2.0 ** -23
     b = (rel * (1 + 1.5 * norm_inf) + 2.0 ** -22) * (1 + 1e-6)
     assert (np.abs(key_a - key_e) <= b).all(), float(np.abs(key_a - key_e).max() - b)
+
+
+def test_wide_threshold_below_the_floor_is_exact():
+    """The wide check may use any T' <= T (vs_gemm_x1.hip verify_wide_kernel):
+    with a_M the M-th smallest approximate key, T' = min(T, a_M + 2.000001 B)
+    keeps every row outside S at key >= T' and the M best-approximate rows in S
+    (exact keys <= a_M + B), so the check passes whenever T' < T; whenever it
+    accepts, S holds the exact top-M.  Deep lists (many lists, far floors) shrink
+    S to the rows near the top."""
+    rng = np.random.default_rng(99)
+    B, M = 1e-3, 19
+    accepted = 0
+    sizes = []
+    for q in range(80):
+        n = 4000
+        e = rng.standard_normal(n)
+        if q % 3:
+            e[rng.choice(n, 60, replace=False)] = -5.0 + rng.uniform(0, 6 * B, 60)
+        a = e + rng.uniform(-B, B, n)
+        lists = _lane_lists(a, 128, 8, rng)
+        full = [lst for lst in lists if len(lst) == 8]
+        T = min(a[lst[-1]] for lst in full)
+        entries = np.concatenate(lists)
+        aM = np.sort(a[entries])[M - 1]
+        Tp = min(T, aM + 2.000001 * B)
+        S = [r for r in entries if a[r] < Tp]
+        ok, top = _accept(S, Tp, e, B, M)
+        if Tp < T:
+            assert ok  # passes by construction when the threshold is below the floor
+        if ok:
+            accepted += 1
+            sizes.append(len(S))
+            exact = np.lexsort((np.arange(n), e))[:M]
+            np.testing.assert_array_equal(top, exact)
+    assert accepted == 80
+    assert max(sizes) < 128 * 8
