@@ -45,6 +45,10 @@
 #ifndef VS_X1_PRIO
 #define VS_X1_PRIO 0
 #endif
+// LDS images in the ring (5: 4 steps in flight, all 160 KB; 4: -1 %, profiles/r02y)
+#ifndef VS_X1_NBUF
+#define VS_X1_NBUF 5
+#endif
 #ifndef VS_X1_STAGGER
 #define VS_X1_STAGGER 1
 #endif
@@ -569,7 +573,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   const int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   const int64_t ldb = a.ld * filter_bytes(EL);
   for (int c = 0; c < nchunk; ++c) {
-    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, 4, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, VS_X1_NBUF, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
                        ldb, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.self0, a.qrow,
                        a.qcount, c, nchunk, part.KP, x1_qg(), part.key, part.id);
