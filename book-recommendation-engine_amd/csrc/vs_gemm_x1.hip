@@ -569,6 +569,11 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     return v > 0 ? v : kX1ChunkTiles;
   }();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
+  // A gathered later stage holds its few queries in the first query tile(s):
+  // every XCD takes every query tile there (QG = nqt), so the working
+  // workgroups of tile 0 spread over all XCDs instead of the 2 of 8 that QG = 4
+  // gives it (clustered C3: 202 -> 151 ms per step, profiles/r02za).
+  const int qg = a.qcount ? nqt : x1_qg();
   // a gathered later stage (usually empty: its tiles exit at once) is one launch
   const int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   const int64_t ldb = a.ld * filter_bytes(EL);
@@ -576,7 +581,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, VS_X1_NBUF, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
                        ldb, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.self0, a.qrow,
-                       a.qcount, c, nchunk, part.KP, x1_qg(), part.key, part.id);
+                       a.qcount, c, nchunk, part.KP, qg, part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
