@@ -451,13 +451,15 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const int nqt = x.nq_pad / kX1Q;
   const int ntiles = (ntotal + kX1Q - 1) / kX1Q;
   const int L = x1_lane_len();
-  // enough lists that their 4*nsplit*L entries cover 8*KF candidates, and two
-  // workgroups per CU on 256 CUs: 128 lists per query at C3.  More lists put
+  // enough lists that their 4*nsplit*L entries cover 16*KF candidates (C4's
+  // self-join, KF = 64: 128 lists, which lets the int8 stage settle it: 283k ->
+  // 372k students/s, profiles/r02zc), and two workgroups per CU on 256 CUs: 128
+  // lists per query at C3.  More lists put
   // the wide check's floor T (the best last entry of a full list) deeper
   // behind the top-M, which the bound needs on clustered data and on the int8
   // plane (profiles/r02l_ab_split.txt; one workgroup per CU left 0.7 % of the
   // C3 queries to the exact engine on int8)
-  x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, 2 * ((KF + L - 1) / L)),
+  x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, 4 * ((KF + L - 1) / L)),
                                     std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
   // the deep stage (a gathered batch of the few queries an earlier stage could
   // not settle): as many lists as two workgroups per CU give ONE query tile, so
