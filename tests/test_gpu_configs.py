@@ -1,0 +1,70 @@
+"""GPU, BASELINE configs C2 and C4 at full size with the DEFAULT engine (the
+staged int8 -> bf16 -> fp32 filter-and-verify path), checked against the fp64
+oracle on sampled queries / students from the first and last query tiles and
+across the self-join's 65,536-row chunks.
+
+C2: 1M x 1536 fp32, batch 1024, top-10 inner product (bench.py --workload c2).
+C4: 1M x 1536 fp32, cosine top-50 self-join excluding self (bench.py --workload
+c4, graph_refresher/main.py:339-354 at 1M students).  The rows are read back
+from the index (vs_reconstruct_n is bit-exact) and scored in fp64
+(oracle/flat.py).  Acceptance as everywhere: labels exact except documented
+ties, scores within 1e-5."""
+
+import numpy as np
+import pytest
+
+from oracle import flat
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+N, D_ = 1_000_000, 1536
+
+
+def _rows(index, chunk=250_000):
+    return np.concatenate([index.reconstruct_n(r0, min(chunk, N - r0))
+                           for r0 in range(0, N, chunk)])
+
+
+def test_c2_batch1024_sampled_against_oracle():
+    from vsearch import faiss as vfaiss
+    from vsearch.synth import synthetic_rows
+
+    k = 10
+    index = vfaiss.IndexFlatIP(D_)
+    index.add_synthetic(N, seed=1234)
+    xq = synthetic_rows(50_000_000, 1024, D_, 5678)
+    D, I = index.search(xq, k)
+    assert I.shape == (1024, k) and (I >= 0).all() and (I < N).all()
+    assert (np.diff(D, axis=1) <= 0).all()
+    sample = [0, 1, 255, 256, 511, 767, 768, 1023]
+    xb = _rows(index)
+    s = np.zeros((len(sample), N))
+    q64 = xq[sample].astype(np.float64)
+    for r0 in range(0, N, 250_000):
+        s[:, r0:r0 + 250_000] = q64 @ xb[r0:r0 + 250_000].astype(np.float64).T
+    for row, q in enumerate(sample):
+        ref = flat.faiss_order(np.arange(N, dtype=np.int64), -s[row], k,
+                               flat.METRIC_INNER_PRODUCT)
+        for j in range(k):
+            assert abs(float(D[q, j]) - s[row, ref[j]]) <= 1e-5 * max(1.0, abs(s[row, ref[j]]))
+            if I[q, j] != ref[j]:  # a different label only as a documented tie
+                assert abs(s[row, I[q, j]] - s[row, ref[j]]) <= 1e-5 * max(1.0, abs(s[row, ref[j]]))
+
+
+def test_c4_selfjoin_top50_sampled_against_oracle():
+    from vsearch import faiss as vfaiss
+
+    k = 50
+    index = vfaiss.IndexFlatIP(D_)
+    index.add_synthetic(N, seed=4321)
+    S, I = index.selfjoin(k)
+    assert I.shape == (N, k) and (I >= 0).all() and (I < N).all()
+    assert not (I == np.arange(N)[:, None]).any()
+    sample = np.array([0, 1, 255, 256, 65535, 65536, 131071, 500000, 999743, 999999])
+    xb = _rows(index)
+    Sr, Ir = flat.pgvector_cosine_topk(xb, k, q_rows=sample)
+    for row, q in enumerate(sample):
+        diff = I[q] != Ir[row]
+        for j in np.nonzero(diff)[0]:  # documented ties only
+            assert abs(float(S[q, j]) - float(Sr[row, j])) < 1e-5, (q, j)
+        np.testing.assert_allclose(S[q][~diff], Sr[row][~diff], rtol=1e-5, atol=1e-6)
