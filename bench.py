@@ -388,6 +388,12 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
                           "per fp32 product (bf16 copies of rows and queries), against the dense "
                           "bf16 peak; candidates are then rescored exactly in fp64 and a "
                           "rigorous error bound proves the exact top-k is among them")
+    if kind in ("mfma_x1", "mfma_x1_i8"):
+        # the same algorithmic work (2*N*d per query, exact results) against the
+        # fp32 matrix peak an exact fp32 engine would be bounded by
+        r["fp32_equivalent"] = {"achieved_TFLOPs": round(achieved, 3),
+                                "fp32_matrix_peak": FP32_MFMA_PEAK_TFLOPS,
+                                "ratio": round(achieved / FP32_MFMA_PEAK_TFLOPS, 3)}
     if kind == "mfma_x1_i8":
         r["peak_note"] = ("filter pass of the filter-and-verify engine: one int8 MFMA product "
                           "per fp32 product (int8 codes of rows and queries, one fp32 scale per "
