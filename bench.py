@@ -458,6 +458,7 @@ def run_knn(args, ctx):
         lambda i: index.search_device(xq, k, stream=ctx.stream), args.steps, args.warmup)
     fw = ctx.lib.filter_wide_stats()
     f2 = ctx.lib.filter_second_stats()
+    we, wr = ctx.lib.filter_wide_sets()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
@@ -536,6 +537,8 @@ def run_knn(args, ctx):
         res["roofline"] = rf
         if fq:
             res["filter_verify"] = {"plane": plane, "queries": fq, "wide_checked": fw,
+                                    "wide_set_mean": round(we / fw, 1) if fw else 0.0,
+                                    "wide_rescored_mean": round(wr / fw, 1) if fw else 0.0,
                                     "to_bf16_stage": f2,
                                     "fallback_queries": ff,
                                     "fallback_rate": round(ff / fq, 6), "exact_check": exact_check}
@@ -580,6 +583,7 @@ def run_selfjoin(args, ctx):
     elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
     fw = ctx.lib.filter_wide_stats()
     f2 = ctx.lib.filter_second_stats()
+    we, wr = ctx.lib.filter_wide_sets()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Ih = I.cpu()
     sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
@@ -640,6 +644,8 @@ def run_selfjoin(args, ctx):
         res["roofline"] = rf
         if fq:
             res["filter_verify"] = {"plane": plane, "students": fq, "wide_checked": fw,
+                                    "wide_set_mean": round(we / fw, 1) if fw else 0.0,
+                                    "wide_rescored_mean": round(wr / fw, 1) if fw else 0.0,
                                     "to_bf16_stage": f2,
                                     "fallback_students": ff,
                                     "fallback_rate": round(ff / fq, 6),

@@ -139,7 +139,10 @@ const char* g_timer_kernel = "";
 
 // Filter-and-verify statistics, counted on the device (no host sync in a
 // search): [0] queries, [1] flagged by the first check (given to the wide
-// check), [2] flagged by both (redone by the exact engine).  One buffer per device.
+// check), [2] flagged by both (redone by the exact engine), [3] handed to a
+// second filter stage, [4] wide-set entries, [5] of them rescored (the rest
+// reuse the first check's keys).  One buffer per device.
+constexpr int kStatSlots = 6;
 std::mutex g_stats_mu;
 std::vector<unsigned long long*> g_dev_stats;
 
@@ -148,8 +151,8 @@ unsigned long long* device_stats(int dev) {
   if ((int)g_dev_stats.size() <= dev) g_dev_stats.resize(dev + 1, nullptr);
   if (!g_dev_stats[dev]) {
     unsigned long long* p = nullptr;
-    if (hipMalloc(&p, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, kStatSlots * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kStatSlots * sizeof(unsigned long long)) != hipSuccess) return nullptr;
     g_dev_stats[dev] = p;
   }
   return g_dev_stats[dev];
@@ -607,7 +610,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   if (wide_enabled())
     VS_HIP(launch_verify_wide(mode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
                               idx->norms, Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
-                              vp.KP, flags, st, qinv, xinv, qr2, Dk),
+                              vp.KP, flags, st, qinv, xinv, qr2, Dk, Ik, dst + 4),
            "vs: verify wide");
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, last_plane ? dst + 2 : dst + 3,
                               nullptr, st),
@@ -1341,16 +1344,16 @@ int vs_fill_synthetic(float* out, int64_t rows, int64_t d, uint64_t seed, int64_
 
 // The counters live on the devices (written by the searches' own kernels); reading
 // them waits for every search already queued on those devices.
-static int read_filter_stats(unsigned long long out[4], int reset) {
-  out[0] = out[1] = out[2] = out[3] = 0;
+static int read_filter_stats(unsigned long long out[kStatSlots], int reset) {
+  for (int i = 0; i < kStatSlots; ++i) out[i] = 0;
   std::lock_guard<std::mutex> g(g_stats_mu);
   for (int dev = 0; dev < (int)g_dev_stats.size(); ++dev) {
     if (!g_dev_stats[dev]) continue;
     DeviceGuard dg(dev);
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[kStatSlots] = {};
     VS_HIP(hipDeviceSynchronize(), "vs_filter_stats");
     VS_HIP(hipMemcpy(h, g_dev_stats[dev], sizeof(h), hipMemcpyDeviceToHost), "vs_filter_stats");
-    for (int i = 0; i < 4; ++i) out[i] += h[i];
+    for (int i = 0; i < kStatSlots; ++i) out[i] += h[i];
     if (reset) VS_HIP(hipMemset(g_dev_stats[dev], 0, sizeof(h)), "vs_filter_stats");
   }
   return VS_OK;
@@ -1358,7 +1361,7 @@ static int read_filter_stats(unsigned long long out[4], int reset) {
 
 int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
   if (!queries || !fallbacks) return fail(VS_E_INVALID, "vs_filter_stats: null output");
-  unsigned long long c[4];
+  unsigned long long c[kStatSlots];
   int rc = read_filter_stats(c, reset);
   if (rc) return rc;
   *queries = (int64_t)c[0];
@@ -1368,16 +1371,26 @@ int vs_filter_stats(int64_t* queries, int64_t* fallbacks, int reset) {
 
 int vs_filter_wide_stats(int64_t* wide) {
   if (!wide) return fail(VS_E_INVALID, "vs_filter_wide_stats: null output");
-  unsigned long long c[4];
+  unsigned long long c[kStatSlots];
   int rc = read_filter_stats(c, 0);
   if (rc) return rc;
   *wide = (int64_t)c[1];
   return VS_OK;
 }
 
+int vs_filter_wide_sets(int64_t* entries, int64_t* rescored) {
+  if (!entries || !rescored) return fail(VS_E_INVALID, "vs_filter_wide_sets: null output");
+  unsigned long long c[kStatSlots];
+  int rc = read_filter_stats(c, 0);
+  if (rc) return rc;
+  *entries = (int64_t)c[4];
+  *rescored = (int64_t)c[5];
+  return VS_OK;
+}
+
 int vs_filter_second_stats(int64_t* second) {
   if (!second) return fail(VS_E_INVALID, "vs_filter_second_stats: null output");
-  unsigned long long c[4];
+  unsigned long long c[kStatSlots];
   int rc = read_filter_stats(c, 0);
   if (rc) return rc;
   *second = (int64_t)c[3];

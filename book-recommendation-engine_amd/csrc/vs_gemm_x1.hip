@@ -1170,7 +1170,10 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // dropped only rows lexicographically after its last entry), and then the set
 // may be *all* list entries below T, not just the KF merged ones.  More than
 // kWideCap entries below T, fewer than M, or a non-finite key: the query stays
-// flagged.
+// flagged.  The KF merged candidates the first check rescored (Dk/Ik, exact
+// keys in okey/oid) keep their exact keys: an entry lexicographically at or
+// before the KF-th merged one is one of them, and only the others are read
+// from HBM again (C4: ~40 % of the wide set).
 template <int MODE>
 __global__ __launch_bounds__(256) void verify_wide_kernel(
     const int* __restrict__ qlist, const int* __restrict__ count, int KF, int M,
@@ -1179,9 +1182,13 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
     const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8,
-    const float* __restrict__ Dk) {
+    const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
+    unsigned long long* __restrict__ sizes) {
   __shared__ float ck[kWideCap];
   __shared__ int cid[kWideCap];
+  __shared__ float rk[64], kk[64];  // the first check's exact keys / the reused ones
+  __shared__ int ri[64], ki[64];
+  __shared__ int cntk;
   __shared__ float wT[4];
   __shared__ int wB[4];
   __shared__ int cnt, bad;
@@ -1209,8 +1216,13 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     }
     if (tid == 0) {
       cnt = 0;
+      cntk = 0;
       bad = 0;
       eMs = FLT_MAX;
+    }
+    if (tid < 64) {  // the first check's output for this query (KP <= 64 entries)
+      rk[tid] = tid < KP ? okey[(int64_t)q * KP + tid] : FLT_MAX;
+      ri[tid] = tid < KP ? oid[(int64_t)q * KP + tid] : -1;
     }
     const float* qrow = Q + (int64_t)q * ld;
     if (wv == 0) {
@@ -1233,26 +1245,54 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     // T' = a_M + 2B passes the check whenever it is below T, and rescoring only
     // the entries below T' keeps the set small when the lists reach deep (many
     // lists per query: T far behind the top).
+    // Tighter still: e1_M, the M-th exact key among the first check's KF rows,
+    // bounds E_M from above, and every row with approximate key >= e1_M + B has
+    // an exact key > e1_M >= E_M; those M rows (approximate keys <= e1_M + B)
+    // stay in the set.  T' = e1_M + B is ~a_M + B: half the window of a_M + 2B.
     if (bounded && Dk) {
       const float aM = Dk[(int64_t)q * KF + M - 1];
-      const double tp = (double)aM + 2.000001 * bkey;
+      double tp = (double)aM + 2.000001 * bkey;
+      if (ri[M - 1] >= 0 && isfinite(rk[M - 1]))
+        tp = fmin(tp, (double)rk[M - 1] + 1.000001 * bkey);
       if (isfinite(tp) && tp < (double)T) {
         float t = (float)tp;
         if ((double)t < tp) t = nextafterf(t, INFINITY);
         T = fminf(T, t);
       }
     }
+    // the KF-th merged entry: entries up to it were rescored by the first check
+    // (all of them when the merge found fewer than KF)
+    const float kfk = Dk ? Dk[(int64_t)q * KF + KF - 1] : -FLT_MAX;
+    const int kfi = Dk ? (int)Ik[(int64_t)q * KF + KF - 1] : INT_MIN;
     // gather every entry below T (all entries when no list is full)
     for (int j = tid; j < P * L; j += 256) {
       const int64_t o = lbase + (int64_t)(j / L) * LKP + j % L;
       const int r = lid[o];
-      if (r >= 0 && (!bounded || lkey[o] < T)) {
-        const int s = atomicAdd(&cnt, 1);
-        if (s < kWideCap) cid[s] = r;
+      const float lk = lkey[o];
+      if (r >= 0 && (!bounded || lk < T)) {
+        int hit = -1;
+        if (Dk && (kfi < 0 || !lex_less(kfk, kfi, lk, r)))
+          for (int t = 0; t < KP && t < 64; ++t) hit = ri[t] == r ? t : hit;
+        if (hit >= 0) {
+          const int s = atomicAdd(&cntk, 1);
+          if (s < 64) {
+            kk[s] = rk[hit];
+            ki[s] = r;
+          }
+        } else {
+          const int s = atomicAdd(&cnt, 1);
+          if (s < kWideCap) cid[s] = r;
+        }
       }
     }
     __syncthreads();
-    const int n = cnt;
+    const int nu = cnt;  // rows to rescore
+    const int nk = min(cntk, 64);
+    const int n = nu + cntk;
+    if (sizes && tid == 0) {
+      atomicAdd(sizes, (unsigned long long)n);
+      atomicAdd(sizes + 1, (unsigned long long)nu);
+    }
     if (!(n > kWideCap || n < M || !isfinite(T))) {  // uniform
       auto put = [&](int j, int r, double acc) {
         if (lane == 0) {
@@ -1264,18 +1304,23 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
       if (ld <= 256 * kQV) {  // two rows per wave step, the query in registers
         QSlice qsl;
         load_qslice(qrow, ld, lane, qsl);
-        for (int j = wv; j < n; j += 8) {
-          const int ra = cid[j], rb = j + 4 < n ? cid[j + 4] : ra;
+        for (int j = wv; j < nu; j += 8) {
+          const int ra = cid[j], rb = j + 4 < nu ? cid[j + 4] : ra;
           double da, db;
           wave_dot2(X + (int64_t)ra * ld, X + (int64_t)rb * ld, qsl, ld, lane, da, db);
           put(j, ra, da);
-          if (j + 4 < n) put(j + 4, rb, db);
+          if (j + 4 < nu) put(j + 4, rb, db);
         }
       } else {
-        for (int j = wv; j < n; j += 4) {
+        for (int j = wv; j < nu; j += 4) {
           const int r = cid[j];
           put(j, r, wave_dot(X + (int64_t)r * ld, qrow, ld, lane));
         }
+      }
+      if (tid < nk) {  // the reused exact keys after the rescored ones
+        ck[nu + tid] = kk[tid];
+        cid[nu + tid] = ki[tid];
+        if (!isfinite(kk[tid])) bad = 1;
       }
       __syncthreads();
       if (!bad) {  // uniform
@@ -1313,14 +1358,15 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
-                              const float* xinv, const float* qr2i8, const float* Dk) {
-  if (KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
+                              const float* xinv, const float* qr2i8, const float* Dk,
+                              const int64_t* Ik, unsigned long long* sizes) {
+  if (KF > KP || KP > 64 || (Dk && !Ik) || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
   if (nq_max <= 0) return hipSuccess;
   const int grid = std::min(nq_max, 2048);
 #define VS_WIDE(MD)                                                                               \
   hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(grid), dim3(256), 0, st, qlist, count, KF, M, X, \
                      xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey,   \
-                     oid, KP, fail, qinv, xinv, qr2i8, Dk)
+                     oid, KP, fail, qinv, xinv, qr2i8, Dk, Ik, sizes)
   if (mode == MODE_IP)
     VS_WIDE(MODE_IP);
   else if (mode == MODE_L2)

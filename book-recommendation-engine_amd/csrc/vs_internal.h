@@ -163,16 +163,20 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // Second verification of the queries qlist[0 .. *count) (device count, fixed
 // grid): every lane-list entry below the smallest full-list floor (or below
 // Dk's M-th key + 2 B when that is smaller; Dk = the merged approximate keys,
-// [nq][KF]) is rescored
+// [nq][KF], Ik its rows) is rescored
 // exactly (up to kWideCap per query) and the condition re-checked on that wider
 // set; passing queries get their sorted exact list in okey/oid and fail[q] = 0.
+// okey/oid hold on entry the first check's exact keys of Ik (KP <= 64), which
+// are reused instead of read again.  sizes (optional): += the wide-set entries
+// and the rescored ones.
 constexpr int kWideCap = 2048;
 hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
                               int M, const float* X, const float* xn, const float* Q,
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
-                              const float* xinv, const float* qsc, const float* Dk);
+                              const float* xinv, const float* qsc, const float* Dk,
+                              const int64_t* Ik, unsigned long long* sizes = nullptr);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
 // (key, label) order, the per-shard half of an exact sharded merge).  With

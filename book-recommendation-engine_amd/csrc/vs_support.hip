@@ -26,19 +26,22 @@ namespace vs {
 template <int KP, typename IdT>
 __device__ __forceinline__ void wave_tree_merge(float (&lk)[KP], IdT (&li)[KP], float* sk,
                                                 IdT* si, int lane) {
-  // sk/si: LDS [64][KP]; on return lane 0 holds the merge of the 64 lists.
+  // sk/si: LDS [64][KP + 1] (the odd row stride spreads the active lanes' rows
+  // over all banks; a stride of KP put every even lane on one bank); on return
+  // lane 0 holds the merge of the 64 lists.
+  constexpr int KS = KP + 1;
   for (int step = 1; step < 64; step <<= 1) {
     if ((lane & (step - 1)) == 0) {
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
-        sk[lane * KP + j] = lk[j];
-        si[lane * KP + j] = li[j];
+        sk[lane * KS + j] = lk[j];
+        si[lane * KS + j] = li[j];
       }
     }
     __syncthreads();
     if ((lane & (2 * step - 1)) == 0)
-      merge2_sorted<KP, IdT>(sk + lane * KP, si + lane * KP, sk + (lane + step) * KP,
-                             si + (lane + step) * KP, lk, li);
+      merge2_sorted<KP, IdT>(sk + lane * KS, si + lane * KS, sk + (lane + step) * KS,
+                             si + (lane + step) * KS, lk, li);
     __syncthreads();
   }
 }
@@ -116,8 +119,8 @@ __global__ __launch_bounds__(64) void merge_lists_kernel(
     int* __restrict__ oid, int P2, int emit, int k, int mode, int raw, int64_t id_base,
     float min_score, float* __restrict__ D, int64_t* __restrict__ I, int64_t ldo,
     const int* __restrict__ qlist, const int* __restrict__ qcount) {
-  __shared__ float sk[64 * KP];
-  __shared__ int si[64 * KP];
+  __shared__ float sk[64 * (KP + 1)];
+  __shared__ int si[64 * (KP + 1)];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
   const int g = blockIdx.y;
@@ -236,8 +239,8 @@ __global__ __launch_bounds__(64) void merge_parts_kernel(const float* __restrict
                                                          int nparts, int nq, int k_in, int k,
                                                          int mode, float* __restrict__ D,
                                                          int64_t* __restrict__ I) {
-  __shared__ float sk[64 * KP];
-  __shared__ int64_t si[64 * KP];
+  __shared__ float sk[64 * (KP + 1)];
+  __shared__ int64_t si[64 * (KP + 1)];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
   const bool asc = (mode == MODE_L2 || mode == MODE_L2D);

@@ -78,6 +78,7 @@ SIGNATURES = {
     "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
     "vs_filter_wide_stats": (_c_int, [_i64p]),
     "vs_filter_second_stats": (_c_int, [_i64p]),
+    "vs_filter_wide_sets": (_c_int, [_i64p, _i64p]),
 }
 
 _lock = threading.Lock()
@@ -204,6 +205,16 @@ def filter_wide_stats() -> int:
     w = ctypes.c_int64(0)
     check(load().vs_filter_wide_stats(ctypes.byref(w)))
     return w.value
+
+
+def filter_wide_sets():
+    """(entries, rescored): wide-set entries summed over the wide-checked
+    queries, and how many of them were read again and rescored, since the last
+    filter_stats reset (read them before that reset)."""
+    e = ctypes.c_int64(0)
+    r = ctypes.c_int64(0)
+    check(load().vs_filter_wide_sets(ctypes.byref(e), ctypes.byref(r)))
+    return e.value, r.value
 
 
 def filter_second_stats() -> int:

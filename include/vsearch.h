@@ -213,6 +213,10 @@ int vs_filter_wide_stats(int64_t* wide);
 /* Queries the staged engine handed from the int8 plane to the bf16 plane since
  * the last vs_filter_stats reset.  Diagnostic only: no reference interface. */
 int vs_filter_second_stats(int64_t* second);
+/* Entries the wide checks examined (summed over queries) and how many of them
+ * were read from HBM and rescored (the rest reuse the first check's exact keys),
+ * since the last vs_filter_stats reset.  Diagnostic only: no reference interface. */
+int vs_filter_wide_sets(int64_t* entries, int64_t* rescored);
 int vs_timer_reset(void);
 int vs_timer_read(double* total_ms, int64_t* launches);
 /* The same for the spans of one kernel name only (the filter engine's first

@@ -212,3 +212,41 @@ def test_wide_threshold_below_the_floor_is_exact():
             np.testing.assert_array_equal(top, exact)
     assert accepted == 80
     assert max(sizes) < 128 * 8
+
+
+def test_wide_threshold_from_first_check_exact_keys():
+    """The tighter wide threshold (verify_wide_kernel): e1_M, the M-th exact key
+    among the first check's KF best-approximate rows, bounds the true E_M from
+    above, so T' = min(T, a_M + 2.000001 B, e1_M + 1.000001 B) keeps every row
+    outside S at an exact key > e1_M >= E_M; the M rows behind e1_M are in S.
+    The check passes whenever T' < T, S holds the exact top-M, and S is about
+    half the size the a_M + 2B window gives.  Errors here sit at the bound's
+    edges (+-B) as well as inside it."""
+    rng = np.random.default_rng(7)
+    B, M, KF = 1e-3, 19, 32
+    tight, loose = [], []
+    for q in range(80):
+        n = 4000
+        e = rng.standard_normal(n) * 0.01
+        err = rng.uniform(-B, B, n)
+        edge = rng.random(n) < 0.3
+        err[edge] = np.where(rng.random(edge.sum()) < 0.5, -B, B)
+        a = e + err
+        lists = _lane_lists(a, 128, 8, rng)
+        full = [lst for lst in lists if len(lst) == 8]
+        T = min(a[lst[-1]] for lst in full)
+        entries = np.concatenate(lists)
+        first = entries[np.lexsort((entries, a[entries]))[:KF]]
+        aM = np.sort(a[entries])[M - 1]
+        e1M = np.sort(e[first])[M - 1]
+        Tp = min(T, aM + 2.000001 * B, e1M + 1.000001 * B)
+        S = [r for r in entries if a[r] < Tp]
+        ok, top = _accept(S, Tp, e, B, M)
+        if Tp < T:
+            assert ok
+        assert ok
+        exact = np.lexsort((np.arange(n), e))[:M]
+        np.testing.assert_array_equal(top, exact)
+        tight.append(len(S))
+        loose.append(sum(1 for r in entries if a[r] < min(T, aM + 2.000001 * B)))
+    assert np.mean(tight) < 0.75 * np.mean(loose)
