@@ -7,9 +7,9 @@
 // writes caller-allocated D/I, remove_ids compacts stably.
 //
 // Concurrency follows faiss's contract (concurrent searches allowed, add/remove
-// exclusive): a shared_mutex guards the storage; per-call scratch comes from the
-// stream-ordered allocator so concurrent searches on different streams never
-// share workspace.
+// exclusive): a shared_mutex guards the storage; per-call scratch comes from a
+// chunk cache whose chunks carry the event of their last use, so a search on
+// another stream waits (on the device) before it reuses one.
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -110,19 +110,131 @@ struct DeviceGuard {
 
 // Stream-ordered scratch allocation, released on scope exit (on the same stream;
 // the device's default pool keeps the memory cached, vs_create).
+// Scratch chunks (vs_internal.h): power-of-two sizes from 64 MB, kept after
+// use with the event of their last use; a taker's stream waits on that event
+// (a device-side wait).  The stream-ordered allocator cost ~76 us of host time
+// per hipFreeAsync at C2 (the search loop was host-bound: 2.6 ms of host per
+// 2.45 ms of kernels) and ~12 ms per call on C4's large lists (rocprofv3
+// --hip-trace, profiles/r02zl, r02zm).
+}  // namespace (the chunk cache is shared with vs_support.hip)
+
+namespace {
+std::mutex g_chunk_mu;
+std::vector<ScratchChunk> g_chunk_idle;
+size_t g_chunk_idle_bytes = 0;
+constexpr size_t kChunkMin = size_t(64) << 20;
+constexpr size_t kChunkIdleCap = size_t(16) << 30;  // per process
+}  // namespace
+
+namespace vs {
+void scratch_trim() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::vector<ScratchChunk> drop;
+  {
+    std::lock_guard<std::mutex> g(g_chunk_mu);
+    for (size_t i = 0; i < g_chunk_idle.size();) {
+      if (g_chunk_idle[i].dev == dev) {
+        drop.push_back(g_chunk_idle[i]);
+        g_chunk_idle_bytes -= g_chunk_idle[i].size;
+        g_chunk_idle[i] = g_chunk_idle.back();
+        g_chunk_idle.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+  if (drop.empty()) return;
+  (void)hipDeviceSynchronize();
+  for (auto& c : drop) {
+    (void)hipFree(c.p);
+    (void)hipEventDestroy(c.ev);
+  }
+}
+
+hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
+  size_t sz = kChunkMin;
+  while (sz < bytes) sz <<= 1;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    std::lock_guard<std::mutex> g(g_chunk_mu);
+    for (size_t i = 0; i < g_chunk_idle.size(); ++i) {
+      if (g_chunk_idle[i].dev == dev && g_chunk_idle[i].size == sz) {
+        *out = g_chunk_idle[i];
+        g_chunk_idle[i] = g_chunk_idle.back();
+        g_chunk_idle.pop_back();
+        g_chunk_idle_bytes -= sz;
+        return hipStreamWaitEvent(st, out->ev, 0);
+      }
+    }
+  }
+  ScratchChunk c;
+  c.size = sz;
+  c.dev = dev;
+  e = hipMalloc(&c.p, sz);
+  if (e != hipSuccess) {  // idle chunks of other sizes may hold the memory
+    (void)hipGetLastError();
+    scratch_trim();
+    e = hipMalloc(&c.p, sz);
+    if (e != hipSuccess) return e;
+  }
+  e = hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    (void)hipFree(c.p);
+    return e;
+  }
+  *out = c;
+  return hipSuccess;
+}
+
+void scratch_chunk_put(const ScratchChunk& c, hipStream_t st) {
+  if (!c.p) return;
+  (void)hipEventRecord(c.ev, st);
+  {
+    std::lock_guard<std::mutex> g(g_chunk_mu);
+    if (g_chunk_idle_bytes + c.size <= kChunkIdleCap) {
+      g_chunk_idle.push_back(c);
+      g_chunk_idle_bytes += c.size;
+      return;
+    }
+  }
+  (void)hipEventSynchronize(c.ev);
+  (void)hipFree(c.p);
+  (void)hipEventDestroy(c.ev);
+}
+}  // namespace vs
+
+namespace {
+
+// Per-call scratch: bump allocation from cached chunks, returned at scope end.
 struct Scratch {
+  static constexpr size_t kAlign = 256;
   hipStream_t st;
-  std::vector<void*> ptrs;
+  std::vector<ScratchChunk> chunks;
+  char* cur = nullptr;
+  size_t left = 0;
   explicit Scratch(hipStream_t s) : st(s) {}
   hipError_t alloc(void** p, size_t bytes) {
     *p = nullptr;
     if (bytes == 0) return hipSuccess;
-    hipError_t e = hipMallocAsync(p, bytes, st);
-    if (e == hipSuccess) ptrs.push_back(*p);
-    return e;
+    bytes = (bytes + kAlign - 1) & ~(kAlign - 1);
+    if (bytes > left) {
+      ScratchChunk c;
+      hipError_t e = scratch_chunk_get(bytes, st, &c);
+      if (e != hipSuccess) return e;
+      chunks.push_back(c);
+      cur = (char*)c.p;
+      left = c.size;
+    }
+    *p = cur;
+    cur += bytes;
+    left -= bytes;
+    return hipSuccess;
   }
   ~Scratch() {
-    for (void* p : ptrs) (void)hipFreeAsync(p, st);
+    for (auto& c : chunks) scratch_chunk_put(c, st);
   }
 };
 
@@ -288,6 +400,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     return e;
   };
   hipError_t e = allocate(cap);
+  if (e != hipSuccess) scratch_trim(), e = allocate(cap);  // cached scratch chunks first
   if (e != hipSuccess) {  // retry without the growth headroom
     cap = need;
     e = allocate(cap);

@@ -170,6 +170,20 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // are reused instead of read again.  sizes (optional): += the wide-set entries
 // and the rescored ones.
 constexpr int kWideCap = 2048;
+
+// Scratch chunks (vs_api.hip): device memory of at least `bytes` whose previous
+// use the taker's stream `st` waits for; put records the chunk's last use on
+// `st` and keeps it for the next taker.  scratch_trim frees the idle chunks of
+// the current device (synchronising it).
+struct ScratchChunk {
+  void* p = nullptr;
+  size_t size = 0;
+  int dev = 0;
+  hipEvent_t ev = nullptr;
+};
+hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out);
+void scratch_chunk_put(const ScratchChunk& c, hipStream_t st);
+void scratch_trim();
 hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
                               int M, const float* X, const float* xn, const float* Q,
                               const float* qn, int64_t ld, const BoundArgs& ba,

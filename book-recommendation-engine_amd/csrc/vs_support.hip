@@ -182,21 +182,24 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
   const int* ci = part.id;
   int P = part.P;
   int KL = part.KL > 0 ? part.KL : KP;
-  void* tmp[2] = {nullptr, nullptr};
-  int cur = 0;
+  // one stream-ordered buffer for every level (each level writes its own
+  // slice): one allocation and one free per merge
+  size_t total = 0;
+  for (int p = P; p > 64; p = (p + 63) / 64) total += (size_t)nq * ((p + 63) / 64) * KP;
+  ScratchChunk chunk;
   hipError_t e = hipSuccess;
+  if (total) e = scratch_chunk_get(total * (sizeof(float) + sizeof(int)), st, &chunk);
+  float* okb = (float*)chunk.p;
+  int* oib = (int*)(okb + total);
   while (P > 64 && e == hipSuccess) {
     const int P2 = (P + 63) / 64;
-    void* buf = nullptr;
-    e = hipMallocAsync(&buf, (size_t)nq * P2 * KP * (sizeof(float) + sizeof(int)), st);
-    if (e != hipSuccess) break;
-    float* ok = (float*)buf;
-    int* oi = (int*)(ok + (size_t)nq * P2 * KP);
+    float* ok = okb;
+    int* oi = oib;
+    okb += (size_t)nq * P2 * KP;
+    oib += (size_t)nq * P2 * KP;
     hipLaunchKernelGGL((merge_lists_kernel<KP>), dim3(nq, P2), dim3(64), 0, st, ck, ci, P, KL, ok,
                        oi, P2, 0, k, mode, raw, id_base, min_score, D, I, ldo, qlist, qcount);
     e = hipGetLastError();
-    if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
-    tmp[cur] = buf;
     ck = ok;
     ci = oi;
     P = P2;
@@ -208,7 +211,7 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
                        I, ldo, qlist, qcount);
     e = hipGetLastError();
   }
-  if (tmp[cur]) (void)hipFreeAsync(tmp[cur], st);
+  scratch_chunk_put(chunk, st);
   return e;
 }
 
