@@ -85,4 +85,24 @@ __device__ __forceinline__ void merge2_sorted(const float* ak, const IdT* ai, co
   }
 }
 
+// The same for the first `lim` outputs only (both inputs hold at least `lim`
+// written entries, padded with empty ones); outputs past lim are left as they are.
+template <int KP, typename IdT>
+__device__ __forceinline__ void merge2_sorted_n(const float* ak, const IdT* ai, const float* bk,
+                                                const IdT* bi, float (&ok)[KP], IdT (&oi)[KP],
+                                                int lim) {
+  int ia = 0, ib = 0;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    if (j >= lim) break;
+    const float ka = ak[ia], kb = bk[ib];
+    const IdT xa = ai[ia], xb = bi[ib];
+    const bool ta = !lex_less(kb, xb, ka, xa);
+    ok[j] = ta ? ka : kb;
+    oi[j] = ta ? xa : xb;
+    ia += ta ? 1 : 0;
+    ib += ta ? 0 : 1;
+  }
+}
+
 }  // namespace vs

@@ -25,24 +25,32 @@ namespace vs {
 // 6-round pairwise merge through LDS.  Output keys are mapped back to scores.
 template <int KP, typename IdT>
 __device__ __forceinline__ void wave_tree_merge(float (&lk)[KP], IdT (&li)[KP], float* sk,
-                                                IdT* si, int lane) {
+                                                IdT* si, int lane, int nvalid = 64,
+                                                int len0 = KP) {
   // sk/si: LDS [64][KP + 1] (the odd row stride spreads the active lanes' rows
   // over all banks; a stride of KP put every even lane on one bank); on return
-  // lane 0 holds the merge of the 64 lists.
+  // lane 0 holds the merge of the 64 lists.  Only lanes < nvalid hold entries
+  // (rounds past them are skipped), each at most len0 (the rest empty): a
+  // round's lists hold at most `len` entries, so it writes and merges 2 len.
   constexpr int KS = KP + 1;
-  for (int step = 1; step < 64; step <<= 1) {
+  // (KP = 64 keeps full-length rounds: the bounded form spills there)
+  int len = KP <= 32 && len0 < KP ? len0 : KP;
+  for (int step = 1; step < 64 && step < nvalid; step <<= 1) {
+    const int lim = 2 * len < KP ? 2 * len : KP;
     if ((lane & (step - 1)) == 0) {
 #pragma unroll
       for (int j = 0; j < KP; ++j) {
+        if (j >= lim) break;
         sk[lane * KS + j] = lk[j];
         si[lane * KS + j] = li[j];
       }
     }
     __syncthreads();
     if ((lane & (2 * step - 1)) == 0)
-      merge2_sorted<KP, IdT>(sk + lane * KS, si + lane * KS, sk + (lane + step) * KS,
-                             si + (lane + step) * KS, lk, li);
+      merge2_sorted_n<KP, IdT>(sk + lane * KS, si + lane * KS, sk + (lane + step) * KS,
+                               si + (lane + step) * KS, lk, li, lim);
     __syncthreads();
+    len = lim;
   }
 }
 
@@ -147,7 +155,7 @@ __global__ __launch_bounds__(64) void merge_lists_kernel(
       li[4 * j + 3] = iv.w;
     }
   }
-  wave_tree_merge<KP, int>(lk, li, sk, si, lane);
+  wave_tree_merge<KP, int>(lk, li, sk, si, lane, P - g * 64 < 64 ? P - g * 64 : 64, KL);
   if (!emit) {
     if (lane == 0) {
       float* ok = okey + ((int64_t)q * P2 + g) * KP;
