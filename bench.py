@@ -140,17 +140,30 @@ def parse(argv=None):
 
 
 def pmc_traffic(workload: str, kernel_prefix: str, must_contain: str = ""):
-    """HBM bytes per launch of `kernel_prefix` from the newest PMC summary in profiles/
-    (names containing `must_contain`: the x1 kernel's plane)."""
+    """HBM bytes per launch of the benched kernel from the newest PMC summary in
+    profiles/ (tools/pmc_summary.py).  Among the instantiations whose full
+    rocprof name starts with `kernel_prefix` and contains `must_contain` (the
+    x1 kernel's plane), and among each one's launch geometries (grid sizes:
+    full passes vs the staged engine's small gathered ones), the (name, grid)
+    with the most dispatches is the dominant kernel; its bytes are returned
+    with a source string naming the file, the full name, the grid and the
+    dispatch count."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{workload}.json")))
-    if not files:
-        return None, None
-    for path in reversed(files):  # newest tag first; the first summary naming the kernel wins
+    for path in reversed(files):  # newest tag first
         with open(path, encoding="utf-8") as f:
             summ = json.load(f)
+        best = None
         for name, rec in summ.get("kernels", {}).items():
-            if name.startswith(kernel_prefix) and must_contain in name:
-                return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+            if not (name.startswith(kernel_prefix) and must_contain in name):
+                continue
+            groups = rec.get("by_grid") or {"?": rec}
+            for grid, g in groups.items():
+                if best is None or g["dispatches"] > best[0]:
+                    best = (g["dispatches"], g["hbm_bytes_per_launch"], name, grid)
+        if best is not None:
+            n, hbm, name, grid = best
+            return hbm, (f"{os.path.relpath(path, ROOT)}: {name.split('(')[0]} grid {grid}, "
+                         f"{n} dispatches")
     return None, None
 
 
@@ -170,17 +183,26 @@ def cpu_baseline(shard, args, xq_host):
     dt = time.perf_counter() - t0
     threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     qps_full = xq.shape[0] / dt * n / args.ntotal
+    affinity = len(os.sched_getaffinity(0))
     res = {
         "value": round(qps_full, 3),
         "unit": "queries/s",
         "cores": int(threads),
+        # the BLAS pool runs at the thread count the GPU pool grants one GPU's job
+        # (OMP_NUM_THREADS, set by the box; its rules: "leave them", worker pools
+        # sized to the box's CPU share, 16 per GPU) although the affinity mask
+        # shows every host CPU; the all-CPU figure is a linear extrapolation
+        "thread_cap": {"threads_used": int(threads),
+                       "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+                       "reason": "the GPU pool's CPU share for a one-GPU job"},
+        "value_all_host_cpus_extrapolated": round(qps_full * affinity / max(1, int(threads)), 3),
         "kind": "port",
         "sample": f"{xq.shape[0]} queries x {n} rows (first rows of the same corpus), "
                   f"{dt:.2f} s; extrapolated x{n}/{args.ntotal} rows (flat scan is linear in N)",
         "impl": "oracle/flat.py knn_faiss_fp32: faiss BLAS branch restated "
                 "(numpy sgemm blocks + top-k), faiss-cpu not installable offline",
         "cpu_model": cpu_model(),
-        "host_cpus_affinity": len(os.sched_getaffinity(0)),
+        "host_cpus_affinity": affinity,
     }
     # the reference's live shape: one query (mcp_book_server.py:142 -> faiss
     # sequential branch, nq < 20: one thread scans every row with a size-k heap)

@@ -72,6 +72,15 @@ struct vs_index {
   } ad;
   int engine = VS_ENGINE_AUTO;
   std::shared_mutex mu;
+  // Completion marks of the calls that read this index's storage on the
+  // device: one event per stream a search / self-join / device reconstruct ran
+  // on, recorded after its last launch.  Writers that move or free the storage
+  // (growth, remove_ids, reset, destroy) wait for these marks only — not for
+  // the whole device, where other indexes' searches may be running (faiss's
+  // contract: a writer excludes the readers of its own index).
+  std::mutex rd_mu;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
+  hipStream_t wst = nullptr;  // the index's own (non-blocking) writer stream
 };
 
 namespace {
@@ -107,6 +116,58 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+// Records a reader mark of `idx` on `st` when it leaves scope (after the
+// caller's last launch on st; also on an error return).
+struct ReaderMark {
+  vs_index* idx;
+  hipStream_t st;
+  ReaderMark(vs_index* i, hipStream_t s) : idx(i), st(s) {}
+  ~ReaderMark() {
+    std::lock_guard<std::mutex> g(idx->rd_mu);
+    for (auto& r : idx->readers)
+      if (r.first == st) {
+        (void)hipEventRecord(r.second, st);
+        return;
+      }
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(st);  // no mark possible: finish the work instead
+      return;
+    }
+    (void)hipEventRecord(ev, st);
+    idx->readers.emplace_back(st, ev);
+  }
+};
+
+// Waits (host) until every reader mark of `idx` has completed.  Called with
+// the index's writer lock held, so no new reader can start meanwhile.
+hipError_t wait_readers(vs_index* idx) {
+  std::lock_guard<std::mutex> g(idx->rd_mu);
+  for (auto& r : idx->readers) {
+    hipError_t e = hipEventSynchronize(r.second);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// The index's writer stream (created on first use): non-blocking, so it never
+// serialises with the legacy null stream's users, and of the greatest
+// priority, which gives it a hardware queue of its own — streams of one
+// priority share the process's few hardware queues (GPU_MAX_HW_QUEUES), and a
+// shared queue would run the writer behind another stream's search queue.
+hipError_t writer_stream(vs_index* idx, hipStream_t* out) {
+  if (!idx->wst) {
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    e = hipStreamCreateWithPriority(&idx->wst, hipStreamNonBlocking, greatest);
+    if (e != hipSuccess) return e;
+  }
+  *out = idx->wst;
+  return hipSuccess;
+}
 
 // Stream-ordered scratch allocation, released on scope exit (on the same stream;
 // the device's default pool keeps the memory cached, vs_create).
@@ -145,7 +206,7 @@ void scratch_trim() {
     }
   }
   if (drop.empty()) return;
-  (void)hipDeviceSynchronize();
+  for (auto& c : drop) (void)hipEventSynchronize(c.ev);  // each chunk's last use
   for (auto& c : drop) {
     (void)hipFree(c.p);
     (void)hipEventDestroy(c.ev);
@@ -158,7 +219,39 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
+  // An idle chunk last used on this stream needs no wait (stream order), one
+  // whose last use has completed needs none either; a chunk still in use on
+  // another stream would tie this call to that stream's queue (another
+  // index's long searches, say), so a new chunk is allocated instead while
+  // memory allows, and only then is the busy one taken with a device-side wait.
+  int busy = -1;
   {
+    std::lock_guard<std::mutex> g(g_chunk_mu);
+    int pick = -1;
+    for (size_t i = 0; i < g_chunk_idle.size(); ++i) {
+      const ScratchChunk& c = g_chunk_idle[i];
+      if (c.dev != dev || c.size != sz) continue;
+      if (c.st == st || hipEventQuery(c.ev) == hipSuccess) {
+        pick = (int)i;
+        break;
+      }
+      if (busy < 0) busy = (int)i;
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    if (pick >= 0) {
+      *out = g_chunk_idle[pick];
+      g_chunk_idle[pick] = g_chunk_idle.back();
+      g_chunk_idle.pop_back();
+      g_chunk_idle_bytes -= sz;
+      return out->st == st ? hipSuccess : hipStreamWaitEvent(st, out->ev, 0);
+    }
+  }
+  ScratchChunk c;
+  c.size = sz;
+  c.dev = dev;
+  e = hipMalloc(&c.p, sz);
+  if (e != hipSuccess && busy >= 0) {  // short of memory: wait for the busy chunk
+    (void)hipGetLastError();
     std::lock_guard<std::mutex> g(g_chunk_mu);
     for (size_t i = 0; i < g_chunk_idle.size(); ++i) {
       if (g_chunk_idle[i].dev == dev && g_chunk_idle[i].size == sz) {
@@ -170,14 +263,17 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
       }
     }
   }
-  ScratchChunk c;
-  c.size = sz;
-  c.dev = dev;
-  e = hipMalloc(&c.p, sz);
   if (e != hipSuccess) {  // idle chunks of other sizes may hold the memory
     (void)hipGetLastError();
     scratch_trim();
     e = hipMalloc(&c.p, sz);
+  }
+  if (e != hipSuccess) {  // the power-of-two rounding may be what does not fit
+    (void)hipGetLastError();
+    const size_t exact = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    if (exact >= sz) return e;
+    c.size = exact;
+    e = hipMalloc(&c.p, exact);
     if (e != hipSuccess) return e;
   }
   e = hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
@@ -189,8 +285,10 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
   return hipSuccess;
 }
 
-void scratch_chunk_put(const ScratchChunk& c, hipStream_t st) {
-  if (!c.p) return;
+void scratch_chunk_put(const ScratchChunk& c0, hipStream_t st) {
+  if (!c0.p) return;
+  ScratchChunk c = c0;
+  c.st = st;
   (void)hipEventRecord(c.ev, st);
   {
     std::lock_guard<std::mutex> g(g_chunk_mu);
@@ -370,6 +468,9 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   char* fplane[2] = {nullptr, nullptr};
   float* rn2[2] = {nullptr, nullptr};
   float* fscale = nullptr;
+  // the planes the new storage keeps: committed to the index only once the
+  // allocation succeeded (a failed growth leaves the index as it was)
+  bool on[2] = {idx->plane_on[0], idx->plane_on[1]};
   auto release = [&]() {
     if (codes) (void)hipFree(codes);
     if (norms) (void)hipFree(norms);
@@ -388,10 +489,10 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     hipError_t e = hipMalloc(&codes, (size_t)c * idx->rowbytes());
     if (e == hipSuccess) e = hipMalloc(&norms, (size_t)c * sizeof(float));
     for (int p = 0; p < 2; ++p) {
-      if (e == hipSuccess && idx->plane_on[p]) e = hipMalloc(&fplane[p], (size_t)c * idx->planebytes(p));
-      if (e == hipSuccess && idx->plane_on[p]) e = hipMalloc(&rn2[p], (size_t)c * sizeof(float));
+      if (e == hipSuccess && on[p]) e = hipMalloc(&fplane[p], (size_t)c * idx->planebytes(p));
+      if (e == hipSuccess && on[p]) e = hipMalloc(&rn2[p], (size_t)c * sizeof(float));
     }
-    if (e == hipSuccess && idx->plane_on[FILTER_I8])
+    if (e == hipSuccess && on[FILTER_I8])
       e = hipMalloc(&fscale, (size_t)c * sizeof(float));
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -409,16 +510,16 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   // product index holds 10 B per element with both planes, 7 with int8 only,
   // 4 without; searches then use the plane that remains, or the exact fp32
   // engine): bf16 first, then every plane.
-  if (e != hipSuccess && idx->plane_on[FILTER_BF16] && idx->plane_on[FILTER_I8]) {
-    idx->plane_on[FILTER_BF16] = false;
+  if (e != hipSuccess && on[FILTER_BF16] && on[FILTER_I8]) {
+    on[FILTER_BF16] = false;
     e = allocate(cap);
   }
-  if (e != hipSuccess && (idx->plane_on[FILTER_BF16] || idx->plane_on[FILTER_I8])) {
-    idx->plane_on[FILTER_BF16] = idx->plane_on[FILTER_I8] = false;
+  if (e != hipSuccess && (on[FILTER_BF16] || on[FILTER_I8])) {
+    on[FILTER_BF16] = on[FILTER_I8] = false;
     e = allocate(cap);
   }
   if (e != hipSuccess) return hip_fail(e, "vs: allocating row storage");
-  const bool i8 = idx->plane_on[FILTER_I8];
+  const bool i8 = on[FILTER_I8];
   // zero every tail (tile reads past ntotal must see zeros, never NaN garbage)
   const int64_t keep = idx->ntotal;
   VS_HIP(hipMemsetAsync(codes + keep * idx->rowbytes(), 0, (size_t)(cap - keep) * idx->rowbytes(),
@@ -427,7 +528,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   VS_HIP(hipMemsetAsync(norms + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
          "vs: zeroing norms");
   for (int p = 0; p < 2; ++p) {
-    if (!idx->plane_on[p]) continue;
+    if (!on[p]) continue;
     const int64_t pb = idx->planebytes(p);
     VS_HIP(hipMemsetAsync(fplane[p] + keep * pb, 0, (size_t)(cap - keep) * pb, st),
            "vs: zeroing plane");
@@ -445,7 +546,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
                           hipMemcpyDeviceToDevice, st),
            "vs: copying norms");
     for (int p = 0; p < 2; ++p) {
-      if (!idx->plane_on[p]) continue;
+      if (!on[p]) continue;
       VS_HIP(hipMemcpyAsync(fplane[p], idx->fplane[p], (size_t)keep * idx->planebytes(p),
                             hipMemcpyDeviceToDevice, st),
              "vs: copying plane");
@@ -458,9 +559,13 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
                             hipMemcpyDeviceToDevice, st),
              "vs: copying scales");
   }
-  // In-flight searches (any stream) may still read the old storage.
-  VS_HIP(hipDeviceSynchronize(), "vs: storage growth");
+  // The copies above, and searches of this index still in flight (any
+  // stream), read the old storage; other indexes' work is not waited for.
+  VS_HIP(hipStreamSynchronize(st), "vs: storage growth");
+  VS_HIP(wait_readers(idx), "vs: storage growth");
   free_storage(idx);
+  idx->plane_on[0] = on[0];
+  idx->plane_on[1] = on[1];
   idx->codes = codes;
   idx->norms = norms;
   for (int p = 0; p < 2; ++p) {
@@ -541,6 +646,8 @@ int run_gemm(vs_index* idx, const SearchArgs& a, int need, hipStream_t st,
 }
 
 int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st);
+int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
+                      hipStream_t st, const int* gl, const int* gc);
 
 // The filter-and-verify engine (vs_gemm_x1.hip), entirely stream-ordered, as a
 // chain of stages over the planes the index holds (int8, then bf16):
@@ -747,10 +854,77 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, true, true, next, qcount + 1);
   }
   // the exact redo (untimed: the kernel timer holds the first filter pass)
-  SearchArgs ex = a;
-  ex.qbuf = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
-  ex.nq_pad = (int)round_up(a.nq, kBQ);
-  return run_gemm(idx, ex, need, st, next, qcount + 1);
+  return run_gemm_rescored(idx, a, need, KF, plane, st, next, qcount + 1);
+}
+
+// The staged engine's last stage: the exact fp32 MFMA GEMM over the queries no
+// filter stage settled (gathered: gl[0 .. *gc) of `a`) keeps KF candidates per
+// query, which are rescored like every other stage's (verify_rescore: fp64
+// sums, one rounding), so every key the staged engine returns is the fp32
+// rounding of the exact score (oracle/flat.py key_window).  The check verify
+// computes is not used here: this is the last stage.
+int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
+                      hipStream_t st, const int* gl, const int* gc) {
+  const int ntotal = (int)idx->ntotal;
+  const int KP = kp_for(KF);
+  const int nslot = (int)round_up(a.nq, kBQ);
+  Partials part;
+  part.KP = KP;
+  const int ntiles = (ntotal + kBN - 1) / kBN;
+  const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, 256));
+  part.P = 2 * nsplit;
+  // The gathered queries run in slot windows of at most `cap` slots, so the
+  // lists stay within ~1 GB whatever the batch (a 65,536-student self-join
+  // chunk at KP = 64 would need 16 GB for every slot at once); windows past
+  // the device-side count exit at once (usually all but the first).
+  const int cap = (int)std::min<int64_t>(
+      nslot, std::max<int64_t>(kBQ, ((int64_t)1 << 30) / ((int64_t)part.P * KP * 8) / kBQ * kBQ));
+  Scratch scr(st);
+  const size_t n = (size_t)cap * part.P * KP;
+  VS_HIP(scr.alloc((void**)&part.key, n * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&part.id, n * sizeof(int)), "vs: scratch");
+  float *qc = nullptr, *ac = nullptr;
+  int* qrow = nullptr;
+  VS_HIP(scr.alloc((void**)&qc, (size_t)cap * idx->ld * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&ac, (size_t)cap * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qrow, (size_t)cap * sizeof(int)), "vs: scratch");
+  float* Dk = nullptr;
+  int64_t* Ik = nullptr;
+  VS_HIP(scr.alloc((void**)&Dk, (size_t)cap * KF * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&Ik, (size_t)cap * KF * sizeof(int64_t)), "vs: scratch");
+  Partials vp;
+  vp.KP = KP;
+  vp.P = 1;
+  int* flags = nullptr;
+  int* wc = nullptr;
+  VS_HIP(scr.alloc((void**)&vp.key, (size_t)cap * KP * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&vp.id, (size_t)cap * KP * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&flags, (size_t)cap * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
+  const float* Qa = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
+  const float* qinv = a.mode == MODE_COS ? ac : nullptr;
+  const float* xinv = a.mode == MODE_COS ? a.xaux : nullptr;
+  for (int w0 = 0; w0 < nslot; w0 += cap) {
+    const int* wl = gl + w0;  // this window's query ids, wc[0] of them
+    VS_HIP(launch_window_count(gc, w0, cap, wc, st), "vs: window");
+    VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, Qa, a.qaux, idx->ld, idx->esize, ntotal,
+                            cap, nsplit, a.self0, part, st, wl, wc),
+           "vs: gemm_topk launch");
+    // the window's query rows and aux values, slot by slot, for the rescoring
+    VS_HIP(launch_gather_queries(Qa, idx->ld, a.qaux, wl, wc, cap, a.self0, qc, ac, qrow, st),
+           "vs: gathered queries");
+    VS_HIP(launch_merge_partials(MODE_L2, part, cap, KF, 0, 0.0f, Dk, Ik, KF, st, 0, nullptr, wc),
+           "vs: merge");
+    VS_HIP(launch_verify_rescore(a.mode, cap, KF, need, Dk, Ik, (const float*)idx->codes,
+                                 idx->norms, qc, ac, idx->ld, make_bound_args(idx->ld, plane),
+                                 idx->bstats[plane], part, KP, vp.key, vp.id, vp.KP, flags, st,
+                                 qinv, xinv, nullptr, wc),
+           "vs: rescore");
+    VS_HIP(launch_merge_partials(a.mode, vp, cap, a.k, idx->id_base, a.min_score, a.D, a.I, a.k,
+                                 st, a.raw, wl, wc),
+           "vs: merge");
+  }
+  return VS_OK;
 }
 
 // Fraction of int8-stage queries handed on to bf16 above which the int8 stage
@@ -973,8 +1147,12 @@ int vs_destroy(vs_index* idx) {
   if (!idx) return VS_OK;
   {
     DeviceGuard g(idx->device);
-    (void)hipDeviceSynchronize();
+    (void)wait_readers(idx);
+    if (idx->wst) (void)hipStreamSynchronize(idx->wst);
     free_storage(idx);
+    for (auto& r : idx->readers) (void)hipEventDestroy(r.second);
+    idx->readers.clear();
+    if (idx->wst) (void)hipStreamDestroy(idx->wst);
     for (int p = 0; p < 2; ++p)
       if (idx->bstats[p]) (void)hipFree(idx->bstats[p]);
     if (idx->ad.dcount) (void)hipFree(idx->ad.dcount);
@@ -1095,7 +1273,7 @@ int vs_reset(vs_index* idx) {
   if (!idx) return fail(VS_E_INVALID, "vs_reset: null index");
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
-  VS_HIP(hipDeviceSynchronize(), "vs_reset");
+  VS_HIP(wait_readers(idx), "vs_reset");
   free_storage(idx);
   for (int p = 0; p < 2; ++p)
     if (idx->bstats[p]) VS_HIP(hipMemset(idx->bstats[p], 0, 4 * sizeof(unsigned)), "vs_reset");
@@ -1169,6 +1347,7 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
   std::shared_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
   if (!g.ok) return fail(VS_E_HIP, "vs_search: hipSetDevice failed");
+  ReaderMark mark(idx, st);
   const bool out_dev = (flags & VS_OUT_DEVICE) != 0;
   const int mode = idx->metric == VS_METRIC_L2 ? MODE_L2 : MODE_IP;
   Scratch scr(st);
@@ -1260,6 +1439,7 @@ int vs_reconstruct_n(vs_index* idx, int64_t i0, int64_t n, float* out, int flags
   hipStream_t st = (hipStream_t)stream;
   std::shared_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
+  ReaderMark mark(idx, st);
   const hipMemcpyKind kind =
       (flags & VS_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
   if (idx->esize == 4) {
@@ -1307,9 +1487,11 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
   const int64_t nrem = (int64_t)rm.size();
   if (nrem == 0) return VS_OK;
   DeviceGuard g(idx->device);
-  // Searches already queued on other streams read the rows we are about to move.
-  VS_HIP(hipDeviceSynchronize(), "vs_remove_ids: drain");
+  // Searches of this index already queued on other streams read the rows we
+  // are about to move: wait for their marks (not for the device).
+  VS_HIP(wait_readers(idx), "vs_remove_ids: drain");
   hipStream_t st = nullptr;
+  VS_HIP(writer_stream(idx, &st), "vs_remove_ids: stream");
   Scratch scr(st);
   int64_t* drm = nullptr;
   VS_HIP(scr.alloc((void**)&drm, (size_t)nrem * sizeof(int64_t)), "vs_remove_ids: scratch");
@@ -1386,6 +1568,7 @@ int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_se
   hipStream_t st = (hipStream_t)stream;
   std::shared_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
+  ReaderMark mark(idx, st);
   const bool out_dev = (flags & VS_OUT_DEVICE) != 0;
   Scratch scr(st);
   float* Dd = D;

@@ -96,14 +96,16 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
     soff[par] = (uint32_t)(w * 32 + srow) * ldb + (uint32_t)c * 16u;
   }
   // query source offsets (per lane): contiguous tile rows, or the gathered rows
-  uint32_t qoff[4];
+  // (64-bit: a gathered row of a 65,536-query batch can sit past 4 GiB of
+  // query bytes once d * esize exceeds 64 KiB)
+  uint64_t qoff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (qlist) {
       const int slot = qt * kBQ + w * 32 + i * 8 + srow;
       const int src = qlist[min(slot, nf - 1)];
       const int row = (w * 4 + i) * 8 + srow;  // the LDS row decides the swizzle
-      qoff[i] = (uint32_t)src * ldb + (uint32_t)(sphys ^ ((row >> 1) & 7)) * 16u;
+      qoff[i] = (uint64_t)src * ldb + (uint32_t)(sphys ^ ((row >> 1) & 7)) * 16u;
     } else {
       qoff[i] = soff[i & 1] + (uint32_t)(i * 8) * ldb;
     }

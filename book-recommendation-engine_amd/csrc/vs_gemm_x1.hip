@@ -809,6 +809,17 @@ hipError_t launch_compose_list(const int* outer, const int* inner, const int* co
   return hipGetLastError();
 }
 
+__global__ void window_count_kernel(const int* __restrict__ count, int w0, int cap,
+                                    int* __restrict__ out) {
+  const int c = *count - w0;
+  *out = c < 0 ? 0 : (c > cap ? cap : c);
+}
+
+hipError_t launch_window_count(const int* count, int w0, int cap, int* out, hipStream_t st) {
+  hipLaunchKernelGGL(window_count_kernel, dim3(1), dim3(1), 0, st, count, w0, cap, out);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void mul_arrays_kernel(const float* __restrict__ a,
                                                          const float* __restrict__ b, int64_t n,
                                                          float* __restrict__ out) {
@@ -1144,8 +1155,9 @@ __global__ __launch_bounds__(1024) void compact_flags_kernel(const int* __restri
 // acc[0] += n, acc[1] += *count (one thread; a per-index record of a stage)
 __global__ void add_counts_kernel(const int* __restrict__ count, int n,
                                   unsigned long long* __restrict__ acc) {
-  acc[0] += (unsigned long long)n;
-  acc[1] += (unsigned long long)*count;
+  // atomic: searches of one index on two streams may run this concurrently
+  atomicAdd(acc + 0, (unsigned long long)n);
+  atomicAdd(acc + 1, (unsigned long long)*count);
 }
 
 hipError_t launch_add_counts(const int* count, int n, unsigned long long* acc, hipStream_t st) {

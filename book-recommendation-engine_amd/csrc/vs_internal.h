@@ -140,6 +140,9 @@ hipError_t launch_add_counts(const int* count, int n, unsigned long long* acc, h
 // out[j] = outer[inner[j]] for j < *count (j < n).
 hipError_t launch_compose_list(const int* outer, const int* inner, const int* count, int n,
                                int* out, hipStream_t st);
+// *out = clamp(*count - w0, 0, cap): the device-side count of one slot window
+// [w0, w0 + cap) of a gathered batch.
+hipError_t launch_window_count(const int* count, int w0, int cap, int* out, hipStream_t st);
 // out[i] = a[i] * b[i] (the int8 cosine's folded factors s / |x|).
 hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* out,
                              hipStream_t st);
@@ -180,6 +183,7 @@ struct ScratchChunk {
   size_t size = 0;
   int dev = 0;
   hipEvent_t ev = nullptr;
+  hipStream_t st = nullptr;  // the stream of its last use
 };
 hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out);
 void scratch_chunk_put(const ScratchChunk& c, hipStream_t st);

@@ -319,23 +319,28 @@ __global__ __launch_bounds__(256) void row_norms_kernel(const T* __restrict__ X,
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const uint4* xr = (const uint4*)(X + (r0 + row) * ld);
-  float s = 0.0f;
+  // fp64 sum of the exact squares, rounded once: |x|^2 correctly rounded to
+  // fp32 (up to the fp64 sum's 2^-53-level error), so an L2 key
+  // (|q|^2 + |x|^2) - 2 q.x carries only the roundings of its own formula
+  // (the strict tie window of oracle/flat.py key_window)
+  double s = 0.0;
   for (int64_t c = lane; c < ld / EPC; c += 64) {
     const uint4 v = xr[c];
     const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if constexpr (sizeof(T) == 4) {
-        const float f = __uint_as_float(u[i]);
-        s += f * f;
+        const double f = (double)__uint_as_float(u[i]);
+        s = fma(f, f, s);
       } else {
-        const float a = __uint_as_float(u[i] << 16), b = __uint_as_float(u[i] & 0xFFFF0000u);
-        s += a * a + b * b;
+        const double a = (double)__uint_as_float(u[i] << 16),
+                     b = (double)__uint_as_float(u[i] & 0xFFFF0000u);
+        s = fma(a, a, fma(b, b, s));
       }
     }
   }
-  s = wave_sum(s);
-  if (lane == 0) out[r0 + row] = s;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) out[r0 + row] = (float)s;
 }
 
 hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, int64_t n,

@@ -132,13 +132,16 @@ class IndexFlat(Index):
         return self.ntotal
 
     def __del__(self):
+        # no module-global lookups here: at interpreter exit `ctypes` may already
+        # be torn down; the handle object itself is cleared in place
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            try:
-                self._lib.vs_destroy(h)
-            except Exception:  # interpreter shutdown
-                pass
-            self._h = ctypes.c_void_p()
+        if h is None or not h.value:
+            return
+        try:
+            self._lib.vs_destroy(h)
+        except Exception:  # interpreter shutdown: the library may be gone
+            pass
+        h.value = None
 
     # -- mutation ---------------------------------------------------------------------
     def add(self, x) -> None:

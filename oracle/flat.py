@@ -212,7 +212,33 @@ def score_tolerance(metric: int, s_ref, xq_norm2=0.0, xb_norm2=0.0):
     return 1e-5 * scale
 
 
-def mismatches(D, I, Dr, Ir, metric: int, xb, xq, rtol: float = 1e-5):
+U32 = 2.0 ** -24  # unit roundoff of fp32
+
+
+def key_window(metric: int, s, qn2, xn2, d: int, cosine: bool = False):
+    """How far an engine key that is the fp32 ROUNDING of an exactly computed
+    score can sit from the fp64 score s (the filter-and-verify engine: fp64 sums
+    of the fp32 products, rounded once; vs_gemm_x1.hip exact_key; fp64-summed
+    norms, vs_support.hip row_norms_kernel):
+      IP      key = fl(s):                          U|s|
+      L2      key = fl(fl(fl(|q|^2) + fl(|x|^2)) - 2 fl(s)), clamped at 0:
+              every rounding acts on at most 2(|q|^2 + |x|^2):  5U(|q|^2 + |x|^2)
+      cosine  key = fl(fl(s) * fl(fl(1/|q|) * fl(1/|x|))): 6U|sim|
+    (taken as 6U / 8U), plus the fp64 sum's own d * 2^-52 |q||x|.  Two rows can
+    come out in either order only when their windows overlap: that is the tie
+    window the strict checks use (instead of the fp32 contract's 1e-5)."""
+    s = np.abs(np.asarray(s, dtype=np.float64))
+    qn2 = np.asarray(qn2, dtype=np.float64)
+    xn2 = np.asarray(xn2, dtype=np.float64)
+    floor = d * 2.0 ** -52 * np.sqrt(qn2 * xn2) + 1e-300
+    if cosine:
+        return 8 * U32 * s + d * 2.0 ** -52 + 1e-300
+    if metric == METRIC_L2:
+        return 6 * U32 * (qn2 + xn2) + 4 * floor
+    return U32 * s + floor
+
+
+def mismatches(D, I, Dr, Ir, metric: int, xb, xq, rtol: float = 1e-5, strict: bool = False):
     """Parity check of a (D, I) result against the fp64 oracle result (Dr, Ir).
 
     * every returned label is valid and unique per query, -1 exactly where the
@@ -220,6 +246,11 @@ def mismatches(D, I, Dr, Ir, metric: int, xb, xq, rtol: float = 1e-5):
     * D[q, j] within tolerance of the exact score of the returned label;
     * the returned label's exact score within tolerance of the oracle's j-th
       score (a different label is accepted only as a documented tie);
+    Tolerance: the north star's fp32 contract (1e-5 relative; for squared L2
+    the scale includes |q|^2 + |x|^2), or with ``strict`` the rounding window of
+    an exactly rescored key (key_window): D must be the fp32 rounding of the
+    label's exact score, and a different label is a tie only when the two exact
+    scores are within both windows — what the filter-and-verify engine proves.
     Returns a list of human-readable problems (empty = parity)."""
     xb = np.asarray(xb, dtype=np.float32)
     xq = np.asarray(xq, dtype=np.float32)
@@ -247,14 +278,49 @@ def mismatches(D, I, Dr, Ir, metric: int, xb, xq, rtol: float = 1e-5):
                     bad.append((q, j, "padding score", float(D[q, j])))
                 continue
             s_got = exact_scores(xb[ids[j]:ids[j] + 1], xq[q:q + 1], metric)[0, 0]
-            tol = score_tolerance(metric, s_got, nq2[q], nb2[ids[j]]) * (rtol / 1e-5)
+            if strict:
+                tol = float(key_window(metric, s_got, nq2[q], nb2[ids[j]], xb.shape[1]))
+            else:
+                tol = score_tolerance(metric, s_got, nq2[q], nb2[ids[j]]) * (rtol / 1e-5)
             if abs(float(D[q, j]) - s_got) > tol:
                 bad.append((q, j, "score", float(D[q, j]), float(s_got), float(tol)))
             if ids[j] != Ir[q, j]:
-                s_ref = float(Dr[q, j])
-                tol2 = score_tolerance(metric, s_ref, nq2[q], nb2[Ir[q, j]]) * (rtol / 1e-5)
+                s_ref = exact_scores(xb[Ir[q, j]:Ir[q, j] + 1], xq[q:q + 1], metric)[0, 0]
+                if strict:
+                    tol2 = tol + float(key_window(metric, s_ref, nq2[q], nb2[Ir[q, j]], xb.shape[1]))
+                else:
+                    tol2 = score_tolerance(metric, s_ref, nq2[q], nb2[Ir[q, j]]) * (rtol / 1e-5)
                 if abs(s_got - s_ref) > tol2:
-                    bad.append((q, j, "label", int(ids[j]), int(Ir[q, j]), s_got, s_ref))
+                    bad.append((q, j, "label", int(ids[j]), int(Ir[q, j]), s_got, s_ref, tol2))
+    return bad
+
+
+def selfjoin_mismatches(S, I, Sr, Ir, x, q_rows, strict: bool = False):
+    """Self-join check (pgvector cosine, exclude self) of (S, I) against the
+    oracle's (Sr, Ir) for query rows q_rows of x: labels equal except ties,
+    similarities within 1e-5 absolute, or with ``strict`` within the cosine
+    key window (key_window) of the returned label's exact similarity."""
+    x64 = np.asarray(x, dtype=np.float64)
+    nrm = np.sqrt(np.einsum("ij,ij->i", x64, x64))
+    d = x64.shape[1]
+    bad = []
+    for row, q in enumerate(np.asarray(q_rows)):
+        for j in range(I.shape[1]):
+            a, b = int(I[row, j]), int(Ir[row, j])
+            if (a < 0) != (b < 0):
+                bad.append((row, j, "padding", a, b))
+                continue
+            if a < 0:
+                continue
+            s_got = float(x64[q] @ x64[a]) / (nrm[q] * nrm[a])
+            tol = float(key_window(0, s_got, 0, 0, d, cosine=True)) if strict else 1e-5
+            if abs(float(S[row, j]) - s_got) > tol:
+                bad.append((row, j, "sim", float(S[row, j]), s_got, tol))
+            if a != b:
+                s_ref = float(x64[q] @ x64[b]) / (nrm[q] * nrm[b])
+                tol2 = tol + float(key_window(0, s_ref, 0, 0, d, cosine=True)) if strict else 1e-5
+                if abs(s_got - s_ref) > tol2 or a == int(q):
+                    bad.append((row, j, "label", a, b, s_got, s_ref))
     return bad
 
 

@@ -81,3 +81,82 @@ def oracle_merge(Dall, Iall, metric, k):
         D[q, :sel.size] = [s[pos[int(i)]] for i in sel]
         I[q, :sel.size] = sel
     return D, I
+
+
+def assert_against_candidates(D, I, cand, metric, k, d, strict):
+    """One query's result (D, I) against its proven candidate set cand =
+    (ids, fp64 scores, fp64 |x|^2, |q|^2): a set that provably holds the exact
+    top-k (every other row strictly worse).  Every returned label must be a
+    candidate, D[j] within the window of ITS OWN exact score, and a label that
+    differs from the oracle's j-th only inside both windows (a tie).  Window:
+    strict = the rounding of an exactly rescored key (flat.key_window), else the
+    north star's fp32 contract (flat.score_tolerance)."""
+    ids, exact, xn2, qn2 = cand
+    pos = {int(i): j for j, i in enumerate(ids)}
+    key = exact if metric == flat.METRIC_L2 else -exact
+    ref_i = flat.faiss_order(np.asarray(ids, dtype=np.int64), key, k, metric)
+    assert len(set(np.asarray(I).tolist())) == k
+
+    def window(r):
+        p = pos[int(r)]
+        if strict:
+            return float(flat.key_window(metric, exact[p], qn2, xn2[p], d))
+        return float(flat.score_tolerance(metric, exact[p], qn2, xn2[p]))
+
+    for j in range(k):
+        assert int(I[j]) in pos, (j, int(I[j]), "not among the proven candidates")
+        s_got = exact[pos[int(I[j])]]
+        assert abs(float(D[j]) - s_got) <= window(I[j]), (j, int(I[j]), float(D[j]), s_got,
+                                                          window(I[j]))
+        if I[j] != ref_i[j]:
+            s_ref = exact[pos[int(ref_i[j])]]
+            assert abs(s_got - s_ref) <= window(I[j]) + window(ref_i[j]), (
+                j, int(I[j]), int(ref_i[j]), s_got, s_ref)
+
+
+def proven_candidates(index, xs, metric, N, K, m=64, chunk=1_000_000):
+    """Per query of xs: the m best of the index's N rows (read back in chunks by
+    reconstruct_n, bit-exact) by fp32 sgemm, with their fp64 exact scores and
+    norms.  The margin between the K-th and the m-th sgemm score is checked
+    against the worst-case fp32 sgemm error (gamma(d) |q| max|x|), so the set
+    provably holds the exact top-K.  Returns (ids, exact, |x|^2, |q|^2) per
+    query (the form assert_against_candidates takes)."""
+    D_ = xs.shape[1]
+    nq = xs.shape[0]
+    best_s = np.full((nq, 0), -np.inf, np.float32)
+    best_i = np.zeros((nq, 0), np.int64)
+    xmax = 0.0
+    rows = {}
+    for r0 in range(0, N, chunk):
+        xb = index.reconstruct_n(r0, min(chunk, N - r0))
+        xmax = max(xmax, float(np.sqrt(np.einsum("ij,ij->i", xb, xb, dtype=np.float64).max())))
+        s = xs @ xb.T  # fp32 sgemm
+        if metric == flat.METRIC_L2:  # larger = better: 2 q.x - |x|^2 (|q|^2 is constant)
+            s = 2.0 * s - np.einsum("ij,ij->i", xb, xb, dtype=np.float64)[None, :]
+        s = np.asarray(s, np.float32)
+        allv = np.concatenate([best_s, s], axis=1)
+        alli = np.concatenate([best_i, np.broadcast_to(np.arange(r0, r0 + xb.shape[0]), s.shape)],
+                              axis=1)
+        part = np.argpartition(-allv, m - 1, axis=1)[:, :m]
+        best_s = np.take_along_axis(allv, part, axis=1)
+        best_i = np.take_along_axis(alli, part, axis=1)
+        for q in range(nq):  # keep the candidate rows for the exact rescoring
+            for r in best_i[q]:
+                if r0 <= r < r0 + xb.shape[0]:
+                    rows[int(r)] = xb[r - r0].copy()
+    res = []
+    u = 2.0 ** -24
+    gam = D_ * u / (1 - D_ * u)
+    for q in range(nq):
+        ids = best_i[q]
+        order = np.argsort(-best_s[q], kind="stable")
+        s_sorted = best_s[q][order]
+        qn = float(np.sqrt(np.dot(xs[q].astype(np.float64), xs[q].astype(np.float64))))
+        bound = 2.0 * gam * qn * xmax * (2.0 if metric == flat.METRIC_L2 else 1.0) + 1e-3
+        # fp32 preselection can only be wrong inside this margin
+        assert s_sorted[K - 1] - s_sorted[m - 1] > 2 * bound, (q, s_sorted[K - 1], s_sorted[-1])
+        xb = np.stack([rows[int(r)] for r in ids])
+        exact = flat.exact_scores(xb, xs[q:q + 1], metric)[0]
+        xn2 = np.einsum("ij,ij->i", xb.astype(np.float64), xb.astype(np.float64))
+        res.append((ids, exact, xn2, qn * qn))
+    return res

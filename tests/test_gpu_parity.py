@@ -2,13 +2,20 @@
 
 Every test here runs the product path through the C-ABI on cuda:0 and checks it
 with oracle/flat.py (fp64 semantics of faiss IndexFlat::search) or the C heap
-restatement oracle/faiss_flat.c.  Acceptance (oracle.flat.mismatches): labels
-equal except documented ties, scores within 1e-5 * max(1, |s|) (for squared L2
-the scale includes |q|^2 + |x|^2, the magnitude fp32 rounding acts on)."""
+restatement oracle/faiss_flat.c.  Acceptance (oracle.flat.mismatches):
+* searches the staged filter-and-verify engine answers (fp32 rows, more than
+  32 queries, IP k <= 28 / L2 k <= 56; _staged) are checked STRICTLY: every D is
+  the fp32 rounding of its label's fp64 score (flat.key_window) and a label
+  differs from the oracle's only inside a true fp32-key tie;
+* the fp32-accumulating engines (GEMV, skinny, the fp32 MFMA GEMM: faiss's own
+  arithmetic class) meet the north star's fp32 contract: labels equal except
+  ties within, and scores within, 1e-5 * max(1, |s|) (for squared L2 the scale
+  includes |q|^2 + |x|^2, the magnitude fp32 rounding acts on)."""
 
 import numpy as np
 import pytest
 
+from helpers import assert_against_candidates
 from oracle import cfaiss, flat
 
 pytestmark = pytest.mark.gpu
@@ -39,13 +46,22 @@ def _rand(n, d, seed, kind="normal"):
     raise ValueError(kind)
 
 
+def _staged(metric, nq, k, engine="auto"):
+    """Whether a search of an fp32 index is answered by the staged
+    filter-and-verify engine (vs_api.hip run_topk: more than kSkinnyMaxQ = 32
+    queries and a candidate count x1_list_len(need) > 0, need = 2k - 1 for IP)."""
+    need = 2 * k - 1 if metric == IP else k
+    return engine != "fp32" and nq > 32 and need + 8 <= 64
+
+
 def _check(vf, xb, xq, k, metric):
     index = vf.IndexFlat(xb.shape[1], metric)
     index.add(xb)
     D, I = index.search(xq, k)
     Dr, Ir = flat.knn_exact(xb, xq, k, metric)
-    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
-    assert not bad, bad[:5]
+    strict = _staged(metric, xq.shape[0], k) and xb.shape[0] > 0
+    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=strict)
+    assert not bad, (strict, bad[:5])
     return D, I
 
 
@@ -142,8 +158,9 @@ def test_golden_csv_books(vf, metric, golden, golden_vectors):
             D, I = index.search(q, k)
             Ir = exp[f"books_{name}_I"][: q.shape[0], :k]
             Dr = exp[f"books_{name}_D"][: q.shape[0], :k]
-            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, q)
-            assert not bad, bad[:5]
+            strict = _staged(metric, q.shape[0], k)
+            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, q, strict=strict)
+            assert not bad, (strict, bad[:5])
             # fp32 vs fp64 near-ties may swap neighbours; they must stay rare
             assert (I != Ir).mean() < 1e-3
 
@@ -171,12 +188,10 @@ def test_selfjoin_random(vf, k):
     assert (I[17] == -1).all()
     assert not (I == 17).any()
     assert not (I == np.arange(1500)[:, None]).any()
-    diff = I != Ir
-    # differing labels must be score ties within fp32 rounding
-    for q, j in zip(*np.nonzero(diff)):
-        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5, (q, j)
-    ok = ~diff & (I >= 0)
-    np.testing.assert_allclose(S[ok], Sr[ok], rtol=1e-5, atol=1e-6)
+    # the staged engine (k <= 56): similarities are roundings of the exact
+    # cosine, labels differ only inside a true tie (flat.key_window)
+    bad = flat.selfjoin_mismatches(S, I, Sr, Ir, x, np.arange(1500), strict=k <= 56)
+    assert not bad, bad[:5]
 
 
 @pytest.mark.parametrize("engine", ["i8v", "bf16v"])
@@ -200,11 +215,9 @@ def test_selfjoin_filter_fallback_drops_self(vf, k, engine):
         assert nfb >= 1000
     Sr, Ir = flat.pgvector_cosine_topk(x, k)
     assert not (I == np.arange(x.shape[0])[:, None]).any()
-    diff = I != Ir
-    for q, j in zip(*np.nonzero(diff)):
-        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5, (q, j)
-    ok = ~diff & (I >= 0)
-    np.testing.assert_allclose(S[ok], Sr[ok], rtol=1e-5, atol=1e-6)
+    # the redo stage rescores its candidates too: strict like every stage
+    bad = flat.selfjoin_mismatches(S, I, Sr, Ir, x, np.arange(x.shape[0]), strict=True)
+    assert not bad, bad[:5]
 
 
 def test_selfjoin_threshold_and_subrange(vf):
@@ -350,33 +363,32 @@ def test_large_synthetic_sampled(vf, metric):
         assert (np.diff(D, axis=1) >= 0).all()
     else:
         assert (np.diff(D, axis=1) <= 0).all()
-    # exact check on a sample of queries against a chunked fp64 oracle
+    # exact check on a sample of queries against a chunked fp64 oracle: the 64
+    # best rows by exact score with their norms, then the strict check (the
+    # staged engine answers B = 1024)
     sample = [0, 1, 511, 1023]
-    best_k, best_i = None, None
+    m = 64
+    best_k = np.zeros((len(sample), 0))
+    best_i = np.zeros((len(sample), 0), np.int64)
+    best_n = np.zeros((len(sample), 0))
     step = 100_000
     for r0 in range(0, n, step):
         xb = synthetic_rows(r0, step, d, 1234)
         s = flat.exact_scores(xb, xq[sample], metric)
         key = s if metric == L2 else -s
-        ids = np.broadcast_to(np.arange(r0, r0 + step), key.shape)
-        if best_k is None:
-            best_k, best_i = key, ids
-        else:
-            best_k = np.concatenate([best_k, key], axis=1)
-            best_i = np.concatenate([best_i, ids], axis=1)
-        part = np.argpartition(best_k, k, axis=1)[:, : k + 1]
+        xn2 = np.einsum("ij,ij->i", xb.astype(np.float64), xb.astype(np.float64))
+        best_k = np.concatenate([best_k, key], axis=1)
+        best_i = np.concatenate([best_i, np.broadcast_to(np.arange(r0, r0 + step), key.shape)], axis=1)
+        best_n = np.concatenate([best_n, np.broadcast_to(xn2, key.shape)], axis=1)
+        part = np.argpartition(best_k, m - 1, axis=1)[:, :m]
         best_k = np.take_along_axis(best_k, part, axis=1)
         best_i = np.take_along_axis(best_i, part, axis=1)
+        best_n = np.take_along_axis(best_n, part, axis=1)
     for row, q in enumerate(sample):
-        o = np.lexsort((best_i[row], best_k[row]))[:k]
-        ref_i = best_i[row][o]
-        ref_s = best_k[row][o] if metric == L2 else -best_k[row][o]
-        got_s = D[q]
-        for j in range(k):
-            tol = 1e-5 * max(1.0, abs(ref_s[j]), 1100.0 if metric == L2 else 0.0)
-            assert abs(got_s[j] - ref_s[j]) <= tol, (q, j, got_s[j], ref_s[j])
-            if I[q, j] != ref_i[j]:
-                assert abs(ref_s[j] - got_s[j]) <= tol
+        exact = best_k[row] if metric == L2 else -best_k[row]
+        qn2 = float(np.dot(xq[q].astype(np.float64), xq[q].astype(np.float64)))
+        assert_against_candidates(D[q], I[q], (best_i[row], exact, best_n[row], qn2), metric, k, d,
+                                  strict=True)
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
@@ -408,8 +420,9 @@ def test_large_batch_engines(vf, engine, metric):
     for k in (1, 10, 32):
         D, I = index.search(xq, k)
         Dr, Ir = flat.knn_exact(xb, xq, k, metric)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
-        assert not bad, (engine, k, bad[:5])
+        strict = _staged(metric, xq.shape[0], k, engine)  # IP k = 32: the fp32 engine
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=strict)
+        assert not bad, (engine, k, strict, bad[:5])
 
 
 @pytest.mark.parametrize("metric,engine", FILTER_CASES)
@@ -426,7 +439,7 @@ def test_filter_step_shapes(vf, metric, engine, d):
     for k in (1, 10):
         D, I = index.search(xq, k)
         Dr, Ir = flat.knn_exact(xb, xq, k, metric)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
         assert not bad, (d, k, bad[:5])
 
 
@@ -445,18 +458,18 @@ def test_filter_plane_follows_mutations(vf, engine):
         index.add(xb[i0:i0 + 250])
     D, I = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
-    assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True)
     rm = np.arange(100, 3000, 3, dtype=np.int64)
     index.remove_ids(rm)
     xr, _ = flat.remove_ids(xb, rm)
     D, I = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xr, xq, 10, IP)
-    assert not flat.mismatches(D, I, Dr, Ir, IP, xr, xq)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xr, xq, strict=True)
     index.reset()
     index.add(xb[:50])
     D, I = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xb[:50], xq, 10, IP)
-    assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq, strict=True)
 
 
 @pytest.mark.parametrize("engine", ["fp32", "bf16v", "i8v"])
@@ -467,10 +480,8 @@ def test_selfjoin_engines(vf, engine):
     index.add(x)
     S, I = index.selfjoin(15)
     Sr, Ir = flat.pgvector_cosine_topk(x, 15)
-    diff = I != Ir
-    for q, j in zip(*np.nonzero(diff)):
-        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
-    np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
+    bad = flat.selfjoin_mismatches(S, I, Sr, Ir, x, np.arange(2000), strict=engine != "fp32")
+    assert not bad, (engine, bad[:5])
 
 
 @pytest.mark.parametrize("metric,engine", FILTER_CASES)
@@ -486,7 +497,7 @@ def test_filter_ragged_shapes(vf, metric, engine):
         for k in (5, 10):
             D, I = index.search(xq, k)
             Dr, Ir = flat.knn_exact(xb, xq, k, metric)
-            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+            bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
             assert not bad, (n, d, nq, k, bad[:5])
 
 
@@ -502,7 +513,7 @@ def test_filter_repeatable(vf, engine):
     index.add(xb)
     D0, I0 = index.search(xq, 10)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
-    assert not flat.mismatches(D0, I0, Dr, Ir, IP, xb, xq)
+    assert not flat.mismatches(D0, I0, Dr, Ir, IP, xb, xq, strict=True)
     for _ in range(6):
         D, I = index.search(xq, 10)
         np.testing.assert_array_equal(I, I0)
@@ -519,9 +530,9 @@ def test_filter_selfjoin_offsets(vf, engine):
     index.add(x)
     Sr, Ir = flat.pgvector_cosine_topk(x, 12)
     S, I = index.selfjoin(12, q0=1000, nq=700)
-    diff = I != Ir[1000:1700]
-    for q, j in zip(*np.nonzero(diff)):
-        assert abs(float(Sr[1000 + q, j]) - float(S[q, j])) < 1e-5
+    bad = flat.selfjoin_mismatches(S, I, Sr[1000:1700], Ir[1000:1700], x, np.arange(1000, 1700),
+                                   strict=True)
+    assert not bad, bad[:5]
     S2, I2 = index.selfjoin(12, q0=5, nq=300, exclude_self=False)
     assert (I2[:, 0] == np.arange(5, 305)).mean() > 0.99  # a row is its own best match
 
@@ -542,7 +553,7 @@ def test_filter_matches_exact_engine(vf, metric, engine):
         index.set_engine(engine)
         D, I = index.search(xq, k)
         Dr, Ir = flat.knn_exact(xb, xq, k, metric)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
         assert not bad, (k, bad[:5])
         assert (I == Ie).all(axis=1).mean() > 0.99
         np.testing.assert_allclose(D, De, rtol=1e-5, atol=1e-4)
@@ -566,7 +577,7 @@ def test_filter_falls_back_on_ties(vf, metric, engine):
     nq, nfb = _lib.filter_stats(reset=True)
     assert nq == xq.shape[0] and nfb >= 20
     Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
-    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
     assert not bad, bad[:5]
 
 
@@ -586,7 +597,28 @@ def test_filter_every_query_falls_back(vf):
     nq, nfb = _lib.filter_stats(reset=True)
     assert nq == 1024 and nfb > 900
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
-    bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+    bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True)
+    assert not bad, bad[:5]
+
+
+def test_filter_redo_runs_in_slot_windows(vf):
+    """More flagged queries than one slot window of the exact redo (vs_api.hip
+    run_gemm_rescored: lists capped at ~1 GB, here 11,136 slots at k = 20):
+    every window is searched and rescored, queries of the second window included."""
+    from vsearch import _lib
+
+    base = _rand(300, 64, 74)
+    xb = np.repeat(base, 40, axis=0)
+    xq = np.tile(base, (41, 1))[:12288] + 0.001 * _rand(12288, 64, 75)
+    index = vf.IndexFlatIP(64)
+    index.add(xb)
+    _lib.filter_stats(reset=True)
+    D, I = index.search(xq, 20)
+    nq, nfb = _lib.filter_stats(reset=True)
+    assert nq == 12288 and nfb > 11200, nfb
+    sample = np.r_[0:200, 11100:11400, 12088:12288]
+    Dr, Ir = flat.knn_exact(xb, xq[sample], 20, IP)
+    bad = flat.mismatches(D[sample], I[sample], Dr, Ir, IP, xb, xq[sample], strict=True)
     assert not bad, bad[:5]
 
 
@@ -614,7 +646,7 @@ def test_filter_wide_check_settles_scattered_near_duplicates(vf, metric, engine)
     assert nq == xq.shape[0]
     assert wide >= 60 and n_exact == 0, (metric, wide, n_exact)
     Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
-    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq)
+    bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
     assert not bad, bad[:5]
 
 
@@ -631,7 +663,7 @@ def test_filter_engines_agree_and_l2_has_no_int8(vf):
     for engine in ("auto", "bf16v", "i8v", "bf16v", "auto"):
         index.set_engine(engine)
         D, I = index.search(xq, 10)
-        assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq), engine
+        assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True), engine
     l2 = vf.IndexFlatL2(192)
     assert l2.filter_planes == ("bf16",)
     with pytest.raises(RuntimeError):
@@ -664,7 +696,7 @@ def test_staged_engine_hands_clustered_queries_to_bf16(vf):
     nq, n_exact = _lib.filter_stats(reset=True)
     assert nq == 300 and second > 200 and n_exact < 30, (second, n_exact)
     Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
-    bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq)
+    bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True)
     assert not bad, bad[:5]
     # the library has seen the int8 stage hand most queries on: the next search
     # starts on bf16 (nothing handed over), with the same exact results
@@ -672,11 +704,9 @@ def test_staged_engine_hands_clustered_queries_to_bf16(vf):
     second2 = _lib.filter_second_stats()
     _lib.filter_stats(reset=True)
     assert second2 == 0, second2
-    assert not flat.mismatches(D2, I2, Dr, Ir, IP, xb, xq)
+    assert not flat.mismatches(D2, I2, Dr, Ir, IP, xb, xq, strict=True)
     # the same rows through the cosine self-join (a 1000-student sub-range)
     S, J = index.selfjoin(15, q0=3000, nq=1000)
     Sr, Jr = flat.pgvector_cosine_topk(xb, 15, q_rows=np.arange(3000, 4000))
-    diff = J != Jr
-    for q, j in zip(*np.nonzero(diff)):
-        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
-    np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
+    bad = flat.selfjoin_mismatches(S, J, Sr, Jr, xb, np.arange(3000, 4000), strict=True)
+    assert not bad, bad[:5]

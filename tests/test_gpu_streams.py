@@ -60,3 +60,73 @@ def test_two_streams_share_scratch_chunks():
         th.join()
     torch.cuda.synchronize()
     assert not errors, errors
+
+
+def test_writer_of_one_index_does_not_drain_another():
+    """Writers wait for their own index's readers only (vs_api.hip ReaderMark /
+    wait_readers): remove_ids on a small index A returns while a queue of long
+    searches of index B is still running on another stream, and both results
+    stay exact.  (Storage growth frees the old buffers with hipFree; the time
+    it takes beside B's queue is printed, not asserted.)"""
+    import time
+
+    import torch
+
+    from oracle import flat
+    from vsearch import faiss as vfaiss
+    from vsearch.synth import synthetic_rows
+
+    d, k = 1536, 10
+    big = vfaiss.IndexFlatIP(d)
+    big.add_synthetic(2_000_000, seed=5)
+    xq = torch.from_numpy(synthetic_rows(50_000_000, 4096, d, 6)).cuda()
+    D = torch.empty((4096, k), dtype=torch.float32, device="cuda")
+    I = torch.empty((4096, k), dtype=torch.int64, device="cuda")
+    st = torch.cuda.Stream()
+    rng = np.random.default_rng(7)
+    xa = rng.standard_normal((20_000, 64)).astype(np.float32)
+    small = vfaiss.IndexFlatIP(64)
+    small.add(xa)
+    small.search(xa[:100], k)  # a reader mark of A's own
+    # warm-up: B's search once, timed alone
+    with torch.cuda.stream(st):
+        big.search_device(xq.data_ptr(), 4096, k, D.data_ptr(), I.data_ptr(), stream=st.cuda_stream)
+    st.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):
+        big.search_device(xq.data_ptr(), 4096, k, D.data_ptr(), I.data_ptr(), stream=st.cuda_stream)
+    st.synchronize()
+    one = time.perf_counter() - t0
+    reps = max(8, int(0.5 / max(one, 1e-3)))
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):  # a queue of B searches, ~0.5 s of device work
+        for _ in range(reps):
+            big.search_device(xq.data_ptr(), 4096, k, D.data_ptr(), I.data_ptr(),
+                              stream=st.cuda_stream)
+    t_q = time.perf_counter()
+    probe = torch.cuda.Stream(priority=-1)  # diagnostic: a high-priority torch stream
+    with torch.cuda.stream(probe):
+        z = torch.ones(1024, device="cuda") * 2
+    probe.synchronize()
+    t_probe = time.perf_counter() - t_q
+    t_q = time.perf_counter()
+    rm = np.arange(0, 20_000, 3, dtype=np.int64)
+    assert small.remove_ids(rm) == rm.size
+    t_rm = time.perf_counter() - t_q
+    t_g = time.perf_counter()
+    small.add(xa[:10_000])  # 16,667 + 10,000 rows: past the first capacity -> growth
+    t_grow = time.perf_counter() - t_g
+    st.synchronize()
+    total = time.perf_counter() - t0
+    print(f"B queue {reps} x {one * 1e3:.1f} ms = {total * 1e3:.0f} ms; remove_ids on A "
+          f"{t_rm * 1e3:.1f} ms; growth of A {t_grow * 1e3:.1f} ms; high-priority torch "
+          f"probe {t_probe * 1e3:.1f} ms ({float(z[0])})")
+    assert t_rm < 0.25 * reps * one, (t_rm, reps * one)
+    # both indexes still exact
+    xr, _ = flat.remove_ids(xa, rm)
+    xr = np.concatenate([xr, xa[:10_000]])
+    Da, Ia = small.search(xa[:300], k)
+    Dr, Ir = flat.knn_exact(xr, xa[:300], k, flat.METRIC_INNER_PRODUCT)
+    assert not flat.mismatches(Da, Ia, Dr, Ir, flat.METRIC_INNER_PRODUCT, xr, xa[:300], strict=True)
+    Db, Ib = big.search(xq[:512].cpu().numpy(), k)
+    assert (Ib == I[:512].cpu().numpy()).all()

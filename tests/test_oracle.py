@@ -170,3 +170,64 @@ def test_mismatch_checker_catches_errors():
     D2 = D.copy()
     D2[1, 1] += 0.01
     assert flat.mismatches(D2, I, D, I, L2, xb, xq)
+
+
+def _engine_keys(xb, xq, metric):
+    """The filter engine's final keys restated in numpy: fp64 dot products
+    rounded once, fp64-summed norms rounded once, L2 by faiss's BLAS formula in
+    fp32 (vs_gemm_x1.hip exact_key, vs_device.h l2_from_ip)."""
+    ip = (xq.astype(np.float64) @ xb.astype(np.float64).T).astype(np.float32)
+    if metric == IP:
+        return ip
+    qn = np.einsum("ij,ij->i", xq.astype(np.float64), xq.astype(np.float64)).astype(np.float32)
+    xn = np.einsum("ij,ij->i", xb.astype(np.float64), xb.astype(np.float64)).astype(np.float32)
+    return np.maximum((qn[:, None] + xn[None, :]) - np.float32(2) * ip, np.float32(0))
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_strict_checker_accepts_rounded_keys_and_rejects_near_swaps(metric):
+    """strict=True accepts exactly what an exactly rescored engine can return
+    (its keys within key_window of the fp64 score, labels swapped only inside
+    overlapping windows) and rejects a near-neighbour swap that the fp32
+    contract's 1e-5 window would let through."""
+    rng = np.random.default_rng(5)
+    xb = rng.standard_normal((3000, 1536)).astype(np.float32)
+    xq = rng.standard_normal((8, 1536)).astype(np.float32)
+    keys = _engine_keys(xb, xq, metric)
+    D, I = flat.select_topk(keys.astype(np.float64), 10, metric, rule="lex")
+    Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
+    assert not flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
+    # a near-duplicate of query 0's best row, slightly worse: its exact score is
+    # inside 1e-5 relative but far outside the rounding window
+    best = int(Ir[0, 0])
+    s0 = flat.exact_scores(xb[best:best + 1], xq[:1], metric)[0, 0]
+    eps = 3e-6 * max(abs(s0), 1.0)
+    step = xq[0] / np.linalg.norm(xq[0])
+    xb2 = np.concatenate([xb, (xb[best] - (eps / np.linalg.norm(xq[0])) * step)[None]]).astype(np.float32)
+    new = xb2.shape[0] - 1
+    Dr2, Ir2 = flat.knn_exact(xb2, xq, 10, metric)
+    assert Ir2[0, 1] == new  # the oracle ranks it second
+    I_sw = Ir2.copy()
+    I_sw[0, 0], I_sw[0, 1] = Ir2[0, 1], Ir2[0, 0]
+    D_sw = Dr2.copy()
+    D_sw[0, 0], D_sw[0, 1] = Dr2[0, 1], Dr2[0, 0]
+    assert flat.mismatches(D_sw, I_sw, Dr2, Ir2, metric, xb2, xq, strict=True)
+    if metric == IP:  # the old 1e-5 window would have accepted the swap
+        assert not [b for b in flat.mismatches(D_sw, I_sw, Dr2, Ir2, metric, xb2, xq)
+                    if b[2] == "label"]
+    # a score that is not the rounding of the label's exact score
+    D_off = D.copy()
+    D_off[1, 3] = np.nextafter(np.nextafter(D[1, 3], np.inf, dtype=np.float32), np.inf,
+                               dtype=np.float32) if metric == IP else D[1, 3] * np.float32(1 + 1e-5)
+    assert flat.mismatches(D_off, I, Dr, Ir, metric, xb, xq, strict=True)
+
+
+def test_strict_selfjoin_checker():
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal((400, 64)).astype(np.float32)
+    Sr, Ir = flat.pgvector_cosine_topk(x, 10)
+    assert not flat.selfjoin_mismatches(Sr, Ir, Sr, Ir, x, np.arange(400), strict=True)
+    S2 = Sr.copy()
+    S2[3, 2] += 2e-6
+    assert flat.selfjoin_mismatches(S2, Ir, Sr, Ir, x, np.arange(400), strict=True)
+    assert not flat.selfjoin_mismatches(S2, Ir, Sr, Ir, x, np.arange(400))

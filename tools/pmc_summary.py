@@ -19,17 +19,23 @@ import sys
 
 
 def load(path):
+    """Mean counter value per kernel name and per (name, grid size): one
+    instantiation runs full-size passes and small gathered ones (the staged
+    engine's later stages), whose bytes must not be averaged together."""
     agg = collections.defaultdict(list)
+    grid = collections.defaultdict(list)
     with open(path, newline="") as f:
         for r in csv.DictReader(f):
             agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+            grid[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+    return ({k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()},
+            {k: (sum(v) / len(v), len(v)) for k, v in grid.items()})
 
 
 def main():
     prof, tag, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-    fetch, nf = load(os.path.join(prof, "pmc_fetch", "run_counter_collection.csv"))
-    write, _ = load(os.path.join(prof, "pmc_write", "run_counter_collection.csv"))
+    fetch, nf, fgrid = load(os.path.join(prof, "pmc_fetch", "run_counter_collection.csv"))
+    write, _, wgrid = load(os.path.join(prof, "pmc_write", "run_counter_collection.csv"))
     out = {"source": prof, "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
            "kernels": {}}
     for name in fetch:
@@ -42,6 +48,12 @@ def main():
             "fetch_kb_per_launch": fk,
             "write_kb_per_launch": wk,
             "hbm_bytes_per_launch": 2.0 * fk * 1024 + wk * 1024,
+            "by_grid": {
+                str(g): {"dispatches": n, "fetch_kb_per_launch": f,
+                         "write_kb_per_launch": wgrid.get((name, g), (0.0, 0))[0],
+                         "hbm_bytes_per_launch": 2.0 * f * 1024
+                         + wgrid.get((name, g), (0.0, 0))[0] * 1024}
+                for (nm, g), (f, n) in sorted(fgrid.items()) if nm == name},
         }
     dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                        f"{tag}_pmc_{workload}.json")
