@@ -441,9 +441,8 @@ int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
                               (int8_t*)idx->fplane[FILTER_I8], idx->fscale, idx->rn2[FILTER_I8], st),
            "vs: int8 filter plane");
   if (idx->plane_on[FILTER_BF16]) {
-    VS_HIP(launch_f32_to_bf16((const float*)idx->row(r0), idx->ld,
-                              (uint16_t*)idx->fplane[FILTER_BF16] + r0 * idx->ld, idx->ld, n,
-                              idx->ld, st),
+    VS_HIP(launch_bf16_plane((const float*)idx->codes, idx->ld, r0, n,
+                             (uint16_t*)idx->fplane[FILTER_BF16], st),
            "vs: bf16 filter plane");
     VS_HIP(launch_resid_norms((const float*)idx->codes, idx->ld, r0, n, idx->rn2[FILTER_BF16], st),
            "vs: residual norms");
@@ -529,9 +528,6 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
          "vs: zeroing norms");
   for (int p = 0; p < 2; ++p) {
     if (!on[p]) continue;
-    const int64_t pb = idx->planebytes(p);
-    VS_HIP(hipMemsetAsync(fplane[p] + keep * pb, 0, (size_t)(cap - keep) * pb, st),
-           "vs: zeroing plane");
     VS_HIP(hipMemsetAsync(rn2[p] + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
            "vs: zeroing residual norms");
   }
@@ -547,7 +543,9 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
            "vs: copying norms");
     for (int p = 0; p < 2; ++p) {
       if (!on[p]) continue;
-      VS_HIP(hipMemcpyAsync(fplane[p], idx->fplane[p], (size_t)keep * idx->planebytes(p),
+      // tile-major planes: rows [0, keep) are the first ceil(keep / 256) tiles
+      VS_HIP(hipMemcpyAsync(fplane[p], idx->fplane[p],
+                            (size_t)round_up(keep, 256) * idx->planebytes(p),
                             hipMemcpyDeviceToDevice, st),
              "vs: copying plane");
       VS_HIP(hipMemcpyAsync(rn2[p], idx->rn2[p], (size_t)keep * sizeof(float),
@@ -559,6 +557,12 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
                             hipMemcpyDeviceToDevice, st),
              "vs: copying scales");
   }
+  // the planes' rows past the kept ones read zeros (after the prefix copy,
+  // which brings whole tiles)
+  for (int p = 0; p < 2; ++p)
+    if (on[p])
+      VS_HIP(launch_plane_zero_rows(fplane[p], idx->planebytes(p), keep, cap - keep, st),
+             "vs: zeroing plane");
   // The copies above, and searches of this index still in flight (any
   // stream), read the old storage; other indexes' work is not waited for.
   VS_HIP(hipStreamSynchronize(st), "vs: storage growth");
@@ -733,8 +737,12 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const char* QH = nullptr;
   const float* qs = nullptr;    // int8: query scales
   const float* qr2 = nullptr;   // int8: query residual norms (for the bound)
-  if (self_rows) {
-    QH = idx->fplane[plane] + a.self0 * pb;
+  // stored rows starting on a tile boundary are read from the index's own
+  // (tile-major) plane; any other batch is converted (the same codes)
+  const bool plane_rows = self_rows && a.self0 % kX1Q == 0;
+  x.qtile0 = plane_rows ? (int)(a.self0 / kX1Q) : 0;
+  if (plane_rows) {
+    QH = idx->fplane[plane];
     if (i8) {
       qs = idx->fscale + a.self0;
       qr2 = idx->rn2[FILTER_I8] + a.self0;
@@ -750,12 +758,9 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
       qs = sc;
       qr2 = r;
     } else {
-      VS_HIP(launch_f32_to_bf16(Q, idx->ld, (uint16_t*)qh, idx->ld, qa_rows, idx->ld, st),
-             "vs: query plane");
+      VS_HIP(launch_bf16_plane(Q, idx->ld, 0, qa_rows, (uint16_t*)qh, st), "vs: query plane");
     }
-    if (x.nq_pad > qa_rows)
-      VS_HIP(hipMemsetAsync(qh + (size_t)qa_rows * pb, 0, (size_t)(x.nq_pad - qa_rows) * pb, st),
-             "vs: query plane");
+    VS_HIP(launch_plane_zero_rows(qh, pb, qa_rows, x.nq_pad - qa_rows, st), "vs: query plane");
     QH = qh;
   }
   const unsigned* stats = idx->bstats[plane];  // the index's maxima (kept by add / remove)
@@ -769,7 +774,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     VS_HIP(scr.alloc((void**)&cx, (size_t)idx->capacity * sizeof(float)), "vs: scratch");
     VS_HIP(launch_mul_arrays(idx->fscale, a.xaux, idx->capacity, cx, st), "vs: cosine factors");
     x.xs = cx;
-    if (self_rows) {
+    if (plane_rows) {
       qs = cx + a.self0;
     } else {
       float* cq = nullptr;
@@ -1541,8 +1546,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
              "vs_remove_ids: bound maxima");
   for (int p = 0; p < 2; ++p) {
     if (!idx->plane_on[p]) continue;
-    const int64_t pb = idx->planebytes(p);
-    VS_HIP(hipMemsetAsync(idx->fplane[p] + nt * pb, 0, (size_t)nrem * pb, st),
+    VS_HIP(launch_plane_zero_rows(idx->fplane[p], idx->planebytes(p), nt, nrem, st),
            "vs_remove_ids: zero tail");
     VS_HIP(hipMemsetAsync(idx->rn2[p] + nt, 0, (size_t)nrem * sizeof(float), st),
            "vs_remove_ids: zero tail");

@@ -167,7 +167,7 @@ template <int KR, int MODE, int NBUF, int EL>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ XH, const float* __restrict__ xs, const float* __restrict__ xaux,
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
-    int nqa, int64_t ldb, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int64_t self0,
+    int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
     int qg, float* __restrict__ pkey, int* __restrict__ pid) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
@@ -246,12 +246,15 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 
   if (t1 > t0) {  // uniform over the workgroup
+    // Planes are tile-major (vs_internal.h plane_offset): the 64-B step s of
+    // the 256 rows of tile t is one contiguous 16-KB block, so a DMA piece (16
+    // rows x 64 B) reads 1 KB of consecutive bytes — eight whole 128-B lines,
+    // not sixteen half lines of sixteen row-major rows.
     // per-lane DMA source: row (lane >> 2) of a 16-row piece, 16-B chunk
     // swizzled by the LDS slot (c ^ ((slot >> 2) & 3))
-    const uint32_t soff =
-        (uint32_t)(lane >> 2) * (uint32_t)ldb + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
+    const uint32_t soff = (uint32_t)(lane >> 2) * 64u + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
     const int fsw = (c32 >> 2) & 3;
-    const char* qtile = QH + (int64_t)qt * kT * ldb + (uint32_t)(32 * w) * (uint32_t)ldb;
+    const char* qtile = QH + (int64_t)(qtile0 + qt) * nksteps * kStepB + (uint32_t)(32 * w) * 64u;
     const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
     const int nsteps = (t1 - t0) * nksteps;
 
@@ -267,8 +270,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       const int f = tile_perm(tt);
       const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
       xhi = f & 0xF0;
-      xlane = (uint32_t)((ln >> 2) ^ (f & 0x0C)) * (uint32_t)ldb +
-              (uint32_t)((ln & 3) ^ (ln >> 4)) * 16u;
+      xlane = (uint32_t)((ln >> 2) ^ (f & 0x0C)) * 64u + (uint32_t)((ln & 3) ^ (ln >> 4)) * 16u;
     };
     set_xoff(t0);
 
@@ -308,9 +310,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     auto stage_piece = [&](int i) {
       // uniform bases (the piece's permuted 16-row group of the load tile, the
       // query tile's) + per-lane offsets below 256 rows
-      const char* xbase = XH + (int64_t)lt * kT * ldb + lk_ * 64 +
-                          (uint32_t)((32 * w + 16 * (i >> 1)) ^ xhi) * (uint32_t)ldb;
-      const char* qbase = qtile + lk_ * 64 + (uint32_t)(16 * (i >> 1)) * (uint32_t)ldb;
+      const char* xbase = XH + ((int64_t)lt * nksteps + lk_) * kStepB +
+                          (uint32_t)((32 * w + 16 * (i >> 1)) ^ xhi) * 64u;
+      const char* qbase = qtile + (int64_t)lk_ * kStepB + (uint32_t)(16 * (i >> 1)) * 64u;
       const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
 #if !VS_X1_P_NODMA
       if ((i & 1) == 0) {
@@ -577,10 +579,11 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // a gathered later stage (usually empty: its tiles exit at once) is one launch
   const int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   const int64_t ldb = a.ld * filter_bytes(EL);
+  if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
     hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, VS_X1_NBUF, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
-                       ldb, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.self0, a.qrow,
+                       (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0, a.self0, a.qrow,
                        a.qcount, c, nchunk, part.KP, qg, part.key, part.id);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -734,7 +737,6 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restric
   bad = __any(bad);
   const float s = bad ? 0.0f : m / 127.0f;
   double acc = 0.0;
-  uint32_t* out = (uint32_t*)(codes + (r0 + row) * ld);
   for (int64_t c = lane * 4; c < ld; c += 256) {
     const f32x4 v = *(const f32x4*)(xr + c);
     uint32_t packed = 0;
@@ -746,7 +748,7 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restric
       const double r = (double)v[i] - (double)s * (double)code;
       acc += r * r;
     }
-    out[c >> 2] = packed;
+    *(uint32_t*)(codes + plane_offset(r0 + row, c, ld)) = packed;  // tile-major
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   if (lane == 0) {

@@ -79,12 +79,23 @@ hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize
 // (twice the bf16 rate, exact int32 sums, half the bytes per element).
 enum Filter : int { FILTER_BF16 = 0, FILTER_I8 = 1 };
 inline int filter_bytes(int filter) { return filter == FILTER_I8 ? 1 : 2; }
+// Filter planes are stored TILE-MAJOR: [tile of 256 rows][64-B step][256
+// rows][64 B], so the bytes one filter-pass step reads from a tile (256 rows x
+// 64 B) are one contiguous 16-KB block and every DMA piece is 1 KB of
+// consecutive bytes (whole 128-B lines; cdna_hip_programming.md: fragment-
+// shaped pieces of half lines cost the TA twice).  `ldb` = bytes per row, a
+// multiple of 64.  Any row range of a capacity that is a multiple of 256 rows
+// lives inside the same prefix of tiles whatever the capacity.
+__host__ __device__ inline int64_t plane_offset(int64_t row, int64_t byte, int64_t ldb) {
+  return ((row >> 8) * (ldb >> 6) + (byte >> 6)) * 16384 + (row & 255) * 64 + (byte & 63);
+}
 struct X1Args {
   int filter = FILTER_BF16;
-  const void* XH = nullptr;      // database plane [capacity][ld] (row-major)
+  const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
-  const void* QH = nullptr;      // query plane [nq_pad][ld] (self-join: stored rows)
+  const void* QH = nullptr;      // query plane, tile-major (self-join: the stored plane)
+  int qtile0 = 0;                // QH's tile of query tile 0 (self-join: self0 / 256)
   const float* qs = nullptr;     // int8: per-query factor s_q (IP) or s_q / |q| (COS)
   const float* qaux = nullptr;   // per-query aux, nqa entries (padding queries read 0)
   int nqa = 0;
@@ -124,8 +135,8 @@ hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, u
 // rn2[r] = |x_r - bf16_rne(x_r)|^2 (rounded up) for fp32 rows [r0, r0+n).
 hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n, float* out,
                               hipStream_t st);
-// int8 filter plane of fp32 rows [r0, r0+n) (stride ld): codes (int8, stride
-// ld), scale[r] = max|x_r| / 127 and, when rn2 != nullptr, rn2[r] = |x_r - scale
+// int8 filter plane of fp32 rows [r0, r0+n) (stride ld): codes (int8,
+// tile-major plane rows r0..), scale[r] = max|x_r| / 127 and, when rn2 != nullptr, rn2[r] = |x_r - scale
 // * code_r|^2 rounded up (+inf for a row with a non-finite element).
 hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
                               float* scale, float* rn2, hipStream_t st);
@@ -215,6 +226,12 @@ hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, in
 // rounded through bf16 (the value a bf16 index stores).
 hipError_t launch_f32_to_bf16(const float* in, int64_t ldi, uint16_t* out, int64_t ldo,
                               int64_t rows, int64_t cols, hipStream_t st);
+// bf16 plane (tile-major) of fp32 rows [r0, r0+n) of stride ld (ld elements
+// per plane row, RNE).
+hipError_t launch_bf16_plane(const float* X, int64_t ld, int64_t r0, int64_t n, uint16_t* plane,
+                             hipStream_t st);
+// Zeroes plane rows [r0, r0+n) of a tile-major plane with ldb bytes per row.
+hipError_t launch_plane_zero_rows(char* plane, int64_t ldb, int64_t r0, int64_t n, hipStream_t st);
 hipError_t launch_bf16_to_f32(const uint16_t* in, int64_t ldi, float* out, int64_t ldo,
                               int64_t rows, int64_t cols, hipStream_t st);
 hipError_t launch_round_bf16(float* x, int64_t n, hipStream_t st);

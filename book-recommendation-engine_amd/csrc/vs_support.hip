@@ -381,6 +381,49 @@ static dim3 pitched_grid(int64_t rows, int64_t ldo) {
   return dim3((unsigned)gx, (unsigned)gy, (unsigned)gz);
 }
 
+// One wave per plane row: 4 elements (8 B) per lane per pass.
+__global__ __launch_bounds__(256) void bf16_plane_kernel(const float* __restrict__ X, int64_t ld,
+                                                         int64_t r0, int64_t n,
+                                                         uint16_t* __restrict__ plane) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* xr = X + (r0 + row) * ld;
+  char* base = (char*)plane;
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+    const uint32_t lo = (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16);
+    const uint32_t hi = (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16);
+    *(uint2*)(base + plane_offset(r0 + row, 2 * c, 2 * ld)) = make_uint2(lo, hi);
+  }
+}
+
+hipError_t launch_bf16_plane(const float* X, int64_t ld, int64_t r0, int64_t n, uint16_t* plane,
+                             hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ld % 64 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bf16_plane_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, ld, r0,
+                     n, plane);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void plane_zero_rows_kernel(char* __restrict__ plane,
+                                                              int64_t ldb, int64_t r0, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  for (int64_t c = lane * 16; c < ldb; c += 1024)
+    *(uint4*)(plane + plane_offset(r0 + row, c, ldb)) = make_uint4(0, 0, 0, 0);
+}
+
+hipError_t launch_plane_zero_rows(char* plane, int64_t ldb, int64_t r0, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ldb % 64 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(plane_zero_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, plane,
+                     ldb, r0, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_f32_to_bf16(const float* in, int64_t ldi, uint16_t* out, int64_t ldo,
                               int64_t rows, int64_t cols, hipStream_t st) {
   if (rows <= 0) return hipSuccess;
