@@ -783,6 +783,12 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
       qs = cq;
     }
   }
+  if (i8) {  // the per-lane factor bounds of the fast reject (scalar loads in the kernel)
+    float* gm = nullptr;
+    VS_HIP(scr.alloc((void**)&gm, (size_t)(idx->capacity / 16) * sizeof(float)), "vs: scratch");
+    VS_HIP(launch_group_max(x.xs, idx->capacity, gm, st), "vs: factor bounds");
+    x.xgmax = gm;
+  }
   x.xaux = a.xaux;
   x.QH = QH;
   x.qs = qs;
@@ -997,9 +1003,104 @@ int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st) {
   return VS_OK;
 }
 
+// Inner-product searches whose answer needs more than the 64 entries a list
+// holds: faiss's tie rule with k > 32 (it reads the 2k-1 best (key, label)
+// entries; service.py:529-531 oversamples to k = 60) and raw searches with
+// 64 < k <= 128 (a shard's half of a sharded k > 32 search).  Two pages:
+//  1. the lexicographic top-64 of every query (the exact engine, raw order);
+//  2. for the queries that may need more (page_check: the k-th key's run of
+//     equal keys reaches entry 63; raw: the page is full), the next 64 entries,
+//     by the same kernel with the list admission floored at entry 63 (so every
+//     row's key is the same instructions' result in both pages), gathered;
+//  3. page_finish: the pages concatenated, faiss's rule, the k outputs.
+// The small-batch GEMV serves one or two fp32 queries (the k = 60 single query);
+// everything else runs the fp32 / bf16 MFMA GEMM.
+int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st) {
+  const int nq = a.nq;
+  const int ntotal = (int)idx->ntotal;
+  Scratch scr(st);
+  float *D1 = nullptr, *D2 = nullptr, *fkey = nullptr;
+  int64_t *I1 = nullptr, *I2 = nullptr;
+  int *fid = nullptr, *flags = nullptr, *qlist = nullptr, *qcount = nullptr;
+  const int nslot = (int)round_up(nq, kBQ);
+  VS_HIP(scr.alloc((void**)&D1, (size_t)nq * 64 * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&I1, (size_t)nq * 64 * sizeof(int64_t)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&D2, (size_t)nq * 64 * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&I2, (size_t)nq * 64 * sizeof(int64_t)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&fkey, (size_t)nq * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&fid, (size_t)nq * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&flags, (size_t)nq * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qlist, (size_t)nslot * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qcount, sizeof(int)), "vs: scratch");
+  const bool gemv_fits =
+      (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
+  const bool gemv = a.self0 < 0 && nq <= 2 && idx->esize == 4 && gemv_fits;
+  Partials gp;  // GEMV lists (both pages)
+  gp.KP = 64;
+  if (gemv) {
+    const int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
+    gp.P = nblocks;
+    const size_t n = (size_t)nq * gp.P * gp.KP;
+    VS_HIP(scr.alloc((void**)&gp.key, n * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&gp.id, n * sizeof(int)), "vs: scratch");
+    KernelTimer tm(st, "gemv_topk");
+    VS_HIP(launch_gemv_topk(64, MODE_IP, nq, idx->codes, idx->esize, a.qbuf, idx->ld, ntotal,
+                            nblocks, gp, st),
+           "vs: gemv_topk launch");
+    tm.stop();
+    VS_HIP(launch_merge_partials(MODE_IP, gp, nq, 64, idx->id_base, a.min_score, D1, I1, 64, st, 1),
+           "vs: merge launch");
+  } else {
+    SearchArgs p1 = a;
+    p1.k = 64;
+    p1.raw = 1;
+    p1.D = D1;
+    p1.I = I1;
+    const int rc = run_gemm(idx, p1, 64, st);
+    if (rc) return rc;
+  }
+  VS_HIP(launch_page_check(D1, I1, nq, a.k, a.raw, idx->id_base, fkey, fid, flags, st),
+         "vs: page check");
+  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, nullptr, nullptr, st), "vs: flags");
+  if (gemv) {  // every block exits at once when no query needs the second page
+    VS_HIP(launch_gemv_topk(64, MODE_IP, nq, idx->codes, idx->esize, a.qbuf, idx->ld, ntotal, gp.P,
+                            gp, st, fkey, fid, qcount),
+           "vs: gemv_topk launch");
+    VS_HIP(launch_merge_partials(MODE_IP, gp, nq, 64, idx->id_base, a.min_score, D2, I2, 64, st, 1),
+           "vs: merge launch");
+  } else {
+    // the flagged queries, gathered, in slot windows of lists of at most ~1 GB
+    Partials part;
+    part.KP = 64;
+    const int ntiles = (ntotal + kBN - 1) / kBN;
+    const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, 256));
+    part.P = 2 * nsplit;
+    const int cap = (int)std::min<int64_t>(
+        nslot, std::max<int64_t>(kBQ, ((int64_t)1 << 30) / ((int64_t)part.P * 64 * 8) / kBQ * kBQ));
+    VS_HIP(scr.alloc((void**)&part.key, (size_t)cap * part.P * 64 * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, (size_t)cap * part.P * 64 * sizeof(int)), "vs: scratch");
+    int* wc = nullptr;
+    VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
+    const void* qmat = a.qb16 ? a.qb16 : (const void*)a.qbuf;
+    for (int w0 = 0; w0 < nslot; w0 += cap) {
+      VS_HIP(launch_window_count(qcount, w0, cap, wc, st), "vs: window");
+      VS_HIP(launch_gemm_topk(64, MODE_IP, idx->codes, a.xaux, qmat, a.qaux, idx->ld, idx->esize,
+                              ntotal, cap, nsplit, -1, part, st, qlist + w0, wc, fkey, fid),
+             "vs: gemm_topk launch");
+      VS_HIP(launch_merge_partials(MODE_IP, part, cap, 64, idx->id_base, a.min_score, D2, I2, 64,
+                                   st, 1, qlist + w0, wc),
+             "vs: merge launch");
+    }
+  }
+  VS_HIP(launch_page_finish(D1, I1, D2, I2, flags, nq, a.k, a.raw, a.D, a.I, st), "vs: pages");
+  return VS_OK;
+}
+
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
 // zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
 int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engine) {
+  if (a.mode == MODE_IP && (a.raw ? a.k > VS_MAX_K : 2 * a.k - 1 > VS_MAX_K))
+    return run_wide_k(idx, a, st);
   // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
   // lowest 2k-1 (key, label) entries of every partial list to be exact; `raw`
   // output (plain lexicographic order) needs k.
@@ -1345,7 +1446,11 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
   if (!idx) return fail(VS_E_INVALID, "vs_search: null index");
   if (n < 0) return fail(VS_E_INVALID, "vs_search: n < 0");
   if (k <= 0) return fail(VS_E_INVALID, "vs_search: k must be > 0");  // faiss: FAISS_THROW_IF_NOT(k > 0)
-  if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_search: k > VS_MAX_K (64) not supported yet");
+  // raw inner-product searches (a shard's half of a sharded k > 32 search) go to
+  // 2 * VS_MAX_K
+  if (k > VS_MAX_K && !(k <= 2 * VS_MAX_K && (flags & VS_RAW_ORDER) &&
+                        idx->metric == VS_METRIC_INNER_PRODUCT))
+    return fail(VS_E_UNSUPPORTED, "vs_search: k > VS_MAX_K (64) not supported");
   if (n == 0) return VS_OK;
   if (!x || !D || !I) return fail(VS_E_INVALID, "vs_search: null buffer");
   hipStream_t st = (hipStream_t)stream;
@@ -1622,6 +1727,8 @@ int vs_merge_topk(const float* D_parts, const int64_t* I_parts, int64_t nparts, 
   if (nparts < 1 || nq < 0 || k_in < 1 || k < 1)
     return fail(VS_E_INVALID, "vs_merge_topk: bad sizes");
   if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_merge_topk: k > VS_MAX_K");
+  if (k_in > 2 * VS_MAX_K || nparts > 64)
+    return fail(VS_E_UNSUPPORTED, "vs_merge_topk: k_in > 2 * VS_MAX_K or more than 64 parts");
   if (metric != VS_METRIC_L2 && metric != VS_METRIC_INNER_PRODUCT)
     return fail(VS_E_INVALID, "vs_merge_topk: bad metric");
   if (nq == 0) return VS_OK;

@@ -36,12 +36,20 @@ namespace vs {
 // Workgroup -> (query tile, split) mapping is XCD-aware: consecutive logical ids
 // (which share a database split and differ in query tile) are packed onto one XCD
 // so the 4 MiB L2 there serves each database tile to all query tiles in flight.
-template <int KP, int MODE, typename T>
+//
+// FLOOR (inner product, KP = 64 only): the lists admit only entries that come
+// strictly after the query's floor (fkey[q], fid[q]) in (key, row) order — the
+// second page of a query's lexicographic order, which faiss's inner-product tie
+// rule reads for k > 32 (vs_api.hip run_wide_k).  The keys are the same
+// instructions' as without the floor, so a row's key is bit-identical in both
+// pages.
+template <int KP, int MODE, typename T, bool FLOOR = false>
 __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
     const T* __restrict__ X, const float* __restrict__ xaux, const T* __restrict__ Q,
     const float* __restrict__ qaux, int64_t ld, int nstage, int ntotal, int ntiles, int nsplit,
     int nqt, int64_t self0, float* __restrict__ pkey, int* __restrict__ pid,
-    const int* __restrict__ qlist, const int* __restrict__ qcount) {
+    const int* __restrict__ qlist, const int* __restrict__ qcount,
+    const float* __restrict__ fkey, const int* __restrict__ fid) {
   static_assert(sizeof(T) == 4 || sizeof(T) == 2, "fp32 or bf16 rows");
   // [buf][X|Q][128 rows][128 B]; viewed as floats (32 per row) for addressing.
   __shared__ __attribute__((aligned(16))) float smem[2 * 2 * kBN * kBK];
@@ -75,6 +83,12 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
   float qa = 0.0f;
   if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa = qaux[qsrc];
   const int selfrow = self0 >= 0 ? (int)(self0 + qsrc) : -1;
+  float fk = 0.0f;
+  int fi = 0;
+  if constexpr (FLOOR) {
+    fk = fkey[qsrc];
+    fi = fid[qsrc];
+  }
 
   float lk[KP];
   int li[KP];
@@ -201,7 +215,8 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
             key = -(v * (qa * xa[i]));
           }
           acc[s][j * 4 + i] = key;
-          const bool cand = row < ntotal && row != selfrow && lex_less(key, row, tk, ti);
+          bool cand = row < ntotal && row != selfrow && lex_less(key, row, tk, ti);
+          if constexpr (FLOOR) cand = cand && lex_less(fk, fi, key, row);
           m |= (uint32_t)cand << (j * 4 + i);
         }
       }
@@ -230,23 +245,24 @@ __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
   }
 }
 
-template <int KP, int MODE>
+template <int KP, int MODE, bool FLOOR = false>
 static hipError_t gemm_dispatch_mode(const void* X, const float* xaux, const void* Q,
                                      const float* qaux, int64_t ld, int esize, int ntotal,
                                      int nq_pad, int nsplit, int64_t self0, Partials part,
-                                     hipStream_t st, const int* qlist, const int* qcount) {
+                                     hipStream_t st, const int* qlist, const int* qcount,
+                                     const float* fkey = nullptr, const int* fid = nullptr) {
   const int ntiles = (ntotal + kBN - 1) / kBN;
   const int nqt = nq_pad / kBQ;
   const int nblk = nqt * nsplit;
   const int nstage = (int)(ld * esize / 128);
   if (esize == 4)
-    hipLaunchKernelGGL((gemm_topk<KP, MODE, float>), dim3(nblk), dim3(256), 0, st,
+    hipLaunchKernelGGL((gemm_topk<KP, MODE, float, FLOOR>), dim3(nblk), dim3(256), 0, st,
                        (const float*)X, xaux, (const float*)Q, qaux, ld, nstage, ntotal, ntiles,
-                       nsplit, nqt, self0, part.key, part.id, qlist, qcount);
+                       nsplit, nqt, self0, part.key, part.id, qlist, qcount, fkey, fid);
   else
-    hipLaunchKernelGGL((gemm_topk<KP, MODE, uint16_t>), dim3(nblk), dim3(256), 0, st,
+    hipLaunchKernelGGL((gemm_topk<KP, MODE, uint16_t, FLOOR>), dim3(nblk), dim3(256), 0, st,
                        (const uint16_t*)X, xaux, (const uint16_t*)Q, qaux, ld, nstage, ntotal,
-                       ntiles, nsplit, nqt, self0, part.key, part.id, qlist, qcount);
+                       ntiles, nsplit, nqt, self0, part.key, part.id, qlist, qcount, fkey, fid);
   return hipGetLastError();
 }
 
@@ -273,10 +289,17 @@ static hipError_t gemm_dispatch(int mode, const void* X, const float* xaux, cons
 hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, const void* Q,
                             const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
                             int nsplit, int64_t self0, Partials part, hipStream_t st,
-                            const int* qlist, const int* qcount) {
+                            const int* qlist, const int* qcount, const float* fkey,
+                            const int* fid) {
   if (nq_pad % kBQ != 0 || (ld * esize) % 128 != 0 || part.KP != KP || part.P != 2 * nsplit ||
-      (esize != 4 && esize != 2) || ((qlist == nullptr) != (qcount == nullptr)))
+      (esize != 4 && esize != 2) || ((qlist == nullptr) != (qcount == nullptr)) ||
+      ((fkey == nullptr) != (fid == nullptr)))
     return hipErrorInvalidValue;
+  if (fkey) {  // the second page of an inner-product search (64-entry lists)
+    if (KP != 64 || mode != MODE_IP) return hipErrorInvalidValue;
+    return gemm_dispatch_mode<64, MODE_IP, true>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
+                                                 nsplit, self0, part, st, qlist, qcount, fkey, fid);
+  }
   switch (KP) {
     case 8:
       return gemm_dispatch<8>(mode, X, xaux, Q, qaux, ld, esize, ntotal, nq_pad, nsplit, self0, part, st, qlist, qcount);

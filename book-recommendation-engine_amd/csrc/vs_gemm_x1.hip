@@ -52,6 +52,11 @@
 #ifndef VS_X1_STAGGER
 #define VS_X1_STAGGER 1
 #endif
+// Step schedule: 1 = fragment reads half a step ahead, DMA pieces between the
+// MFMAs of each wave (round 2); 2 = separate load and matrix segments (below).
+#ifndef VS_X1_SCHED
+#define VS_X1_SCHED 2
+#endif
 // Diagnostic builds only (tools/x1_probe.sh; wrong results by design): drop the
 // LDS-DMA, the fragment reads, the mid-step barrier or the epilogue.
 #ifndef VS_X1_P_NODMA
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
     int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
-    int qg, float* __restrict__ pkey, int* __restrict__ pid) {
+    int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
   constexpr int D = NBUF - 1;      // steps in flight
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
@@ -351,26 +356,57 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         };
         // int8: xs holds s_x (IP) or s_x / |x| (COS), qsc s_q or s_q / |q|
         f32x4 xa[4], xsv[4];
+        // The per-row values of the lane's 16 rows: four 16-B loads in ONE asm
+        // statement that also retires them (vmcnt(0): it drains the LDS-DMA
+        // pieces in flight too).  Loads the compiler sees would get a vmcnt
+        // counted without the DMA pieces, and its waits leak into the loop (a
+        // drain at the top of every step); here the drain happens only on this
+        // path: int8 blocks that pass the fast reject below (rare after the
+        // first tiles), bf16 L2 / cosine tiles.
+        const int gbase = t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0));  // uniform
+        auto load_rows = [&](const float* src, f32x4 (&o)[4]) {
+          const float* p0 = src + rowof(0);
+          const float* p1 = src + rowof(1);
+          const float* p2 = src + rowof(2);
+          const float* p3 = src + rowof(3);
+          asm volatile(
+              "global_load_dwordx4 %0, %4, off\n\t"
+              "global_load_dwordx4 %1, %5, off\n\t"
+              "global_load_dwordx4 %2, %6, off\n\t"
+              "global_load_dwordx4 %3, %7, off\n\t"
+              "s_waitcnt vmcnt(0)"
+              : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
+              : "v"(p0), "v"(p1), "v"(p2), "v"(p3)
+              : "memory");
+        };
+        auto load_aux = [&]() {
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-          const int g = rowof(jj);
-          if constexpr ((MODE == MODE_L2 || MODE == MODE_COS) && EL != FILTER_I8)
-            xa[jj] = *(const f32x4*)(xaux + g);
-          xsv[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (EL == FILTER_I8) xsv[jj] = *(const f32x4*)(xs + g);
-        }
+          for (int jj = 0; jj < 4; ++jj) {
+            xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+            xsv[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          if constexpr ((MODE == MODE_L2 || MODE == MODE_COS) && EL != FILTER_I8) load_rows(xaux, xa);
+          if constexpr (EL == FILTER_I8) load_rows(xs, xsv);
+        };
         // int8: a block's scores are fl(fl(float(sum)) * fl(f_q * f_x)), monotone
         // in the sum and in f_x (both factors >= 0), so the lane's largest
         // factor over its 16 rows and the largest sum bound every score of the
         // block from above: when that bound cannot beat the list, the block is
-        // skipped without converting its 16 sums
+        // skipped without converting its 16 sums.  The lane's 16 rows are the
+        // rows of its 32-row group whose bit 2 is fh >> 2, and xgmax holds that
+        // maximum per (group, bit): two SCALAR loads per block (the vector
+        // loads of the 16 factors, which the compiler retires with a vmcnt
+        // that also drains the LDS-DMA pieces in flight, happen only for
+        // blocks that pass)
         float fmax = 0.0f;
+        bool loaded = false;
         if constexpr (EL == FILTER_I8) {
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fmax = fmaxf(fmax, xsv[jj][e]);
+          const int grp = gbase >> 5;  // uniform
+          const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
+          fmax = (fh & 4) ? g1 : g0;
+        } else {
+          load_aux();
+          loaded = true;
         }
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
@@ -380,6 +416,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
             for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
             const float upper = amax > 0 ? (float)amax * (qsc[qb] * fmax) : 0.0f;
             if (!(upper > -lk[qb][KR - 1])) continue;  // key = -score < last needs score > -last
+            if (!loaded) {
+              load_aux();
+              loaded = true;
+            }
           }
           f32x16 key;
 #pragma unroll
@@ -438,6 +478,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     };
 
     if ((VS_X1_PRIO == 1 && w >= 4) || (VS_X1_PRIO == 2 && w < 4)) __builtin_amdgcn_s_setprio(1);
+#if VS_X1_SCHED == 1
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
 #pragma unroll
@@ -529,6 +570,73 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
       buf = nbuf;
     }
+#else
+    // Segmented schedule: every step of a wave is a LOAD segment (the step's 12
+    // fragment reads, the 4 LDS-DMA pieces of step s+3, the wait for this
+    // wave's pieces of step s+1) and a MATRIX segment (the step's 16 MFMAs),
+    // each closed by a barrier.  Waves 4-7 run one barrier behind waves 0-3,
+    // so on every SIMD one wave's load segment — whose DMA issue stalls that
+    // wave for ~100-185 cycles per piece (MI355X_MICROARCH.md, LDS-DMA piece
+    // issue cost) — runs beside its partner's matrix segment, and no wave's
+    // MFMA stream is cut by its own DMA issue (the 8-phase GEMM template's
+    // pairing, cdna_hip_programming.md).  3 steps in flight over a ring of 5
+    // images: the image a DMA refills was read two barriers earlier by every
+    // wave (reads retired by the lgkmcnt wait that opens the reader's matrix
+    // segment); an image is read only after the barrier that follows every
+    // wave's counted wait for its pieces.
+    static_assert(NBUF == 5, "segmented schedule: 3 steps in flight over 5 images");
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stage_piece(j);
+      advance_cursor();
+    }
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step 0
+    __builtin_amdgcn_s_barrier();
+    const bool lag = VS_X1_STAGGER && w >= 4;
+    if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
+    int buf = 0, t = t0, ks = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      rd(buf, 0, fa0, fb0);
+      rd(buf, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) stage_piece(i);
+      advance_cursor();
+      __builtin_amdgcn_sched_barrier(0);
+      // this wave's pieces of step s+1 (the younger steps s+2, s+3 stay in flight)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, fb0);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa0, fb0);
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (++ks == nksteps) {  // beside the partner's matrix segment
+        ks = 0;
+#if !VS_X1_P_NOEPI
+        epilogue(t);
+#else
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+#endif
+        ++t;
+      }
+      buf = buf + 1 == NBUF ? 0 : buf + 1;
+    }
+    if (!lag && VS_X1_STAGGER) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
   }
 
@@ -584,7 +692,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, VS_X1_NBUF, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
                        (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0, a.self0, a.qrow,
-                       a.qcount, c, nchunk, part.KP, qg, part.key, part.id);
+                       a.qcount, c, nchunk, part.KP, qg, part.key, part.id, a.xgmax);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -620,7 +728,7 @@ hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStre
       part.P != 4 * a.nsplit || a.nsplit < 1 || a.ntotal <= 0)
     return hipErrorInvalidValue;
   if (a.filter == FILTER_I8) {
-    if (!a.xs || !a.qs || a.ld > kI8MaxLd) return hipErrorInvalidValue;
+    if (!a.xs || !a.qs || !a.xgmax || a.ld > kI8MaxLd) return hipErrorInvalidValue;
     return x1_dispatch<FILTER_I8>(mode, a, part, st, ndispatch);
   }
   return x1_dispatch<FILTER_BF16>(mode, a, part, st, ndispatch);
@@ -827,6 +935,31 @@ __global__ __launch_bounds__(256) void mul_arrays_kernel(const float* __restrict
                                                          float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) out[i] = a[i] * b[i];
+}
+
+// out[2 g + b] = max of f[r] over the rows r of 32-row group g with bit 2 of r
+// equal to b (f >= 0); n a multiple of 32.
+__global__ __launch_bounds__(256) void group_max_kernel(const float* __restrict__ f, int64_t ngrp,
+                                                        float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (group, bit)
+  if (i >= 2 * ngrp) return;
+  const float* p = f + (i >> 1) * 32 + (i & 1) * 4;
+  float m = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x4 v = *(const f32x4*)(p + 8 * j);
+    m = fmaxf(fmaxf(fmaxf(m, v[0]), fmaxf(v[1], v[2])), v[3]);
+  }
+  out[i] = m;
+}
+
+hipError_t launch_group_max(const float* f, int64_t n, float* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n % 32 != 0) return hipErrorInvalidValue;
+  const int64_t m = 2 * (n / 32);
+  hipLaunchKernelGGL(group_max_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, f,
+                     n / 32, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* out,

@@ -27,14 +27,21 @@ __device__ __forceinline__ void widen_chunk(const uint4 v, float (&f)[16 / sizeo
   }
 }
 
-template <int NQ, int KP, int MODE, typename T>
+// FLOOR: query q's list admits only rows strictly after (fkey[q], fid[q]) in
+// (key, row) order (the second page of an inner-product search, vs_api.hip
+// run_wide_k); `run` (optional device flag): nothing to do when *run == 0.
+template <int NQ, int KP, int MODE, typename T, bool FLOOR = false>
 __global__ __launch_bounds__(256) void gemv_topk(const T* __restrict__ X,
                                                  const float* __restrict__ Q, int64_t ld,
                                                  int ntotal, int rows_per_block,
                                                  float* __restrict__ pkey,
-                                                 int* __restrict__ pid) {
+                                                 int* __restrict__ pid,
+                                                 const float* __restrict__ fkey,
+                                                 const int* __restrict__ fid,
+                                                 const int* __restrict__ run) {
   constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   extern __shared__ __attribute__((aligned(16))) float sq[];  // [NQ][ld]
+  if (run && *run == 0) return;  // uniform
   const int tid = threadIdx.x;
   for (int64_t i = (int64_t)tid * 4; i < (int64_t)NQ * ld; i += 1024)
     *(f32x4*)(sq + i) = *(const f32x4*)(Q + i);
@@ -50,6 +57,13 @@ __global__ __launch_bounds__(256) void gemv_topk(const T* __restrict__ X,
   float lk[KP];
   int li[KP];
   list_init<KP, int>(lk, li);
+  float fk = 0.0f;
+  int fi = 0;
+  if constexpr (FLOOR) {
+    const int ql = (tid & 63) < NQ ? (tid & 63) : 0;
+    fk = fkey[ql];
+    fi = fid[ql];
+  }
 
   for (int r = rb0 + 4 * w; r < rb1; r += 16) {
     float acc[4][NQ];
@@ -108,7 +122,7 @@ __global__ __launch_bounds__(256) void gemv_topk(const T* __restrict__ X,
       const int row = r + a;
       if (lane < NQ && row < ntotal) {
         const float key = (MODE == MODE_L2D) ? mine : -mine;
-        list_insert<KP, int>(lk, li, key, row);
+        if (!FLOOR || lex_less(fk, fi, key, row)) list_insert<KP, int>(lk, li, key, row);
       }
     }
   }
@@ -150,17 +164,27 @@ __global__ __launch_bounds__(256) void gemv_topk(const T* __restrict__ X,
 
 template <int NQ, int KP, typename T>
 static hipError_t gemv_dispatch_t(int mode, const T* X, const float* Q, int64_t ld,
-                                  int ntotal, int nblocks, Partials part, hipStream_t st) {
+                                  int ntotal, int nblocks, Partials part, hipStream_t st,
+                                  const float* fkey, const int* fid, const int* run) {
   const int ntot16 = (ntotal + 15) & ~15;
   int rpb = (ntot16 + nblocks - 1) / nblocks;
   rpb = (rpb + 15) & ~15;
   const size_t lds = (size_t)NQ * ld * sizeof(float) + (size_t)4 * NQ * KP * 8;
+  if (fkey) {
+    if constexpr (KP == 64 && NQ <= 2) {
+      if (mode != MODE_IP) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_IP, T, true>), dim3(nblocks), dim3(256), lds, st,
+                         X, Q, ld, ntotal, rpb, part.key, part.id, fkey, fid, run);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (mode == MODE_L2D)
     hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_L2D, T>), dim3(nblocks), dim3(256), lds, st, X, Q,
-                       ld, ntotal, rpb, part.key, part.id);
+                       ld, ntotal, rpb, part.key, part.id, nullptr, nullptr, run);
   else if (mode == MODE_IP)
     hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_IP, T>), dim3(nblocks), dim3(256), lds, st, X, Q,
-                       ld, ntotal, rpb, part.key, part.id);
+                       ld, ntotal, rpb, part.key, part.id, nullptr, nullptr, run);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -168,44 +192,49 @@ static hipError_t gemv_dispatch_t(int mode, const T* X, const float* Q, int64_t 
 
 template <int NQ, int KP>
 static hipError_t gemv_dispatch_q(int mode, const void* X, int esize, const float* Q, int64_t ld,
-                                  int ntotal, int nblocks, Partials part, hipStream_t st) {
+                                  int ntotal, int nblocks, Partials part, hipStream_t st,
+                                  const float* fkey, const int* fid, const int* run) {
   if (esize == 4)
-    return gemv_dispatch_t<NQ, KP, float>(mode, (const float*)X, Q, ld, ntotal, nblocks, part, st);
+    return gemv_dispatch_t<NQ, KP, float>(mode, (const float*)X, Q, ld, ntotal, nblocks, part, st,
+                                          fkey, fid, run);
   return gemv_dispatch_t<NQ, KP, uint16_t>(mode, (const uint16_t*)X, Q, ld, ntotal, nblocks, part,
-                                           st);
+                                           st, fkey, fid, run);
 }
 
 template <int KP>
 static hipError_t gemv_dispatch(int mode, int nq, const void* X, int esize, const float* Q,
                                 int64_t ld, int ntotal, int nblocks, Partials part,
-                                hipStream_t st) {
+                                hipStream_t st, const float* fkey, const int* fid,
+                                const int* run) {
   switch (nq) {
     case 1:
-      return gemv_dispatch_q<1, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<1, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     case 2:
-      return gemv_dispatch_q<2, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<2, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     case 3:
     case 4:
-      return gemv_dispatch_q<4, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<4, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     default:
-      return gemv_dispatch_q<8, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch_q<8, KP>(mode, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
   }
 }
 
 hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, const float* Q,
-                            int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st) {
+                            int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st,
+                            const float* fkey, const int* fid, const int* run) {
   if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks || (ld * esize) % 16 != 0 ||
-      (esize != 4 && esize != 2))
+      (esize != 4 && esize != 2) || ((fkey == nullptr) != (fid == nullptr)) ||
+      (fkey && (KP != 64 || nq > 2 || mode != MODE_IP)))
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:
-      return gemv_dispatch<8>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<8>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     case 16:
-      return gemv_dispatch<16>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<16>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     case 32:
-      return gemv_dispatch<32>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<32>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     case 64:
-      return gemv_dispatch<64>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st);
+      return gemv_dispatch<64>(mode, nq, X, esize, Q, ld, ntotal, nblocks, part, st, fkey, fid, run);
     default:
       return hipErrorInvalidValue;
   }

@@ -59,14 +59,21 @@ struct Partials {
 // With `qlist`, query slot s of the (nq_pad-row) batch is row qlist[s] of Q (and
 // of qaux; self row self0 + qlist[s]), only slots s < *qcount are computed
 // (query tiles past the device-side count return at once), lists indexed by slot.
+// With fkey/fid (inner product, KP = 64): only rows strictly after the query's
+// floor (fkey, fid) in (key, row) order enter (floors indexed like qaux).
 hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, const void* Q,
                             const float* qaux, int64_t ld, int esize, int ntotal, int nq_pad,
                             int nsplit, int64_t self0, Partials part, hipStream_t st,
-                            const int* qlist = nullptr, const int* qcount = nullptr);
+                            const int* qlist = nullptr, const int* qcount = nullptr,
+                            const float* fkey = nullptr, const int* fid = nullptr);
 // Streaming (HBM-bound) distance + top-k for nq <= kGemvMaxQ.
 // X fp32 or bf16 rows; Q always fp32 (values already rounded for bf16 indexes).
+// With fkey/fid (inner product, KP = 64): the floor of each query, as in
+// launch_gemm_topk; `run` (device, optional): every block exits when *run == 0.
 hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, const float* Q,
-                            int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st);
+                            int64_t ld, int ntotal, int nblocks, Partials part, hipStream_t st,
+                            const float* fkey = nullptr, const int* fid = nullptr,
+                            const int* run = nullptr);
 // Small-batch MFMA path (nq <= kSkinnyMaxQ, KP <= 32, IP or L2 via norms):
 // one list per query per block, part.P == nblocks.
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
@@ -93,6 +100,7 @@ struct X1Args {
   int filter = FILTER_BF16;
   const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
+  const float* xgmax = nullptr;  // int8: launch_group_max of xs (capacity rows)
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
   const void* QH = nullptr;      // query plane, tile-major (self-join: the stored plane)
   int qtile0 = 0;                // QH's tile of query tile 0 (self-join: self0 / 256)
@@ -154,6 +162,9 @@ hipError_t launch_compose_list(const int* outer, const int* inner, const int* co
 // *out = clamp(*count - w0, 0, cap): the device-side count of one slot window
 // [w0, w0 + cap) of a gathered batch.
 hipError_t launch_window_count(const int* count, int w0, int cap, int* out, hipStream_t st);
+// out[2 g + b] = max of f over the rows of 32-row group g whose bit 2 is b
+// (the int8 filter's per-lane factor bound), n a multiple of 32.
+hipError_t launch_group_max(const float* f, int64_t n, float* out, hipStream_t st);
 // out[i] = a[i] * b[i] (the int8 cosine's folded factors s / |x|).
 hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* out,
                              hipStream_t st);
@@ -218,6 +229,17 @@ hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t
 // Shard lists [nparts][nq][k_in] (scores, int64 labels) -> [nq][k].
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts,
                               int nq, int k_in, int k, float* D, int64_t* I, hipStream_t st);
+// Inner product with k > 32 (vs_support.hip): D1/I1 = the first page (the
+// lexicographic top-64 of each query: scores, labels with id_base); flags[q] =
+// a second page is needed (the k-th key's run of equal keys reaches entry 63, or
+// raw and the page is full), fkey/fid = its floor (key and local row of entry 63).
+hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, int raw,
+                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st);
+// The two pages -> (D, I) rows of k <= 128 entries (faiss's rule unless raw);
+// D2/I2 rows are read only where flags[q].
+hipError_t launch_page_finish(const float* D1, const int64_t* I1, const float* D2,
+                              const int64_t* I2, const int* flags, int nq, int k, int raw,
+                              float* D, int64_t* I, hipStream_t st);
 // out[r] = sum_j X[r][j]^2 for rows [r0, r0+n) (fp32 or bf16 rows).
 hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, int64_t n,
                             float* out, hipStream_t st);

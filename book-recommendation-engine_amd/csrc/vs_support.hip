@@ -282,14 +282,25 @@ __global__ __launch_bounds__(64) void merge_parts_kernel(const float* __restrict
                             D + (int64_t)q * k + lane, I + (int64_t)q * k + lane);
 }
 
+__global__ void merge_parts_wide_kernel(const float* __restrict__ Dp,
+                                        const int64_t* __restrict__ Ip, int nparts, int nq,
+                                        int k_in, int need, int k, float* __restrict__ D,
+                                        int64_t* __restrict__ I);
+
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts, int nq,
                               int k_in, int k, float* D, int64_t* I, hipStream_t st) {
   if (k < 1 || k > 64 || nq < 0 || nparts < 1 || k_in < 1) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   // the pool keeps the lexicographically best `need` entries of all parts: k for
-  // L2; for inner product the 2k-1 that faiss's tie rule reads (capped at 64)
+  // L2; for inner product the 2k-1 that faiss's tie rule reads
   const bool asc = (mode == MODE_L2 || mode == MODE_L2D);
-  const int need = asc ? k : (2 * k - 1 < 64 ? 2 * k - 1 : 64);
+  if (!asc && 2 * k - 1 > 64) {  // raw shard lists of up to 128 entries
+    if (k_in > 128 || nparts > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(merge_parts_wide_kernel, dim3(nq), dim3(64), 0, st, Dp, Ip, nparts, nq,
+                       k_in, 2 * k - 1, k, D, I);
+    return hipGetLastError();
+  }
+  const int need = asc ? k : 2 * k - 1;
   const int KP = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 64;
   switch (KP) {
 #define VS_MERGEP_CASE(KPV)                                                                   \
@@ -306,6 +317,128 @@ hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int 
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Inner product with k > 32 (faiss's tie rule reads the 2k-1 <= 127 best (key,
+// label) entries; lists hold 64): the search's first page is its lexicographic
+// top-64 (D1/I1, scores + labels with id_base), and where the rule may need more
+// — the k-th key's run of equal keys reaching entry 63 — a second page holds the
+// next 64 entries after entry 63 (D2/I2, rows of the flagged queries only).  Raw
+// searches with 64 < k <= 128 take both pages whenever the first is full.
+// One thread per query: flags[q], and the floor of the second page (the key and
+// local row of entry 63).
+__global__ __launch_bounds__(256) void page_check_kernel(const float* __restrict__ D1,
+                                                         const int64_t* __restrict__ I1, int nq,
+                                                         int k, int raw, int64_t id_base,
+                                                         float* __restrict__ fkey,
+                                                         int* __restrict__ fid,
+                                                         int* __restrict__ flags) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const float* d = D1 + (int64_t)q * 64;
+  const int64_t* i = I1 + (int64_t)q * 64;
+  const bool full = i[63] >= 0;
+  flags[q] = full && (raw || d[63] == d[k - 1]) ? 1 : 0;
+  fkey[q] = -d[63];  // key = -score (inner product)
+  fid[q] = full ? (int)(i[63] - id_base) : -1;
+}
+
+hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, int raw,
+                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || k > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(page_check_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, D1, I1, nq, k,
+                     raw, id_base, fkey, fid, flags);
+  return hipGetLastError();
+}
+
+// One wave per query: the two pages concatenated (the second page starts after
+// the first's last entry, so the concatenation is the lexicographic top-128),
+// then faiss's tie rule (unless raw) and the k outputs.
+__global__ __launch_bounds__(64) void page_finish_kernel(
+    const float* __restrict__ D1, const int64_t* __restrict__ I1, const float* __restrict__ D2,
+    const int64_t* __restrict__ I2, const int* __restrict__ flags, int k, int raw,
+    float* __restrict__ D, int64_t* __restrict__ I) {
+  __shared__ float sk[128];
+  __shared__ int64_t si[128];
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const bool two = flags[q] != 0;
+  const int64_t o = (int64_t)q * 64 + lane;
+  const int64_t a = I1[o];
+  sk[lane] = a >= 0 ? -D1[o] : FLT_MAX;
+  si[lane] = a >= 0 ? a : -1;
+  const int64_t b = two ? I2[o] : -1;
+  sk[64 + lane] = b >= 0 ? -D2[o] : FLT_MAX;
+  si[64 + lane] = b >= 0 ? b : -1;
+  __syncthreads();
+  if (lane == 0 && !raw) faiss_ip_tie_order<int64_t>(sk, si, 128, k);
+  __syncthreads();
+  for (int j = lane; j < k; j += 64) {
+    const int64_t id = si[j];
+    D[(int64_t)q * k + j] = id >= 0 ? -sk[j] : -FLT_MAX;
+    I[(int64_t)q * k + j] = id;
+  }
+}
+
+hipError_t launch_page_finish(const float* D1, const int64_t* I1, const float* D2,
+                              const int64_t* I2, const int* flags, int nq, int k, int raw,
+                              float* D, int64_t* I, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || k > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(page_finish_kernel, dim3(nq), dim3(64), 0, st, D1, I1, D2, I2, flags, k, raw,
+                     D, I);
+  return hipGetLastError();
+}
+
+// Shard merge when the inner-product rule needs more than 64 entries (k > 32):
+// each part is a raw lexicographic list of k_in <= 128 entries; one thread
+// merges them (nparts x 127 steps) into LDS, then the rule and the k outputs.
+__global__ __launch_bounds__(64) void merge_parts_wide_kernel(const float* __restrict__ Dp,
+                                                              const int64_t* __restrict__ Ip,
+                                                              int nparts, int nq, int k_in,
+                                                              int need, int k,
+                                                              float* __restrict__ D,
+                                                              int64_t* __restrict__ I) {
+  __shared__ float sk[128];
+  __shared__ int64_t si[128];
+  __shared__ int head[64];  // nparts <= 64 (launcher)
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  head[lane] = 0;
+  __syncthreads();
+  if (lane == 0) {
+    for (int j = 0; j < 128; ++j) {
+      float bk = FLT_MAX;
+      int64_t bi = -1;
+      int bp = -1;
+      if (j < need) {
+        for (int p = 0; p < nparts; ++p) {
+          if (head[p] >= k_in) continue;
+          const int64_t off = ((int64_t)p * nq + q) * k_in + head[p];
+          const int64_t id = Ip[off];
+          if (id < 0) continue;
+          const float key = -Dp[off];
+          if (bp < 0 || lex_less(key, id, bk, bi)) {
+            bk = key;
+            bi = id;
+            bp = p;
+          }
+        }
+      }
+      if (bp >= 0) ++head[bp];
+      sk[j] = bp >= 0 ? bk : FLT_MAX;
+      si[j] = bp >= 0 ? bi : -1;
+    }
+    faiss_ip_tie_order<int64_t>(sk, si, 128, k);
+  }
+  __syncthreads();
+  for (int j = lane; j < k; j += 64) {
+    const int64_t id = si[j];
+    D[(int64_t)q * k + j] = id >= 0 ? -sk[j] : -FLT_MAX;
+    I[(int64_t)q * k + j] = id;
+  }
 }
 
 // ---------------------------------------------------------------------------

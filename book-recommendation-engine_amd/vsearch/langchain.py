@@ -43,7 +43,8 @@ from . import faiss as vfaiss
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["Document", "InMemoryDocstore", "DistanceStrategy", "FAISS"]
+__all__ = ["Document", "InMemoryDocstore", "DistanceStrategy", "FAISS",
+           "migrate_reference_store", "full_faiss_rebuild"]
 
 
 class Document:
@@ -530,9 +531,12 @@ class FAISS:
             # LangChain classes, which this loader never unpickles
             raise ReferenceStoreError(
                 f"{path}: found {index_name}.pkl (a LangChain pickle) but no "
-                f"{index_name}.docstore.json. Rebuild the store once from the catalog "
-                "with vsearch.langchain.full_faiss_rebuild (the reference's own "
-                "book_vector full_faiss_rebuild, main.py:428-471); the pickle is not loaded.")
+                f"{index_name}.docstore.json. Migrate it once with "
+                "vsearch.langchain.migrate_reference_store (the vectors of "
+                f"{index_name}.faiss kept, the docstore rebuilt from the catalog rows in "
+                "label order, no re-embedding), or rebuild it with "
+                "vsearch.langchain.full_faiss_rebuild (the reference's own book_vector "
+                "full_faiss_rebuild, main.py:428-471); the pickle is not loaded.")
         index = vfaiss.read_index(str(path / f"{index_name}.faiss"),
                                   device=kwargs.pop("device", None),
                                   index_factory=kwargs.pop("index_factory", None))
@@ -547,6 +551,68 @@ class FAISS:
 class ReferenceStoreError(ValueError):
     """load_local found a LangChain-written store (index.pkl docstore) that this
     drop-in does not unpickle; see full_faiss_rebuild."""
+
+
+def migrate_reference_store(folder_path: str, texts: List[str], metadatas: List[dict],
+                            embeddings=None, ids: Optional[List[str]] = None,
+                            index_name: str = "index", *, verify_sample: int = 0,
+                            **kwargs: Any) -> "FAISS":
+    """Migrates a store the reference wrote (``index.faiss`` + LangChain's pickled
+    ``index.pkl``) WITHOUT re-embedding the catalogue: the vectors are read from
+    ``index.faiss`` (faiss's flat format, vsearch.faiss.read_index) onto the GPU,
+    and the docstore — which lives only in the pickle, never opened here — is
+    rebuilt from the caller's catalogue rows.
+
+    ``texts`` / ``metadatas`` must be the rows in the order the store was built,
+    i.e. label order: the reference's full rebuild embeds
+    ``SELECT ... FROM catalog`` row by row with the main.py:449-460 text and the
+    main.py:461-465 metadata (vsearch.synth.book_text / book_metadata restate
+    both) and appends incremental books with ``add_texts`` (main.py:148).  A row
+    count that differs from ``index.faiss``'s ntotal is refused.  ``ids``
+    default to fresh uuid4 strings, as ``FAISS.from_texts`` assigns them
+    (docstore ids are internal to the store: the reference's readers use
+    ``metadata["book_id"]``).  ``verify_sample`` > 0 embeds that many evenly
+    spaced texts with ``embeddings`` and checks them against the stored rows
+    (the label order check, at that many embedding calls instead of all).
+    Writes ``index.docstore.json`` beside the untouched ``index.faiss`` /
+    ``index.pkl``; afterwards ``FAISS.load_local`` opens the directory."""
+    path = Path(folder_path)
+    index = vfaiss.read_index(str(path / f"{index_name}.faiss"),
+                              device=kwargs.pop("device", None),
+                              index_factory=kwargs.pop("index_factory", None))
+    texts = list(texts)
+    metadatas = list(metadatas)
+    n = int(index.ntotal)
+    if len(texts) != n or len(metadatas) != n:
+        raise ValueError(f"migrate_reference_store: {index_name}.faiss holds {n} rows but "
+                         f"{len(texts)} texts / {len(metadatas)} metadatas were given (the rows "
+                         "must be the catalogue in the store's label order)")
+    ids = list(ids) if ids is not None else [str(uuid.uuid4()) for _ in texts]
+    if len(ids) != n or len(set(ids)) != n:
+        raise ValueError("migrate_reference_store: ids must be n distinct strings")
+    if verify_sample > 0 and n:
+        if embeddings is None:
+            raise ValueError("migrate_reference_store: verify_sample needs embeddings")
+        pick = sorted({int(i) for i in np.linspace(0, n - 1, min(verify_sample, n))})
+        got = np.asarray(embeddings.embed_documents([texts[i] for i in pick]), dtype=np.float32)
+        for j, i in enumerate(pick):
+            if not np.allclose(index.reconstruct(i), got[j], rtol=1e-5, atol=1e-6):
+                raise ValueError(f"migrate_reference_store: row {i} of {index_name}.faiss is "
+                                 f"not the embedding of texts[{i}]: the rows are not in the "
+                                 "store's label order")
+    docstore = InMemoryDocstore({_id: Document(page_content=t, metadata=m, id=_id)
+                                 for t, m, _id in zip(texts, metadatas, ids)})
+    store = FAISS(embeddings, index, docstore, dict(enumerate(ids)), **kwargs)
+    payload = {
+        "format": "vsearch-docstore-v1",
+        "index_to_docstore_id": [[i, _id] for i, _id in enumerate(ids)],
+        "docstore": {k: v.to_json() for k, v in docstore._dict.items()},
+    }
+    tmp = path / f"{index_name}.docstore.json.tmp"
+    with open(tmp, "w", encoding="utf-8") as f:
+        json.dump(payload, f)
+    tmp.replace(path / f"{index_name}.docstore.json")
+    return store
 
 
 def full_faiss_rebuild(texts: List[str], embeddings, metadatas: List[dict], folder_path: str,

@@ -47,8 +47,9 @@ extern "C" {
  * (key, label), key = distance (L2) or -score (IP), in that order, instead of
  * faiss's inner-product tie order.  The per-shard half of an exact row-sharded
  * search: faiss's IP tie rule is a function of the 2k-1 best (key, label) pairs
- * of the union, so each shard returns its raw best 2k-1 and vs_merge_topk
- * applies the rule once (vsearch/sharded.py).  No effect on L2. */
+ * of the union, so each shard returns its raw best 2k-1 (inner product: k up to
+ * 2 * VS_MAX_K under this flag) and vs_merge_topk applies the rule once
+ * (vsearch/sharded.py).  No effect on L2. */
 #define VS_RAW_ORDER 4
 
 /* Status codes. */
@@ -58,7 +59,9 @@ extern "C" {
 #define VS_E_OOM (-3)     /* device allocation failed                          */
 #define VS_E_UNSUPPORTED (-4)
 
-/* Largest k served by the fused GPU top-k (register lists of up to 64 entries). */
+/* Largest k of a search (register lists of up to 64 entries; inner-product
+ * searches that need more — faiss's tie rule at k > 32, raw k up to 128 — read a
+ * second page of 64 after the first, vs_api.hip run_wide_k). */
 #define VS_MAX_K 64
 
 typedef struct vs_index vs_index;
@@ -151,7 +154,8 @@ int vs_set_id_base(vs_index* idx, int64_t id_base);
  * lower label first; inner product follows faiss's CMin-heap rule (equal scores
  * come out in DESCENDING label order, and which tied labels stay depends on the
  * labels of the better rows — vs_support.hip faiss_ip_tie_order, exact for
- * k <= 32).  L2 calls with n < 20 use faiss's sequential branch (direct sum of
+ * every k <= VS_MAX_K: the rule reads the 2k-1 <= 127 best entries, taken from
+ * a second page where the k-th key's run of equal keys fills the first).  L2 calls with n < 20 use faiss's sequential branch (direct sum of
  * squares), n >= 20 the BLAS branch (|q|^2 + |x|^2 - 2 q.x clamped at 0).
  * Asynchronous on `stream` when every buffer is on the device (no host wait).
  * Caller: FAISS.similarity_search_with_score_by_vector, reached from
@@ -185,8 +189,9 @@ int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_se
 
 /* Merge nparts per-shard top-k lists into one (faiss: the ResultHandler merge;
  * GPU-side half of the RCCL all-gather top-k merge).  Inputs are DEVICE arrays
- * laid out [nparts][nq][k_in] (scores + int64 labels, -1 = empty); outputs are
- * DEVICE arrays [nq][k].  metric picks the order (L2 ascending, IP descending). */
+ * laid out [nparts][nq][k_in] (scores + int64 labels, -1 = empty; raw order for
+ * inner product, k_in <= 2 * VS_MAX_K, nparts <= 64); outputs are DEVICE arrays
+ * [nq][k].  metric picks the order (L2 ascending, IP descending). */
 int vs_merge_topk(const float* D_parts, const int64_t* I_parts, int64_t nparts, int64_t nq,
                   int64_t k_in, int64_t k, int metric, float* D, int64_t* I, void* stream);
 

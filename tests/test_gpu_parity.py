@@ -116,9 +116,12 @@ def test_empty_index(vf, metric):
 
 
 @pytest.mark.parametrize("metric", [L2, IP])
-@pytest.mark.parametrize("k", [1, 2, 4, 5, 10, 16])
+@pytest.mark.parametrize("k", [1, 2, 4, 5, 10, 16, 33, 50, 60, 64])
 def test_ties_match_faiss_heap(vf, metric, k):
-    """Tie-heavy integer data: labels must equal the C faiss-heap restatement exactly."""
+    """Tie-heavy integer data: labels must equal the C faiss-heap restatement
+    exactly.  Inner product with k > 32 reads up to 2k - 1 = 127 entries: the
+    two-page search (vs_api.hip run_wide_k; nq = 1 on the GEMV, 7 and 40 on the
+    fp32 MFMA GEMM; service.py:529-531 asks for k = 60)."""
     xb = _rand(600, 3, 12, "int")
     for nq in (1, 7, 40):
         xq = _rand(nq, 3, 13 + nq, "int")
@@ -128,6 +131,44 @@ def test_ties_match_faiss_heap(vf, metric, k):
         Dc, Ic = cfaiss.knn_seq(xb, xq, k, metric)
         np.testing.assert_array_equal(I, Ic)
         np.testing.assert_array_equal(D, Dc)
+
+
+@pytest.mark.parametrize("nq", [1, 2, 5, 300])
+@pytest.mark.parametrize("k", [40, 60, 64])
+def test_ip_wide_k_duplicate_rows(vf, nq, k):
+    """Float rows with a block of 150 duplicates (the re-ingested book of
+    book_vector/main.py:148, which add_texts appends again): the duplicates'
+    run of equal keys fills the first page, and faiss's rule picks the k
+    smallest of their labels (descending); checked against the C heap
+    restatement (labels exact, scores within the fp32 contract)."""
+    d = 64
+    xb = _rand(6000, d, 71)
+    dup = _rand(1, d, 72)[0]
+    pos = np.random.default_rng(73).choice(6000, 150, replace=False)
+    xb[pos] = dup
+    xq = _rand(nq, d, 74) * 0.05 + dup  # near the duplicated row
+    index = vf.IndexFlat(d, IP)
+    index.add(xb)
+    D, I = index.search(xq, k)
+    Dc, Ic = cfaiss.knn_seq(xb, xq, k, IP)
+    np.testing.assert_array_equal(I, Ic)
+    np.testing.assert_allclose(D, Dc, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("nq", [1, 7, 200])
+@pytest.mark.parametrize("k", [65, 100, 127])
+def test_raw_search_beyond_64(vf, nq, k):
+    """VS_RAW_ORDER inner-product searches of up to 2 * VS_MAX_K entries (a
+    shard's half of a sharded k > 32 search): the lexicographic (key, label)
+    order, both pages, against the fp64 oracle; integer rows (exact scores)."""
+    xb = _rand(900, 4, 81, "int")
+    xq = _rand(nq, 4, 82, "int")
+    index = vf.IndexFlat(4, IP)
+    index.add(xb)
+    D, I = index.search(xq, k, raw=True)
+    Dr, Ir = flat.knn_lex(xb, xq, k, IP)
+    np.testing.assert_array_equal(I, Ir)
+    np.testing.assert_array_equal(D, Dr)
 
 
 @pytest.mark.parametrize("metric", [L2, IP])

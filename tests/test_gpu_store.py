@@ -232,3 +232,40 @@ def test_reference_store_migration_on_gpu(tmp_path, golden):
     for qi, kw in enumerate(inputs["keywords"][:8]):
         got = [pos[doc.metadata["book_id"]] for doc in store.similarity_search(kw, k=5)]
         assert got == exp["books_l2_I"][341 + qi, :5].tolist()
+
+
+def test_reference_store_migration_without_reembedding_on_gpu(tmp_path, golden):
+    """A faiss-written flat file (the reference's index.faiss, written here from
+    the golden book embeddings with faiss's IxF2 layout) plus a pickle that is
+    never read migrates to the HIP index with no embed_documents call, and the
+    reopened store returns the golden search order."""
+    from helpers import OracleIndex
+    from vsearch import faiss as vfaiss
+    from vsearch import langchain as vlc
+    from vsearch.synth import SynthEmbeddings
+
+    inputs, exp = golden
+    emb = SynthEmbeddings()
+
+    class NoEmbed:
+        def embed_documents(self, t):
+            raise AssertionError("the migration must not re-embed the catalogue")
+
+        def embed_query(self, t):
+            return emb.embed_query(t)
+
+    d = tmp_path / "vector_store"
+    d.mkdir()
+    ref = OracleIndex(emb.dim, 1)
+    ref.add(np.asarray(emb.embed_documents(inputs["book_texts"]), dtype=np.float32))
+    vfaiss.write_index(ref, str(d / "index.faiss"))
+    (d / "index.pkl").write_bytes(b"\x80\x04cos\nsystem\n.")
+    with pytest.raises(vlc.ReferenceStoreError):
+        vlc.FAISS.load_local(str(d), NoEmbed(), allow_dangerous_deserialization=True)
+    vlc.migrate_reference_store(str(d), inputs["book_texts"], inputs["book_metadata"], NoEmbed())
+    store = vlc.FAISS.load_local(str(d), NoEmbed(), allow_dangerous_deserialization=True)
+    assert isinstance(store.index, vfaiss.IndexFlat) and store.index.ntotal == 341
+    pos = {m["book_id"]: i for i, m in enumerate(inputs["book_metadata"])}
+    for qi, kw in enumerate(inputs["keywords"][:8]):
+        got = [pos[doc.metadata["book_id"]] for doc in store.similarity_search(kw, k=5)]
+        assert got == exp["books_l2_I"][341 + qi, :5].tolist()

@@ -174,6 +174,61 @@ def test_reference_written_store_migrates_by_full_rebuild(tmp_path, patched_inde
         assert a == b
 
 
+def test_reference_store_migrates_without_reembedding(tmp_path, patched_indexes, golden):
+    """A reference-written directory (index.faiss + pickled index.pkl) migrates
+    with the vectors of index.faiss kept and the docstore rebuilt from the
+    catalogue rows in label order: no embed_documents call (beyond the optional
+    sample check), the pickle never read, and the reopened store searches like
+    the one the reference built."""
+    inputs, _ = golden
+    emb = SynthEmbeddings(32)
+    texts, metas = inputs["book_texts"][:40], inputs["book_metadata"][:40]
+    ref_dir = tmp_path / "vector_store"
+    ref_dir.mkdir()
+    idx = OracleIndex(32, flat.METRIC_L2)
+    idx.add(np.asarray(emb.embed_documents(texts), dtype=np.float32))
+    vfaiss.write_index(idx, str(ref_dir / "index.faiss"))
+    poison = b"\x80\x04cos\nsystem\n."  # a pickle that must never be loaded
+    (ref_dir / "index.pkl").write_bytes(poison)
+
+    class Counting:
+        def __init__(self):
+            self.calls = 0
+
+        def embed_documents(self, t):
+            self.calls += len(t)
+            return emb.embed_documents(t)
+
+        def embed_query(self, t):
+            return emb.embed_query(t)
+
+    counting = Counting()
+    factory = lambda d, m: OracleIndex(d, m)  # noqa: E731
+    with pytest.raises(ValueError):  # a row count that is not the store's
+        vlc.migrate_reference_store(str(ref_dir), texts[:39], metas[:39], counting,
+                                    index_factory=factory)
+    with pytest.raises(ValueError):  # rows out of label order fail the sample check
+        vlc.migrate_reference_store(str(ref_dir), texts[::-1], metas[::-1], counting,
+                                    verify_sample=3, index_factory=factory)
+    counting.calls = 0
+    mig = vlc.migrate_reference_store(str(ref_dir), texts, metas, counting, verify_sample=4,
+                                      index_factory=factory)
+    assert counting.calls == 4  # the sample only: the catalogue is not re-embedded
+    assert (ref_dir / "index.pkl").read_bytes() == poison
+    loaded = vlc.FAISS.load_local(str(ref_dir), counting, allow_dangerous_deserialization=True,
+                                  index_factory=factory)
+    assert loaded.index.ntotal == 40
+    np.testing.assert_array_equal(loaded.index.reconstruct_n(0, 40), idx.reconstruct_n(0, 40))
+    assert loaded.index_to_docstore_id == mig.index_to_docstore_id
+    assert [loaded.docstore.search(loaded.index_to_docstore_id[i]).metadata["book_id"]
+            for i in range(40)] == [m["book_id"] for m in metas]
+    ref = vlc.FAISS.from_texts(texts, emb, metadatas=metas)
+    for kw in inputs["keywords"][:5]:
+        a = [d.metadata["book_id"] for d in ref.similarity_search(kw, k=5)]
+        b = [d.metadata["book_id"] for d in loaded.similarity_search(kw, k=5)]
+        assert a == b
+
+
 def test_faiss_flat_file_layout(tmp_path):
     idx = OracleIndex(3, flat.METRIC_INNER_PRODUCT)
     x = np.arange(12, dtype=np.float32).reshape(4, 3)

@@ -76,7 +76,7 @@ def test_sharded_merge_equals_single_index_on_ties(metric, world):
         d = int(rng.integers(1, 3))
         x = rng.integers(-2, 3, size=(n, d)).astype(np.float32)
         xq = rng.integers(-2, 3, size=(5, d)).astype(np.float32)
-        for k in (1, 3, 4, 7, 12, 33):
+        for k in (1, 3, 4, 7, 12, 33, 50, 64):
             Dr, Ir = flat.knn_exact(x, xq, k, metric)
             D, I = _simulate_sharded(x, xq, k, metric, world)
             assert np.array_equal(I, Ir), (trial, n, d, k, I, Ir)
