@@ -1804,6 +1804,12 @@ int vs_filter_second_stats(int64_t* second) {
   return VS_OK;
 }
 
+int vs_x1_stamps(unsigned long long* out, int reset) {
+  if (!out) return fail(VS_E_INVALID, "vs_x1_stamps: null buffer");
+  VS_HIP(x1_stamps(out, reset), "vs_x1_stamps");
+  return VS_OK;
+}
+
 int vs_timer_enable(int on) {
   std::lock_guard<std::mutex> g(g_timer_mu);
   g_timer_on = on != 0;

@@ -83,9 +83,28 @@
 
 namespace vs {
 
+// Diagnostic builds only (VS_X1_STAMP=1, tools/build_variant.sh): per-segment
+// s_memtime sums of the segmented schedule, [group (waves 0-3 | 4-7)][segment]
+// (segments: load issue, vmcnt wait, barrier 1, matrix issue, barrier 2,
+// epilogue), added once per wave at the end; read by vs_x1_stamps.  The real
+// kernel has no stamp.
+#ifndef VS_X1_STAMP
+#define VS_X1_STAMP 0
+#endif
+constexpr int kStampSeg = 6;
+__device__ unsigned long long g_x1_stamps[2 * kStampSeg + 2];
+
 namespace {
 
-constexpr int kT = 256;               // rows (and queries) per tile
+constexpr int kT = 256;
+
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}               // rows (and queries) per tile
 constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
@@ -596,6 +615,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const bool lag = VS_X1_STAGGER && w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
     int buf = 0, t = t0, ks = 0;
+#if VS_X1_STAMP
+    unsigned long long sg[kStampSeg] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tA = stamp_now(), tB;
+#define VS_X1_MARK(i) (tB = stamp_now(), sg[i] += tB - tA, tA = tB)
+#else
+#define VS_X1_MARK(i) ((void)0)
+#endif
     for (int s = 0; s < nsteps; ++s) {
       __builtin_amdgcn_sched_barrier(0);
       rd(buf, 0, fa0, fb0);
@@ -605,10 +631,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int i = 0; i < 4; ++i) stage_piece(i);
       advance_cursor();
       __builtin_amdgcn_sched_barrier(0);
+      VS_X1_MARK(0);
       // this wave's pieces of step s+1 (the younger steps s+2, s+3 stay in flight)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      VS_X1_MARK(1);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      VS_X1_MARK(2);
       if (ks == 0) {  // uniform: a tile's first step starts its accumulators
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, fb0);
@@ -619,8 +648,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
+      VS_X1_MARK(3);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      VS_X1_MARK(4);
       if (++ks == nksteps) {  // beside the partner's matrix segment
         ks = 0;
 #if !VS_X1_P_NOEPI
@@ -633,9 +664,19 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #endif
         ++t;
       }
+      VS_X1_MARK(5);
       buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
     if (!lag && VS_X1_STAGGER) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
+#if VS_X1_STAMP
+    if (lane == 0) {  // vector atomics (lane 0), one per segment
+      const int grp = w >= 4 ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < kStampSeg; ++i) atomicAdd(&g_x1_stamps[grp * kStampSeg + i], sg[i]);
+      atomicAdd(&g_x1_stamps[2 * kStampSeg + grp], (unsigned long long)nsteps);
+    }
+#endif
+#undef VS_X1_MARK
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
   }
@@ -701,6 +742,15 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
 }
 
 int x1_lane_len() { return 8; }
+
+hipError_t x1_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_stamps), sizeof(g_x1_stamps));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[2 * kStampSeg + 2] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_x1_stamps), z, sizeof(z));
+  }
+  return e;
+}
 
 template <int EL>
 static hipError_t x1_dispatch(int mode, const X1Args& a, Partials part, hipStream_t st,

@@ -75,6 +75,7 @@ SIGNATURES = {
     "vs_timer_read": (_c_int, [ctypes.POINTER(ctypes.c_double), _i64p]),
     "vs_timer_kernel": (ctypes.c_char_p, []),
     "vs_timer_read_kernel": (_c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i64p]),
+    "vs_x1_stamps": (_c_int, [ctypes.POINTER(ctypes.c_ulonglong), _c_int]),
     "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
     "vs_filter_wide_stats": (_c_int, [_i64p]),
     "vs_filter_second_stats": (_c_int, [_i64p]),

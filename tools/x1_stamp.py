@@ -1,0 +1,36 @@
+"""Diagnostic: where a step of the filter pass spends its cycles (segmented
+schedule).  Run with VSEARCH_LIB pointing at a VS_X1_STAMP=1 build
+(tools/build_variant.sh stamp -DVS_X1_STAMP=1): one 2.56M x 1536 IP index,
+batch-4096 top-10 searches, then the per-segment s_memtime sums (shares only:
+the stamps' own waits change the lengths)."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "book-recommendation-engine_amd"))
+
+from vsearch import _lib  # noqa: E402
+from vsearch import faiss as vf  # noqa: E402
+from vsearch.synth import synthetic_rows  # noqa: E402
+
+n = int(os.environ.get("PROBE_N", "2560000"))
+index = vf.IndexFlatIP(1536)
+index.reserve(n)
+index.add_synthetic(n, seed=1234)
+xq = synthetic_rows(50_000_000, 4096, 1536, 5678)
+index.search(xq, 10)
+lib = _lib.load()
+buf = (ctypes.c_ulonglong * 14)()
+lib.vs_x1_stamps(buf, 1)
+for _ in range(3):
+    index.search(xq, 10)
+lib.vs_x1_stamps(buf, 1)
+names = ["load issue", "vmcnt wait", "barrier 1", "matrix issue", "barrier 2", "epilogue"]
+for g, label in enumerate(("waves 0-3", "waves 4-7")):
+    segs = [buf[g * 6 + i] for i in range(6)]
+    steps = max(1, buf[12 + g])
+    tot = sum(segs)
+    print(f"{label}: {steps} wave-steps, {tot / steps:.0f} cycles/step")
+    for nm, v in zip(names, segs):
+        print(f"   {nm:12s} {v / steps:8.1f} cycles/step  {100.0 * v / max(1, tot):5.1f} %")
