@@ -53,9 +53,12 @@
 #define VS_X1_STAGGER 1
 #endif
 // Step schedule: 1 = fragment reads half a step ahead, DMA pieces between the
-// MFMAs of each wave (round 2); 2 = separate load and matrix segments (below).
+// MFMAs of each wave (round 2); 2 = separate load and matrix segments (below);
+// 0 = per plane: int8 1, bf16 2 (the faster of the two on each, C3 uniform
+// int8 68.6k vs 65.9k queries/s, clustered bf16 34.4k vs 32.5k:
+// profiles/r03_ab_sched.txt).
 #ifndef VS_X1_SCHED
-#define VS_X1_SCHED 2
+#define VS_X1_SCHED 0
 #endif
 // Diagnostic builds only (tools/x1_probe.sh; wrong results by design): drop the
 // LDS-DMA, the fragment reads, the mid-step barrier or the epilogue.
@@ -91,8 +94,10 @@ namespace vs {
 #ifndef VS_X1_STAMP
 #define VS_X1_STAMP 0
 #endif
-constexpr int kStampSeg = 6;
-__device__ unsigned long long g_x1_stamps[2 * kStampSeg + 2];
+constexpr int kStampSeg = 9;  // + inside the epilogue: reject, factor loads, keys/inserts
+constexpr int kStampCnt = 3;  // epilogue counts: factor loads, blocks inserting, inserts
+constexpr int kStampN = 2 * (kStampSeg + kStampCnt) + 2;
+__device__ unsigned long long g_x1_stamps[kStampN];
 
 namespace {
 
@@ -148,6 +153,33 @@ __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_
 // check's floor T toward the top and failing its bound.
 __device__ __forceinline__ int tile_perm(int t) {
   return (int)(((uint32_t)t * 2654435761u) >> 24) & 0xFC;
+}
+
+__device__ __forceinline__ int sel16i(const i32x16& v, int i) {
+  int r = v[0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) r = i == j ? v[j] : r;
+  return r;
+}
+
+__device__ __forceinline__ float sel4x4(const f32x4 (&v)[4], int i) {
+  float r = v[0][0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) r = i == j ? v[j >> 2][j & 3] : r;
+  return r;
+}
+
+// int8 candidate threshold: an integer T with fl(fl(float(a)) * c) <= lim for
+// every int32 a <= T (c > 0; the scaled score is monotone in a), from an
+// approximate quotient minus a margin, then checked: INT_MIN (every row a
+// candidate) when the check fails.  A smaller T only admits more candidates.
+__device__ __forceinline__ int i8_threshold(float lim, float c) {
+  const float q = lim * __builtin_amdgcn_rcpf(c);
+  const float qm = q > 0.0f ? q * (1.0f - 0x1p-20f) : q * (1.0f + 0x1p-20f);
+  float fl = floorf(qm) - 2.0f;
+  fl = fminf(fmaxf(fl, -2147483520.0f), 2147483520.0f);  // in int range (NaN -> lower bound)
+  const int T = (int)fl;
+  return (float)T * c <= lim ? T : INT_MIN;
 }
 
 __device__ __forceinline__ float sel16(const f32x16& v, int i) {
@@ -360,6 +392,16 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
       lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
     };
+#if VS_X1_STAMP
+    unsigned long long ecnt[kStampCnt] = {0, 0, 0};
+    unsigned long long sg[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tA = 0, tB = 0, eA = 0, eB = 0;
+#define VS_X1_COUNT(i, v) (ecnt[i] += (v))
+#define VS_X1_EMARK(i) (eB = stamp_now(), sg[i] += eB - eA, eA = eB)
+#else
+#define VS_X1_COUNT(i, v) ((void)0)
+#define VS_X1_EMARK(i) ((void)0)
+#endif
     auto epilogue = [&](int t) {
       // uniform: every row of the tile exists and none is excluded
       const bool plain = self0 < 0 && !qrow && (t + 1) * kT <= ntotal;
@@ -368,136 +410,193 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // slot's fields are disjoint bits, so the XOR splits into a uniform part
       // (wr, rb, jj) and one lane part (h), and f leaves the low two bits (e)
       const int fh = (4 * h) ^ (f & 0x04);
+      auto rowof = [&](int rb, int jj) {
+        return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh;
+      };
+      // Phase 1: the candidate rows of every (rb, qb) block, a 16-bit mask per
+      // lane, against each list's last entry before any insertion of this
+      // tile (the last entry only tightens, so the masks are a superset).
+      //  * int8: a row's score fl(fl(float(sum)) * fl(f_q * f_x)) is monotone
+      //    in the sum and in f_x (factors >= 0), so with the lane's largest
+      //    factor over its 16 rows (xgmax: the maximum per 32-row group and
+      //    bit 2 of the row, a SCALAR load) a row can beat the list only if
+      //    its int32 sum exceeds one integer threshold per block (i8_threshold):
+      //    16 integer compares, no conversion;
+      //  * bf16 inner product: the key is -sum, exactly: 16 float compares;
+      //  * bf16 L2 / cosine: every row (the key needs the row's norm).
+      uint32_t cmk[4];  // [rb]: bits 0-15 qb 0, 16-31 qb 1
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
-        auto rowof = [&](int jj) {
-          return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh;
-        };
-        // int8: xs holds s_x (IP) or s_x / |x| (COS), qsc s_q or s_q / |q|
-        f32x4 xa[4], xsv[4];
-        // The per-row values of the lane's 16 rows: four 16-B loads in ONE asm
-        // statement that also retires them (vmcnt(0): it drains the LDS-DMA
-        // pieces in flight too).  Loads the compiler sees would get a vmcnt
-        // counted without the DMA pieces, and its waits leak into the loop (a
-        // drain at the top of every step); here the drain happens only on this
-        // path: int8 blocks that pass the fast reject below (rare after the
-        // first tiles), bf16 L2 / cosine tiles.
-        const int gbase = t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0));  // uniform
-        auto load_rows = [&](const float* src, f32x4 (&o)[4]) {
-          const float* p0 = src + rowof(0);
-          const float* p1 = src + rowof(1);
-          const float* p2 = src + rowof(2);
-          const float* p3 = src + rowof(3);
-          asm volatile(
-              "global_load_dwordx4 %0, %4, off\n\t"
-              "global_load_dwordx4 %1, %5, off\n\t"
-              "global_load_dwordx4 %2, %6, off\n\t"
-              "global_load_dwordx4 %3, %7, off\n\t"
-              "s_waitcnt vmcnt(0)"
-              : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
-              : "v"(p0), "v"(p1), "v"(p2), "v"(p3)
-              : "memory");
-        };
-        auto load_aux = [&]() {
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            xa[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-            xsv[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-          if constexpr ((MODE == MODE_L2 || MODE == MODE_COS) && EL != FILTER_I8) load_rows(xaux, xa);
-          if constexpr (EL == FILTER_I8) load_rows(xs, xsv);
-        };
-        // int8: a block's scores are fl(fl(float(sum)) * fl(f_q * f_x)), monotone
-        // in the sum and in f_x (both factors >= 0), so the lane's largest
-        // factor over its 16 rows and the largest sum bound every score of the
-        // block from above: when that bound cannot beat the list, the block is
-        // skipped without converting its 16 sums.  The lane's 16 rows are the
-        // rows of its 32-row group whose bit 2 is fh >> 2, and xgmax holds that
-        // maximum per (group, bit): two SCALAR loads per block (the vector
-        // loads of the 16 factors, which the compiler retires with a vmcnt
-        // that also drains the LDS-DMA pieces in flight, happen only for
-        // blocks that pass)
         float fmax = 0.0f;
-        bool loaded = false;
         if constexpr (EL == FILTER_I8) {
-          const int grp = gbase >> 5;  // uniform
+          const int grp = (t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0))) >> 5;  // uniform
           const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
           fmax = (fh & 4) ? g1 : g0;
-        } else {
-          load_aux();
-          loaded = true;
         }
+        uint32_t m2 = 0;
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
-          if constexpr (EL == FILTER_I8) {
-            int amax = acc[rb][qb][0];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
-            const float upper = amax > 0 ? (float)amax * (qsc[qb] * fmax) : 0.0f;
-            if (!(upper > -lk[qb][KR - 1])) continue;  // key = -score < last needs score > -last
-            if (!loaded) {
-              load_aux();
-              loaded = true;
-            }
-          }
-          f32x16 key;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              // int8: the exact int32 sum times the two factors (three fp32
-              // roundings, five with the cosine's folded inverse norms)
-              float v;
-              if constexpr (EL == FILTER_I8)
-                v = (float)acc[rb][qb][jj * 4 + e] * (qsc[qb] * xsv[jj][e]);
-              else
-                v = acc[rb][qb][jj * 4 + e];
-              float kk;
-              if constexpr (MODE == MODE_IP || EL == FILTER_I8) {
-                kk = -v;
-              } else if constexpr (MODE == MODE_L2) {
-                kk = l2_from_ip(qa[qb], xa[jj][e], v);
-              } else {
-                kk = -(v * (qa[qb] * xa[jj][e]));
-              }
-              key[jj * 4 + e] = kk;
-            }
-          }
-          // Admission against the list's last entry is key < last key (a row
-          // tied with it is left out even when its label is lower: the lists
-          // are candidate pools, and the verification only needs every row
-          // outside them to have an approximate key >= its list's final last
-          // entry, which this keeps); list_insert orders the admitted rows
-          // lexicographically.
-          float m = key[0];
-#pragma unroll
-          for (int r = 1; r < 16; ++r) m = fminf(m, key[r]);
           const float last = lk[qb][KR - 1];
-          if (m < last) {  // rare after the first tiles
-            uint32_t cm = 0;
-            if (plain) {
+          uint32_t cm = 0;
+          if constexpr (EL == FILTER_I8) {
+            const float c = qsc[qb] * fmax;
+            if (c > 0.0f && -last >= 0.0f) {
+              // a row with sum <= 0 scores <= 0 <= -last; a positive sum scores
+              // at most fl(fl(sum) * c) (the factor monotonicity holds for
+              // positive sums only), which i8_threshold bounds
+              const int T = i8_threshold(-last, c);
+#pragma unroll
+              for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > T) << r;
+            } else if (c > 0.0f) {  // the list admits negative scores: every row
+              cm = 0xFFFFu;
+            } else {  // every score is 0 (a zero query or zero rows): key -0
+              cm = (-0.0f < last) ? 0xFFFFu : 0u;
+            }
+          } else if constexpr (MODE == MODE_IP) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cm |= (uint32_t)(-acc[rb][qb][r] < last) << r;
+          } else {
+            cm = 0xFFFFu;
+          }
+          m2 |= cm << (16 * qb);
+        }
+        cmk[rb] = m2;
+      }
+      VS_X1_EMARK(6);
+      // Phases 2 and 3 per half tile (rb pair): the per-row values (int8
+      // factors; bf16 L2 / cosine norms) of the lane's 32 rows, when any lane of
+      // the wave has a candidate in the pair — eight 16-B loads in ONE asm
+      // statement that also retires them (vmcnt(0), which drains the LDS-DMA
+      // pieces in flight too: twice per tile at most; loads the compiler sees
+      // would get a vmcnt counted without the DMA pieces, and its waits would
+      // leak into the loop) — then the exact keys of the candidates, admitted
+      // with key < the list's last entry (a row tied with it is left out even
+      // when its label is lower: the lists are candidate pools, and the
+      // verification only needs every row outside them to have an approximate
+      // key >= its list's final last entry, which this keeps); list_insert
+      // orders the admitted rows lexicographically.  The fragment registers
+      // are dead here (reloaded by the next load segment).
+      constexpr bool kRows = EL == FILTER_I8 || MODE == MODE_L2 || MODE == MODE_COS;
+      // row blocks per load group: 2 under the segmented schedule; 1 under the
+      // round-2 schedule, whose next-step fragments stay live across the
+      // epilogue (registers)
+      constexpr int G = (VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2)) == 2 ? 2 : 1;
+#pragma unroll
+      for (int hp = 0; hp < 4 / G; ++hp) {
+        f32x4 rv[G][4];
+#pragma unroll
+        for (int r2 = 0; r2 < G; ++r2)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) rv[r2][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint32_t any = 0;
+#pragma unroll
+        for (int r2 = 0; r2 < G; ++r2) any |= cmk[G * hp + r2];
+        if (__ballot(any != 0) == 0) continue;  // uniform
+        if constexpr (kRows) {
+          const float* src = EL == FILTER_I8 ? xs : xaux;
+          if constexpr (G == 2) {
+            const float* a[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = src + rowof(2 * hp + (q >> 2), q & 3);
+            asm volatile(
+                "global_load_dwordx4 %0, %8, off\n\tglobal_load_dwordx4 %1, %9, off\n\t"
+                "global_load_dwordx4 %2, %10, off\n\tglobal_load_dwordx4 %3, %11, off\n\t"
+                "global_load_dwordx4 %4, %12, off\n\tglobal_load_dwordx4 %5, %13, off\n\t"
+                "global_load_dwordx4 %6, %14, off\n\tglobal_load_dwordx4 %7, %15, off\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&v"(rv[0][0]), "=&v"(rv[0][1]), "=&v"(rv[0][2]), "=&v"(rv[0][3]),
+                  "=&v"(rv[G - 1][0]), "=&v"(rv[G - 1][1]), "=&v"(rv[G - 1][2]), "=&v"(rv[G - 1][3])
+                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]),
+                  "v"(a[7])
+                : "memory");
+          } else {
+            const float* a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = src + rowof(hp, q);
+            asm volatile(
+                "global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %5, off\n\t"
+                "global_load_dwordx4 %2, %6, off\n\tglobal_load_dwordx4 %3, %7, off\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&v"(rv[0][0]), "=&v"(rv[0][1]), "=&v"(rv[0][2]), "=&v"(rv[0][3])
+                : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+                : "memory");
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#if VS_X1_STAMP
+          if ((int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
+            VS_X1_COUNT(0, 1);
+#endif
+        }
+#pragma unroll
+        for (int r2 = 0; r2 < G; ++r2) {
+          const int rb = G * hp + r2;
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+            uint32_t cm = (cmk[rb] >> (16 * qb)) & 0xFFFFu;
+            if constexpr ((MODE == MODE_L2 || MODE == MODE_COS) && EL != FILTER_I8) {
+              // every row is a candidate: keys first, admission mask from them
+              f32x16 key;
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float v = acc[rb][qb][jj * 4 + e];
+                  key[jj * 4 + e] = MODE == MODE_L2 ? l2_from_ip(qa[qb], rv[r2][jj][e], v)
+                                                    : -(v * (qa[qb] * rv[r2][jj][e]));
+                }
+              const float last = lk[qb][KR - 1];
+              cm = 0;
 #pragma unroll
               for (int r = 0; r < 16; ++r) cm |= (uint32_t)(key[r] < last) << r;
-            } else {
+              if (!plain) {
 #pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                const int row = rowof(r >> 2) + (r & 3);
-                cm |= (uint32_t)(row < ntotal && row != selfrow[qb] && key[r] < last) << r;
+                for (int r = 0; r < 16; ++r) {
+                  const int row = rowof(rb, r >> 2) + (r & 3);
+                  if (!(row < ntotal && row != selfrow[qb])) cm &= ~(1u << r);
+                }
               }
-            }
-            while (cm) {
-              const int bi = __builtin_ctz(cm);
-              cm &= cm - 1;
-              const int row = rowof(bi >> 2) + (bi & 3);
-              list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+              if (cm) VS_X1_COUNT(1, 1);
+              VS_X1_COUNT(2, __builtin_popcount(cm));
+              while (cm) {
+                const int bi = __builtin_ctz(cm);
+                cm &= cm - 1;
+                const int row = rowof(rb, bi >> 2) + (bi & 3);
+                list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+              }
+            } else {
+              // candidates one at a time: the exact key of the row, then admission
+              int nins = 0;
+              while (cm) {
+                const int bi = __builtin_ctz(cm);
+                cm &= cm - 1;
+                const int row = rowof(rb, bi >> 2) + (bi & 3);
+                float key;
+                if constexpr (EL == FILTER_I8) {
+                  // the exact int32 sum times the two factors (three fp32
+                  // roundings, five with the cosine's folded inverse norms); xs
+                  // holds s_x (IP) or s_x / |x| (COS), qsc s_q or s_q / |q|
+                  key = -((float)sel16i(acc[rb][qb], bi) * (qsc[qb] * sel4x4(rv[r2], bi)));
+                } else {
+                  key = -sel16(acc[rb][qb], bi);
+                }
+                const bool ok = (plain || (row < ntotal && row != selfrow[qb])) && key < lk[qb][KR - 1];
+                if (ok) {
+                  list_insert<KR, int>(lk[qb], li[qb], key, row);
+                  ++nins;
+                }
+              }
+              if (nins) VS_X1_COUNT(1, 1);
+              VS_X1_COUNT(2, nins);
             }
           }
         }
+        VS_X1_EMARK(8);
       }
     };
 
     if ((VS_X1_PRIO == 1 && w >= 4) || (VS_X1_PRIO == 2 && w < 4)) __builtin_amdgcn_s_setprio(1);
-#if VS_X1_SCHED == 1
+    constexpr int kSched = VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2);
+    if constexpr (kSched == 1) {
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
 #pragma unroll
@@ -589,7 +688,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
       buf = nbuf;
     }
-#else
+    } else {
     // Segmented schedule: every step of a wave is a LOAD segment (the step's 12
     // fragment reads, the 4 LDS-DMA pieces of step s+3, the wait for this
     // wave's pieces of step s+1) and a MATRIX segment (the step's 16 MFMAs),
@@ -616,8 +715,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
     int buf = 0, t = t0, ks = 0;
 #if VS_X1_STAMP
-    unsigned long long sg[kStampSeg] = {0, 0, 0, 0, 0, 0};
-    unsigned long long tA = stamp_now(), tB;
+    tA = stamp_now();
 #define VS_X1_MARK(i) (tB = stamp_now(), sg[i] += tB - tA, tA = tB)
 #else
 #define VS_X1_MARK(i) ((void)0)
@@ -669,15 +767,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     }
     if (!lag && VS_X1_STAGGER) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
 #if VS_X1_STAMP
-    if (lane == 0) {  // vector atomics (lane 0), one per segment
+    {  // vector atomics; the counts are summed over the lanes
       const int grp = w >= 4 ? 1 : 0;
+      if (lane == 0) {
 #pragma unroll
-      for (int i = 0; i < kStampSeg; ++i) atomicAdd(&g_x1_stamps[grp * kStampSeg + i], sg[i]);
-      atomicAdd(&g_x1_stamps[2 * kStampSeg + grp], (unsigned long long)nsteps);
+        for (int i = 0; i < kStampSeg; ++i)
+          atomicAdd(&g_x1_stamps[grp * (kStampSeg + kStampCnt) + i], sg[i]);
+        atomicAdd(&g_x1_stamps[2 * (kStampSeg + kStampCnt) + grp], (unsigned long long)nsteps);
+      }
+#pragma unroll
+      for (int i = 0; i < kStampCnt; ++i)
+        atomicAdd(&g_x1_stamps[grp * (kStampSeg + kStampCnt) + kStampSeg + i], ecnt[i]);
     }
 #endif
 #undef VS_X1_MARK
-#endif
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
   }
 
@@ -746,7 +850,7 @@ int x1_lane_len() { return 8; }
 hipError_t x1_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_stamps), sizeof(g_x1_stamps));
   if (e == hipSuccess && reset) {
-    unsigned long long z[2 * kStampSeg + 2] = {};
+    unsigned long long z[kStampN] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_x1_stamps), z, sizeof(z));
   }
   return e;

@@ -123,8 +123,9 @@ constexpr int64_t kI8MaxLd = 131072;
 int x1_list_len(int need);
 // Entries per lane list of the filter pass (8).
 int x1_lane_len();
-// Diagnostic: the per-segment cycle sums of a VS_X1_STAMP build (14 values:
-// [2 groups][6 segments] + steps per group); zeros in a real build.
+// Diagnostic: the per-segment cycle sums of a VS_X1_STAMP build (26 values:
+// [2 groups][9 segments + 3 epilogue counts] + steps per group); zeros in a
+// real build.
 hipError_t x1_stamps(unsigned long long* out, int reset);
 // Writes 4*nsplit lists of part.KP entries per query (nq_pad queries), each holding
 // x1_lane_len() entries and empty padding.  *ndispatch = kernel launches used.

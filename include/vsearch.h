@@ -224,9 +224,11 @@ int vs_filter_second_stats(int64_t* second);
 int vs_filter_wide_sets(int64_t* entries, int64_t* rescored);
 int vs_timer_reset(void);
 /* Diagnostic only (no reference interface): the filter pass's per-segment
- * cycle sums of a stamp build (VS_X1_STAMP=1; zeros otherwise), 14 values:
+ * cycle sums of a stamp build (VS_X1_STAMP=1; zeros otherwise), 26 values:
  * [waves 0-3 | 4-7][load issue, vmcnt wait, barrier 1, matrix issue,
- * barrier 2, epilogue] then the steps of each group; reset != 0 clears them. */
+ * barrier 2, epilogue, epilogue reject, factor loads, keys and inserts;
+ * factor-load paths, inserting blocks, inserts]
+ * then the steps of each group; reset != 0 clears them. */
 int vs_x1_stamps(unsigned long long* out, int reset);
 int vs_timer_read(double* total_ms, int64_t* launches);
 /* The same for the spans of one kernel name only (the filter engine's first

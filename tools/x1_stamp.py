@@ -21,16 +21,22 @@ index.add_synthetic(n, seed=1234)
 xq = synthetic_rows(50_000_000, 4096, 1536, 5678)
 index.search(xq, 10)
 lib = _lib.load()
-buf = (ctypes.c_ulonglong * 14)()
+buf = (ctypes.c_ulonglong * 26)()
 lib.vs_x1_stamps(buf, 1)
 for _ in range(3):
     index.search(xq, 10)
 lib.vs_x1_stamps(buf, 1)
-names = ["load issue", "vmcnt wait", "barrier 1", "matrix issue", "barrier 2", "epilogue"]
+names = ["load issue", "vmcnt wait", "barrier 1", "matrix issue", "barrier 2", "epilogue",
+         " epi reject", " epi loads", " epi keys"]
+tiles_note = "per wave and tile: factor-load paths (wave level), inserting lane-blocks and inserts (summed over lanes)"
 for g, label in enumerate(("waves 0-3", "waves 4-7")):
-    segs = [buf[g * 6 + i] for i in range(6)]
-    steps = max(1, buf[12 + g])
-    tot = sum(segs)
+    segs = [buf[g * 12 + i] for i in range(9)]
+    cnts = [buf[g * 12 + 9 + i] for i in range(3)]
+    steps = max(1, buf[24 + g])
+    tot = sum(segs[:6])
     print(f"{label}: {steps} wave-steps, {tot / steps:.0f} cycles/step")
     for nm, v in zip(names, segs):
         print(f"   {nm:12s} {v / steps:8.1f} cycles/step  {100.0 * v / max(1, tot):5.1f} %")
+    tiles = steps / 24.0
+    print(f"   per tile ({tiles_note}): factor loads {cnts[0] / tiles:.3f}, "
+          f"inserting blocks {cnts[1] / tiles:.3f}, inserts {cnts[2] / tiles:.3f}")
