@@ -393,7 +393,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
     };
 #if VS_X1_STAMP
-    unsigned long long ecnt[kStampCnt] = {0, 0, 0};
+    unsigned long long ecnt[kStampCnt] = {0, 0, 0};  // only [0] (wave level) is kept
     unsigned long long sg[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tA = 0, tB = 0, eA = 0, eB = 0;
 #define VS_X1_COUNT(i, v) (ecnt[i] += (v))
@@ -424,43 +424,43 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       //    16 integer compares, no conversion;
       //  * bf16 inner product: the key is -sum, exactly: 16 float compares;
       //  * bf16 L2 / cosine: every row (the key needs the row's norm).
-      uint32_t cmk[4];  // [rb]: bits 0-15 qb 0, 16-31 qb 1
+      // pass: bit 2 rb + qb set when the block may hold a candidate (phase 1
+      // is per block: a maximum and one compare; the 16-row masks are built
+      // in phase 3 for the blocks that pass only)
+      uint32_t pass = 0;
+      float fmx[4];  // int8: the lane's factor bound per row block
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
-        float fmax = 0.0f;
+        fmx[rb] = 0.0f;
         if constexpr (EL == FILTER_I8) {
           const int grp = (t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0))) >> 5;  // uniform
           const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
-          fmax = (fh & 4) ? g1 : g0;
+          fmx[rb] = (fh & 4) ? g1 : g0;
         }
-        uint32_t m2 = 0;
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
           const float last = lk[qb][KR - 1];
-          uint32_t cm = 0;
+          bool p;
           if constexpr (EL == FILTER_I8) {
-            const float c = qsc[qb] * fmax;
+            const float c = qsc[qb] * fmx[rb];
             if (c > 0.0f && -last >= 0.0f) {
-              // a row with sum <= 0 scores <= 0 <= -last; a positive sum scores
-              // at most fl(fl(sum) * c) (the factor monotonicity holds for
-              // positive sums only), which i8_threshold bounds
-              const int T = i8_threshold(-last, c);
+              int amax = acc[rb][qb][0];
 #pragma unroll
-              for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > T) << r;
-            } else if (c > 0.0f) {  // the list admits negative scores: every row
-              cm = 0xFFFFu;
-            } else {  // every score is 0 (a zero query or zero rows): key -0
-              cm = (-0.0f < last) ? 0xFFFFu : 0u;
+              for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
+              p = amax > i8_threshold(-last, c);
+            } else {
+              p = c > 0.0f || -0.0f < last;
             }
           } else if constexpr (MODE == MODE_IP) {
+            float amax = acc[rb][qb][0];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) cm |= (uint32_t)(-acc[rb][qb][r] < last) << r;
+            for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[rb][qb][r]);
+            p = -amax < last;  // NaN sums never enter
           } else {
-            cm = 0xFFFFu;
+            p = true;
           }
-          m2 |= cm << (16 * qb);
+          pass |= (uint32_t)p << (2 * rb + qb);
         }
-        cmk[rb] = m2;
       }
       VS_X1_EMARK(6);
       // Phases 2 and 3 per half tile (rb pair): the per-row values (int8
@@ -488,9 +488,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         for (int r2 = 0; r2 < G; ++r2)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) rv[r2][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-        uint32_t any = 0;
-#pragma unroll
-        for (int r2 = 0; r2 < G; ++r2) any |= cmk[G * hp + r2];
+        const uint32_t any = (pass >> (2 * G * hp)) & ((1u << (2 * G)) - 1u);
         if (__ballot(any != 0) == 0) continue;  // uniform
         if constexpr (kRows) {
           const float* src = EL == FILTER_I8 ? xs : xaux;
@@ -522,17 +520,15 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 : "memory");
           }
           __builtin_amdgcn_sched_barrier(0);
-#if VS_X1_STAMP
-          if ((int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
-            VS_X1_COUNT(0, 1);
-#endif
+          VS_X1_COUNT(0, 1);  // uniform: a scalar count
         }
 #pragma unroll
         for (int r2 = 0; r2 < G; ++r2) {
           const int rb = G * hp + r2;
 #pragma unroll
           for (int qb = 0; qb < 2; ++qb) {
-            uint32_t cm = (cmk[rb] >> (16 * qb)) & 0xFFFFu;
+            if (!(pass & (1u << (2 * rb + qb)))) continue;
+            uint32_t cm = 0;
             if constexpr ((MODE == MODE_L2 || MODE == MODE_COS) && EL != FILTER_I8) {
               // every row is a candidate: keys first, admission mask from them
               f32x16 key;
@@ -555,8 +551,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   if (!(row < ntotal && row != selfrow[qb])) cm &= ~(1u << r);
                 }
               }
-              if (cm) VS_X1_COUNT(1, 1);
-              VS_X1_COUNT(2, __builtin_popcount(cm));
               while (cm) {
                 const int bi = __builtin_ctz(cm);
                 cm &= cm - 1;
@@ -564,8 +558,19 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
               }
             } else {
-              // candidates one at a time: the exact key of the row, then admission
-              int nins = 0;
+              // the block's candidate rows (int8: sum above the block's integer
+              // threshold; bf16: -sum below the last entry), then one at a time:
+              // the exact key of the row and its admission
+              const float last = lk[qb][KR - 1];
+              if constexpr (EL == FILTER_I8) {
+                const float c = qsc[qb] * fmx[rb];
+                const int T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > T) << r;
+              } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cm |= (uint32_t)(-acc[rb][qb][r] < last) << r;
+              }
               while (cm) {
                 const int bi = __builtin_ctz(cm);
                 cm &= cm - 1;
@@ -580,13 +585,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   key = -sel16(acc[rb][qb], bi);
                 }
                 const bool ok = (plain || (row < ntotal && row != selfrow[qb])) && key < lk[qb][KR - 1];
-                if (ok) {
-                  list_insert<KR, int>(lk[qb], li[qb], key, row);
-                  ++nins;
-                }
+                if (ok) list_insert<KR, int>(lk[qb], li[qb], key, row);
               }
-              if (nins) VS_X1_COUNT(1, 1);
-              VS_X1_COUNT(2, nins);
             }
           }
         }
@@ -622,6 +622,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // image s-1 are consumed before barrier s, after which DMA(s+D) may
     // overwrite it.
     const bool lag = VS_X1_STAGGER && w >= 4;
+#if VS_X1_STAMP
+    tA = stamp_now();
+#define VS_X1_MARK1(i) (tB = stamp_now(), sg[i] += tB - tA, tA = tB)
+#else
+#define VS_X1_MARK1(i) ((void)0)
+#endif
     for (int s = 0; s < nsteps; ++s) {
       const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
       if (lag) {  // uniform
@@ -650,6 +656,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         mfma_rb(3, fa0, fb0);
       }
       __builtin_amdgcn_sched_barrier(0);
+      VS_X1_MARK1(0);
       // retire step s+1 (this wave's pieces); the younger D-2 steps stay in flight
       if (!lag) {  // uniform
 #if !VS_X1_P_NOWAIT
@@ -661,6 +668,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #endif
       }
       __builtin_amdgcn_sched_barrier(0);
+      VS_X1_MARK1(1);
       // second half: next step's sub-step 0 reads first (their latency hides under
       // this half's MFMAs), then sub-step 1's MFMAs with the LDS-DMA of step s+D
       // (into the image of step s-1, which every wave has finished) between them
@@ -674,6 +682,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         __builtin_amdgcn_sched_barrier(0);
       }
       advance_cursor();
+      VS_X1_MARK1(3);
       if (++ks == nksteps) {
         ks = 0;
 #if !VS_X1_P_NOEPI
@@ -686,8 +695,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #endif
         ++t;
       }
+      VS_X1_MARK1(5);
       buf = nbuf;
     }
+#undef VS_X1_MARK1
     } else {
     // Segmented schedule: every step of a wave is a LOAD segment (the step's 12
     // fragment reads, the 4 LDS-DMA pieces of step s+3, the wait for this
@@ -766,6 +777,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
     if (!lag && VS_X1_STAGGER) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
+#undef VS_X1_MARK
+    }
 #if VS_X1_STAMP
     {  // vector atomics; the counts are summed over the lanes
       const int grp = w >= 4 ? 1 : 0;
@@ -775,13 +788,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
           atomicAdd(&g_x1_stamps[grp * (kStampSeg + kStampCnt) + i], sg[i]);
         atomicAdd(&g_x1_stamps[2 * (kStampSeg + kStampCnt) + grp], (unsigned long long)nsteps);
       }
-#pragma unroll
-      for (int i = 0; i < kStampCnt; ++i)
-        atomicAdd(&g_x1_stamps[grp * (kStampSeg + kStampCnt) + kStampSeg + i], ecnt[i]);
+      if (lane == 0)
+        atomicAdd(&g_x1_stamps[grp * (kStampSeg + kStampCnt) + kStampSeg], ecnt[0]);
     }
 #endif
-#undef VS_X1_MARK
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
   }
 
