@@ -515,7 +515,9 @@ def run_knn(args, ctx):
     if is_x1(kname):
         kname, work, kms, nl, split = x1_dominant(ctx, work, kms, nl)
     plane = {"gemm_topk_x1_i8": "i8", "gemm_topk_x1": "bf16"}.get(kname)
-    traffic, tsrc = (pmc_traffic(args.workload, *rocprof_prefix(kname))
+    # clustered data runs the bf16 plane at full size: its own PMC summary
+    pmc_key = args.workload + ("cl" if args.data == "clustered" else "")
+    traffic, tsrc = (pmc_traffic(pmc_key, *rocprof_prefix(kname))
                      if ctx.world == 1 else (None, None))
     if gemv:
         rf = roofline("hbm", n_shard * d * esz * args.steps, kms, nl,

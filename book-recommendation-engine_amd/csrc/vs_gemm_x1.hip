@@ -52,6 +52,13 @@
 #ifndef VS_X1_STAGGER
 #define VS_X1_STAGGER 1
 #endif
+// Round-2 schedule: 1 = the step's 4 LDS-DMA pieces split 2 + 2 over its two
+// halves, NBUF - 2 steps in flight (the first half writes the image of step
+// s-2, whose reads every wave has retired); 0 = all 4 in the second half,
+// NBUF - 1 steps in flight.
+#ifndef VS_X1_DMASPLIT
+#define VS_X1_DMASPLIT 0
+#endif
 // Step schedule: 1 = fragment reads half a step ahead, DMA pieces between the
 // MFMAs of each wave (round 2); 2 = separate load and matrix segments (below);
 // 0 = per plane: int8 1, bf16 2 (the faster of the two on each, C3 uniform
@@ -227,7 +234,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
     int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
-  constexpr int D = NBUF - 1;      // steps in flight
+  // steps in flight (the round-2 schedule with split DMA keeps one fewer)
+  constexpr int D = (VS_X1_DMASPLIT && (VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2)) == 1)
+                        ? NBUF - 2 : NBUF - 1;
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
 
   const int tid = threadIdx.x;
@@ -605,8 +614,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int j = 0; j < 4; ++j) stage_piece(j);
       advance_cursor();
     }
-    if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    // step 0 of the D in flight
+    if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd(0, 0, fa0, fb0);
@@ -630,9 +641,14 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #endif
     for (int s = 0; s < nsteps; ++s) {
       const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+      // this wave's pieces of step s+1: the steps s+2 .. s+D-1 stay in flight
+      // (the lagging waves wait before this step's first pieces, the others
+      // after them)
+      constexpr int kSplit = VS_X1_DMASPLIT ? 2 : 0;  // pieces in the first half
       if (lag) {  // uniform
-        if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -656,12 +672,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         mfma_rb(3, fa0, fb0);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (kSplit) {  // into the image of step s-2 (see above)
+        stage_piece(0);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_piece(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       VS_X1_MARK1(0);
       // retire step s+1 (this wave's pieces); the younger D-2 steps stay in flight
       if (!lag) {  // uniform
 #if !VS_X1_P_NOWAIT
-        if constexpr (NBUF == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (D == 3 && kSplit) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if constexpr (kSplit) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
 #if !VS_X1_P_NOBAR
         __builtin_amdgcn_s_barrier();
@@ -678,7 +703,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int i = 0; i < 4; ++i) {
         mfma_rb(i, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
-        stage_piece(i);
+        if (i >= kSplit) stage_piece(i);  // compile-time
         __builtin_amdgcn_sched_barrier(0);
       }
       advance_cursor();
