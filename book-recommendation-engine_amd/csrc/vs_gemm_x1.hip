@@ -61,6 +61,7 @@
 #endif
 // Step schedule: 1 = fragment reads half a step ahead, DMA pieces between the
 // MFMAs of each wave (round 2); 2 = separate load and matrix segments (below);
+// 3 = the same segments per half step;
 // 0 = per plane: int8 1, bf16 2 (the faster of the two on each, C3 uniform
 // int8 68.6k vs 65.9k queries/s, clustered bf16 34.4k vs 32.5k:
 // profiles/r03_ab_sched.txt).
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // row blocks per load group: 2 under the segmented schedule; 1 under the
       // round-2 schedule, whose next-step fragments stay live across the
       // epilogue (registers)
-      constexpr int G = (VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2)) == 2 ? 2 : 1;
+      constexpr int G = (VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2)) != 1 ? 2 : 1;
 #pragma unroll
       for (int hp = 0; hp < 4 / G; ++hp) {
         f32x4 rv[G][4];
@@ -757,6 +758,44 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #define VS_X1_MARK(i) ((void)0)
 #endif
     for (int s = 0; s < nsteps; ++s) {
+      if constexpr (kSched == 3) {
+      // half-step segments (VS_X1_SCHED=3): sub-step 0 reads + 2 pieces |
+      // its 8 MFMAs | sub-step 1 reads + 2 pieces + the wait for step s+1 |
+      // its 8 MFMAs, four barriers per step (the 8-phase template's finer
+      // interleave); the same images, distances and counted wait as above
+      __builtin_amdgcn_sched_barrier(0);
+      rd(buf, 0, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_piece(0);
+      stage_piece(1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, fb0);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa0, fb0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      rd(buf, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_piece(2);
+      stage_piece(3);
+      advance_cursor();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step s+1
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      } else {
       __builtin_amdgcn_sched_barrier(0);
       rd(buf, 0, fa0, fb0);
       rd(buf, 1, fa1, fb1);
@@ -786,6 +825,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(4);
+      }
       if (++ks == nksteps) {  // beside the partner's matrix segment
         ks = 0;
 #if !VS_X1_P_NOEPI
