@@ -68,6 +68,21 @@
 #ifndef VS_X1_SCHED
 #define VS_X1_SCHED 0
 #endif
+// A/B variant: the int8 fast reject with one factor bound per chunk (the
+// maximum of its tiles' group maxima, loaded once) instead of a scalar load of
+// the tile's group maxima in every epilogue.
+#ifndef VS_X1_XGCHUNK
+#define VS_X1_XGCHUNK 0
+#endif
+// int8 row factors through LDS: the 1 KB of factors of every database tile
+// rides the tile's first LDS-DMA step (8 lanes of each wave, into one of 8
+// side slots), and the epilogue reads them (its factor bounds and exact keys)
+// with ds_reads instead of scalar loads of the group maxima and vector loads
+// that retire with vmcnt(0) — a drain of the DMA ring each time.  The ring
+// drops to 4 images (128 KB + 8 KB of side slots).
+#ifndef VS_X1_SIDE
+#define VS_X1_SIDE 0
+#endif
 // Diagnostic builds only (tools/x1_probe.sh; wrong results by design): drop the
 // LDS-DMA, the fragment reads, the mid-step barrier or the epilogue.
 #ifndef VS_X1_P_NODMA
@@ -110,6 +125,12 @@ __device__ unsigned long long g_x1_stamps[kStampN];
 namespace {
 
 constexpr int kT = 256;
+// the step schedule, the side slots and the ring depth of a plane
+constexpr int x1_sched(int el) { return VS_X1_SCHED ? VS_X1_SCHED : (el == FILTER_I8 ? 1 : 2); }
+constexpr bool x1_side(int el) { return VS_X1_SIDE && el == FILTER_I8 && x1_sched(el) == 1; }
+constexpr int x1_nbuf(int el) { return x1_side(el) ? 4 : VS_X1_NBUF; }
+constexpr int kSideSlots = 8;  // > steps in flight / steps per tile + 1 for every d
+constexpr int kSideSlotB = kT * 4 + 64;  // a tile's factors, then its 16 group maxima
 
 __device__ __forceinline__ unsigned long long stamp_now() {
   unsigned long long t;
@@ -236,9 +257,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
   // steps in flight (the round-2 schedule with split DMA keeps one fewer)
-  constexpr int D = (VS_X1_DMASPLIT && (VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2)) == 1)
-                        ? NBUF - 2 : NBUF - 1;
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
+  constexpr int D = (VS_X1_DMASPLIT && x1_sched(EL) == 1) ? NBUF - 2 : NBUF - 1;
+  constexpr bool kSide = x1_side(EL);
+  constexpr int kSideB = kSide ? kSideSlots * kSideSlotB : 0;
+  static_assert(NBUF * 2 * kStepB + kSideB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB + kSideB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -312,6 +335,19 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 
   if (t1 > t0) {  // uniform over the workgroup
+#if VS_X1_XGCHUNK
+    // A/B variant: one factor bound for the whole chunk (its tiles' group maxima)
+    float xgc = 0.0f;
+    if constexpr (EL == FILTER_I8) {
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      const int n = (t1 - t0) * (kT / 16);
+      const float* g = xgmax + (int64_t)t0 * (kT / 16);
+      for (int i = ln; i < n; i += 64) xgc = fmaxf(xgc, g[i]);
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) xgc = fmaxf(xgc, __shfl_xor(xgc, m));
+      xgc = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, xgc)));
+    }
+#endif
     // Planes are tile-major (vs_internal.h plane_offset): the 64-B step s of
     // the 256 rows of tile t is one contiguous 16-KB block, so a DMA piece (16
     // rows x 64 B) reads 1 KB of consecutive bytes — eight whole 128-B lines,
@@ -381,6 +417,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       const char* qbase = qtile + (int64_t)lk_ * kStepB + (uint32_t)(16 * (i >> 1)) * 64u;
       const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
 #if !VS_X1_P_NODMA
+      if constexpr (kSide) {
+        // the tile's factors with its first step, before the step's pieces (so
+        // every counted wait that retires the step retires them too; a younger
+        // side piece only makes a count wait for one piece more)
+        if (i == 0 && lk_ == 0) {  // uniform
+          const uint32_t sl = lds0 + (uint32_t)(NBUF * 2 * kStepB) +
+                              (uint32_t)((lt & (kSideSlots - 1)) * kSideSlotB);
+          if (lane < 8)
+            glds16(xs + (int64_t)lt * kT + 32 * w, (uint32_t)lane * 16u,
+                   __builtin_amdgcn_readfirstlane(sl + 128u * (uint32_t)w));
+          if (w == 0 && lane < 4)  // uniform w
+            glds16(xgmax + (int64_t)lt * (kT / 16), (uint32_t)lane * 16u,
+                   __builtin_amdgcn_readfirstlane(sl + (uint32_t)(kT * 4)));
+        }
+      }
       if ((i & 1) == 0) {
         if (!(VS_X1_P_NODMA_X))
           glds16(xbase, xlane, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
@@ -423,6 +474,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       auto rowof = [&](int rb, int jj) {
         return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh;
       };
+      // side slots: the factors of the lane's rows (rb, jj, 0..3) of tile t
+      const char* sb = smem + NBUF * 2 * kStepB + (t & (kSideSlots - 1)) * kSideSlotB;
+      auto side_f4 = [&](int rb, int jj) {
+        return *(const f32x4*)(sb + 4 * (((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh));
+      };
       // Phase 1: the candidate rows of every (rb, qb) block, a 16-bit mask per
       // lane, against each list's last entry before any insertion of this
       // tile (the last entry only tightens, so the masks are a superset).
@@ -439,14 +495,34 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // in phase 3 for the blocks that pass only)
       uint32_t pass = 0;
       float fmx[4];  // int8: the lane's factor bound per row block
+#if VS_X1_STAMP
+      if constexpr (EL == FILTER_I8) eA = stamp_now();
+#endif
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         fmx[rb] = 0.0f;
-        if constexpr (EL == FILTER_I8) {
+        if constexpr (kSide) {  // the group maximum of the lane's 16 rows
+          const int g = ((128 * wr + 32 * rb) ^ (f & 0xE0)) >> 5;
+          fmx[rb] = *(const float*)(sb + kT * 4 + 4 * (2 * g + ((fh >> 2) & 1)));
+        } else if constexpr (EL == FILTER_I8) {
+#if VS_X1_XGCHUNK
+          fmx[rb] = xgc;
+#else
           const int grp = (t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0))) >> 5;  // uniform
           const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
           fmx[rb] = (fh & 4) ? g1 : g0;
+#endif
         }
+      }
+#if VS_X1_STAMP
+      if constexpr (EL == FILTER_I8) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) asm volatile("" ::"v"(fmx[rb]));
+        VS_X1_EMARK(7);
+      }
+#endif
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
           const float last = lk[qb][KR - 1];
@@ -490,7 +566,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // row blocks per load group: 2 under the segmented schedule; 1 under the
       // round-2 schedule, whose next-step fragments stay live across the
       // epilogue (registers)
-      constexpr int G = (VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2)) != 1 ? 2 : 1;
+      constexpr int G = x1_sched(EL) != 1 ? 2 : 1;
 #pragma unroll
       for (int hp = 0; hp < 4 / G; ++hp) {
         f32x4 rv[G][4];
@@ -500,7 +576,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
           for (int jj = 0; jj < 4; ++jj) rv[r2][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
         const uint32_t any = (pass >> (2 * G * hp)) & ((1u << (2 * G)) - 1u);
         if (__ballot(any != 0) == 0) continue;  // uniform
-        if constexpr (kRows) {
+        if constexpr (kSide) {
+#pragma unroll
+          for (int r2 = 0; r2 < G; ++r2)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) rv[r2][jj] = side_f4(G * hp + r2, jj);
+        } else if constexpr (kRows) {
           const float* src = EL == FILTER_I8 ? xs : xaux;
           if constexpr (G == 2) {
             const float* a[8];
@@ -605,7 +686,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     };
 
     if ((VS_X1_PRIO == 1 && w >= 4) || (VS_X1_PRIO == 2 && w < 4)) __builtin_amdgcn_s_setprio(1);
-    constexpr int kSched = VS_X1_SCHED ? VS_X1_SCHED : (EL == FILTER_I8 ? 1 : 2);
+    constexpr int kSched = x1_sched(EL);
     if constexpr (kSched == 1) {
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
@@ -909,7 +990,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
-    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, VS_X1_NBUF, EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
+    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, x1_nbuf(EL), EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
                        (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0, a.self0, a.qrow,
                        a.qcount, c, nchunk, part.KP, qg, part.key, part.id, a.xgmax);

@@ -11,7 +11,9 @@ sfx=$1; shift
 src=${X1_SRC:-vs_gemm_x1.hip}
 mkdir -p build_$sfx
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -I. "$@" \
-  -x hip -c "$src" -o build_$sfx/vs_gemm_x1.o
+  -Rpass-analysis=kernel-resource-usage -x hip -c "$src" -o build_$sfx/vs_gemm_x1.o \
+  2> build_$sfx/vs_gemm_x1.remarks
+python3 ../../tools/check_no_spill.py build_$sfx/vs_gemm_x1.remarks gemm_topk_x1 || [ -n "${ALLOW_SPILL:-}" ]  # stamp builds: bf16 kernels spill (diagnose int8 only)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../vsearch/libvsearch_$sfx.so \
   build/vs_api.o build/vs_gemm.o build_$sfx/vs_gemm_x1.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
 echo "built vsearch/libvsearch_$sfx.so"

@@ -27,7 +27,7 @@ for _ in range(3):
     index.search(xq, 10)
 lib.vs_x1_stamps(buf, 1)
 names = ["load issue", "vmcnt wait", "barrier 1", "matrix issue", "barrier 2", "epilogue",
-         " epi reject", " epi loads", " epi keys"]
+         " epi phase 1", " epi bound loads", " epi phases 2-3"]
 tiles_note = "per wave and tile: factor-load paths (wave level), inserting lane-blocks and inserts (summed over lanes)"
 for g, label in enumerate(("waves 0-3", "waves 4-7")):
     segs = [buf[g * 12 + i] for i in range(9)]
