@@ -669,6 +669,15 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
 //     once), whose rows overwrite theirs.
 // The host never waits: counts live in device memory.  `gl` / `gc` (stages
 // after the first): the batch is queries gl[0 .. *gc) of `a`.
+// query cuts in the filter pass (env VS_X1_QCUT=1 turns them on, for A/B)
+static bool qcut_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("VS_X1_QCUT");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
                       int plane, bool last_plane, bool deep = false, const int* gl = nullptr,
                       const int* gc = nullptr) {
@@ -799,6 +808,17 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   x.self0 = self_rows ? a.self0 : -1;
   x.qrow = qrow;
   x.qcount = gc;
+  if (!gathered && x1_qcut_applies(mode, plane) && qcut_enabled()) {
+    // query cuts (vs_gemm_x1.hip "Query cuts"): updated between the pass's
+    // launches, the verification's floor for the rows they drop
+    VS_HIP(scr.alloc((void**)&x.qcut, (size_t)qa_rows * sizeof(float)), "vs: scratch");
+    double* bk = nullptr;
+    VS_HIP(scr.alloc((void**)&bk, (size_t)qa_rows * sizeof(double)), "vs: scratch");
+    VS_HIP(hipMemsetD32Async((hipDeviceptr_t)x.qcut, 0x7f7fffff, (size_t)qa_rows, st), "vs: cuts");
+    VS_HIP(launch_qbound(mode, Q, idx->ld, qaux, plane, stats, qr2, qa_rows, bk, st), "vs: cuts");
+    x.qbkey = bk;
+    x.qcut_m = need;
+  }
   {
     KernelTimer tm(st, gathered ? nullptr : i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1");
     VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &tm.dispatches), "vs: gemm_topk_x1 launch");
@@ -830,7 +850,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const float* xinv = mode == MODE_COS ? a.xaux : nullptr;
   VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
                                Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
-                               st, qinv, xinv, qr2, gc),
+                               st, qinv, xinv, qr2, gc, x.qcut),
          "vs: verify");
   unsigned long long* dst = device_stats(idx->device);
   if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
@@ -841,7 +861,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   if (wide_enabled())
     VS_HIP(launch_verify_wide(mode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
                               idx->norms, Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
-                              vp.KP, flags, st, qinv, xinv, qr2, Dk, Ik, dst + 4),
+                              vp.KP, flags, st, qinv, xinv, qr2, Dk, Ik, dst + 4, x.qcut),
            "vs: verify wide");
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, last_plane ? dst + 2 : dst + 3,
                               nullptr, st),

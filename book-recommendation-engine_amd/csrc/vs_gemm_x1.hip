@@ -129,6 +129,8 @@ constexpr int kT = 256;
 constexpr int x1_sched(int el) { return VS_X1_SCHED ? VS_X1_SCHED : (el == FILTER_I8 ? 1 : 2); }
 constexpr bool x1_side(int el) { return VS_X1_SIDE && el == FILTER_I8 && x1_sched(el) == 1; }
 constexpr int x1_nbuf(int el) { return x1_side(el) ? 4 : VS_X1_NBUF; }
+// the kernels that apply a per-query cut (the others ignore it)
+constexpr bool x1_has_qcut(int mode, int el) { return el == FILTER_I8 || mode == MODE_IP; }
 constexpr int kSideSlots = 8;  // > steps in flight / steps per tile + 1 for every d
 constexpr int kSideSlotB = kT * 4 + 64;  // a tile's factors, then its 16 group maxima
 
@@ -254,7 +256,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
     int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
-    int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax) {
+    int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax,
+    const float* __restrict__ qcut) {
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
   // steps in flight (the round-2 schedule with split DMA keeps one fewer)
   constexpr int D = (VS_X1_DMASPLIT && x1_sched(EL) == 1) ? NBUF - 2 : NBUF - 1;
@@ -298,6 +301,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
 
   int gq[2], selfrow[2];
+  float tq[2];
   float qa[2], qsc[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -308,6 +312,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     qsc[qb] = 0.0f;
     if constexpr (EL == FILTER_I8) qsc[qb] = gq[qb] < nqa ? qs[gq[qb]] : 0.0f;
     selfrow[qb] = qrow ? (gq[qb] < nqa ? qrow[gq[qb]] : -1) : self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
+    // the query's cut (x1_qcut): rows with keys at or above it are dropped
+    // (not on the bf16 L2 / cosine kernels: no register left; x1_has_qcut)
+    tq[qb] = x1_has_qcut(MODE, EL) && qcut && gq[qb] < nqa ? qcut[gq[qb]] : FLT_MAX;
   }
   const int P = nsplit * 4;
   const int pl = sp * 4 + wr * 2 + h;
@@ -332,6 +339,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
     asm volatile("" ::"v"(qa[qb]));
     if constexpr (EL == FILTER_I8) asm volatile("" ::"v"(qsc[qb]));
+    if constexpr (x1_has_qcut(MODE, EL)) asm volatile("" ::"v"(tq[qb]));
   }
 
   if (t1 > t0) {  // uniform over the workgroup
@@ -525,7 +533,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int rb = 0; rb < 4; ++rb) {
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
-          const float last = lk[qb][KR - 1];
+          const float last = fminf(lk[qb][KR - 1], tq[qb]);
           bool p;
           if constexpr (EL == FILTER_I8) {
             const float c = qsc[qb] * fmx[rb];
@@ -631,7 +639,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   key[jj * 4 + e] = MODE == MODE_L2 ? l2_from_ip(qa[qb], rv[r2][jj][e], v)
                                                     : -(v * (qa[qb] * rv[r2][jj][e]));
                 }
-              const float last = lk[qb][KR - 1];
+              const float last = fminf(lk[qb][KR - 1], tq[qb]);
               cm = 0;
 #pragma unroll
               for (int r = 0; r < 16; ++r) cm |= (uint32_t)(key[r] < last) << r;
@@ -652,7 +660,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               // the block's candidate rows (int8: sum above the block's integer
               // threshold; bf16: -sum below the last entry), then one at a time:
               // the exact key of the row and its admission
-              const float last = lk[qb][KR - 1];
+              const float last = fminf(lk[qb][KR - 1], tq[qb]);
               if constexpr (EL == FILTER_I8) {
                 const float c = qsc[qb] * fmx[rb];
                 const int T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
@@ -675,7 +683,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 } else {
                   key = -sel16(acc[rb][qb], bi);
                 }
-                const bool ok = (plain || (row < ntotal && row != selfrow[qb])) && key < lk[qb][KR - 1];
+                const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
+                                key < fminf(lk[qb][KR - 1], tq[qb]);
                 if (ok) list_insert<KR, int>(lk[qb], li[qb], key, row);
               }
             }
@@ -970,6 +979,8 @@ static int x1_qg() {
   return v;
 }
 
+static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
+
 template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
@@ -986,16 +997,24 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // gives it (clustered C3: 202 -> 151 ms per step, profiles/r02za).
   const int qg = a.qcount ? nqt : x1_qg();
   // a gathered later stage (usually empty: its tiles exit at once) is one launch
-  const int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
+  int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
+  const bool cut = a.qcut && x1_has_qcut(MODE, EL) && !a.qcount && a.qbkey && a.qcut_m > 0;
+  // with a cut, at least two launches when the splits are long enough (the
+  // second runs under the cut the first one's lists give)
+  if (cut && nchunk == 1 && per_block >= 16) nchunk = 2;
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
     hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, x1_nbuf(EL), EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
                        (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
                        (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0, a.self0, a.qrow,
-                       a.qcount, c, nchunk, part.KP, qg, part.key, part.id, a.xgmax);
+                       a.qcount, c, nchunk, part.KP, qg, part.key, part.id, a.xgmax, a.qcut);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (cut && c + 1 < nchunk) {
+      e = launch_qcut(a, part, st);
+      if (e != hipSuccess) return e;
+    }
   }
   if (ndispatch) *ndispatch = nchunk;
   return hipSuccess;
@@ -1451,7 +1470,7 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
     const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8,
-    const int* __restrict__ qcount) {
+    const int* __restrict__ qcount, const float* __restrict__ qcut) {
   __shared__ float ek[64];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
@@ -1477,6 +1496,10 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
   }
   for (int o = 32; o > 0; o >>= 1) T = fminf(T, __shfl_xor(T, o));
   bounded = __any(bounded);
+  if (qcut && qcut[q] < FLT_MAX) {  // the pass dropped every row at or above the cut
+    bounded = true;
+    T = fminf(T, qcut[q]);
+  }
 
   const float* qrow = Q + (int64_t)q * ld;
   double qh2, qr2, qn2;
@@ -1538,7 +1561,8 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
                                  const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st, const float* qinv,
-                                 const float* xinv, const float* qr2i8, const int* qcount) {
+                                 const float* xinv, const float* qr2i8, const int* qcount,
+                                 const float* qcut) {
   if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
       L > lists.KP)
     return hipErrorInvalidValue;
@@ -1546,7 +1570,7 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
 #define VS_VERIFY(MD)                                                                             \
   hipLaunchKernelGGL(verify_rescore_kernel<MD>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, X, xn, \
                      Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey, oid,  \
-                     KP, fail, qinv, xinv, qr2i8, qcount)
+                     KP, fail, qinv, xinv, qr2i8, qcount, qcut)
   if (mode == MODE_IP)
     VS_VERIFY(MODE_IP);
   else if (mode == MODE_L2)
@@ -1640,7 +1664,7 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
     const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8,
     const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
-    unsigned long long* __restrict__ sizes) {
+    unsigned long long* __restrict__ sizes, const float* __restrict__ qcut) {
   __shared__ float ck[kWideCap];
   __shared__ int cid[kWideCap];
   __shared__ float rk[64], kk[64];  // the first check's exact keys / the reused ones
@@ -1694,6 +1718,10 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     __syncthreads();
     T = fminf(fminf(wT[0], wT[1]), fminf(wT[2], wT[3]));
     bounded = (wB[0] | wB[1] | wB[2] | wB[3]) != 0;
+    if (qcut && qcut[q] < FLT_MAX) {  // the pass dropped every row at or above the cut
+      bounded = true;
+      T = fminf(T, qcut[q]);
+    }
     const double bkey =
         bound_key(MODE, ba, qs[0], qs[1], MODE == MODE_L2 ? (double)qn[q] : qs[2], stats);
     // Any threshold T' <= T works (every row outside the set still has an
@@ -1816,14 +1844,15 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
                               const float* xinv, const float* qr2i8, const float* Dk,
-                              const int64_t* Ik, unsigned long long* sizes) {
+                              const int64_t* Ik, unsigned long long* sizes,
+                              const float* qcut) {
   if (KF > KP || KP > 64 || (Dk && !Ik) || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
   if (nq_max <= 0) return hipSuccess;
   const int grid = std::min(nq_max, 2048);
 #define VS_WIDE(MD)                                                                               \
   hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(grid), dim3(256), 0, st, qlist, count, KF, M, X, \
                      xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey,   \
-                     oid, KP, fail, qinv, xinv, qr2i8, Dk, Ik, sizes)
+                     oid, KP, fail, qinv, xinv, qr2i8, Dk, Ik, sizes, qcut)
   if (mode == MODE_IP)
     VS_WIDE(MODE_IP);
   else if (mode == MODE_L2)
@@ -1843,6 +1872,112 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
 // approx = hi(x).hi(q) (1 + d), |d| <= (1 + 2^-24)^5 - 1 < 6 * 2^-24; for the
 // cosine the key then needs no further rounding term (the 2^-22 kept below is
 // slack).
+// ---------------------------------------------------------------------------
+// Query cuts.  The verification (above) needs every row outside the rescored
+// set to have an approximate key >= its threshold T, and only ever uses
+// T' = min(T, a_M + 2.000001 B, ...) (wide check) or passes iff T - B > E_M with
+// E_M <= a_M + B (first check).  Every row with approximate key >= a_M + 2 B
+// is therefore useless to both, and a_M, the M-th smallest key over a query's
+// lane lists, only falls while the pass runs.  Between two launches of the
+// filter pass, x1_qcut sets cut[q] = min(cut[q], a_M(now) + 2.000001 B) (rounded
+// up); the next launches drop every row whose key is not below the cut (the
+// kernel's admission limit becomes min(list last, cut)), and the verification
+// takes T = min(T, cut) as the floor of the rows dropped that way.  Since the
+// final a_M <= a_M(now), the cut is never below the verification's own
+// a_M + 2B: no check changes its outcome, and the lists only lose rows that
+// could never enter the rescored set.  What it saves: a lane list admits rows
+// against its own 8th entry (the 8th best of a 1/128 slice of the corpus at C3);
+// the cut is the M-th best over all of them plus 2B.
+
+// bkey[q]: the bound B of query q (bound_key over its split norms, the same
+// double the verification computes).
+template <int MODE>
+__global__ __launch_bounds__(64) void qbound_kernel(const float* __restrict__ Q, int64_t ld,
+                                                    const float* __restrict__ qn, BoundArgs ba,
+                                                    const unsigned* __restrict__ stats,
+                                                    const float* __restrict__ qr2i8, int nq,
+                                                    double* __restrict__ bkey) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (q >= nq) return;
+  double qh2, qr2, qn2;
+  query_split_norms(Q + (int64_t)q * ld, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2);
+  const double b = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
+  if (lane == 0) bkey[q] = b;
+}
+
+__device__ __forceinline__ uint32_t key_order(float f) {  // float order as unsigned order
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_unorder(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// One wave per query: a_M = the M-th smallest key over the query's P lists of
+// L entries (bitwise search on the order-preserving integer image), then the
+// cut.  Fewer than M entries: no cut yet.
+__global__ __launch_bounds__(64) void qcut_kernel(const float* __restrict__ lkey,
+                                                  const int* __restrict__ lid, int P, int LKP, int L,
+                                                  int M, const double* __restrict__ bkey, int nq,
+                                                  float* __restrict__ cut) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (q >= nq) return;
+  const int64_t base = (int64_t)q * P * LKP;
+  const int n = P * L;
+  auto count_below = [&](uint64_t y) {  // entries with order image < y
+    int c = 0;
+    for (int j = lane; j < n; j += 64) {
+      const int64_t o = base + (int64_t)(j / L) * LKP + j % L;
+      c += (lid[o] >= 0 && (uint64_t)key_order(lkey[o]) < y) ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    return c;
+  };
+  if (count_below(1ull << 32) < M) return;  // uniform
+  // the largest x with fewer than M entries below it: the M-th smallest image
+  uint64_t x = 0;
+  for (int b = 31; b >= 0; --b)
+    if (count_below(x + (1ull << b)) < M) x += 1ull << b;
+  const float aM = key_unorder((uint32_t)x);
+  const double tp = (double)aM + 2.000001 * bkey[q];
+  if (lane == 0 && isfinite(tp) && tp < (double)FLT_MAX) {
+    float t = (float)tp;
+    if ((double)t < tp) t = nextafterf(t, INFINITY);
+    if (t < cut[q]) cut[q] = t;
+  }
+}
+
+hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, int filter,
+                         const unsigned* stats, const float* qr2i8, int nq, double* bkey,
+                         hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  if (ld % 4 != 0) return hipErrorInvalidValue;
+  const BoundArgs ba = make_bound_args(ld, filter);
+#define VS_QB(MD) \
+  hipLaunchKernelGGL(qbound_kernel<MD>, dim3(nq), dim3(64), 0, st, Q, ld, qn, ba, stats, qr2i8, nq, bkey)
+  if (mode == MODE_IP)
+    VS_QB(MODE_IP);
+  else if (mode == MODE_L2)
+    VS_QB(MODE_L2);
+  else if (mode == MODE_COS)
+    VS_QB(MODE_COS);
+  else
+    return hipErrorInvalidValue;
+#undef VS_QB
+  return hipGetLastError();
+}
+
+static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st) {
+  const int nq = a.nqa;
+  hipLaunchKernelGGL(qcut_kernel, dim3(nq), dim3(64), 0, st, part.key, part.id, part.P, part.KP,
+                     x1_lane_len(), a.qcut_m, a.qbkey, nq, a.qcut);
+  return hipGetLastError();
+}
+
+bool x1_qcut_applies(int mode, int filter) { return x1_has_qcut(mode, filter); }
+
 BoundArgs make_bound_args(int64_t ld, int filter) {
   BoundArgs ba;
   ba.filter = filter;

@@ -101,6 +101,9 @@ struct X1Args {
   const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
   const float* xgmax = nullptr;  // int8: launch_group_max of xs (capacity rows)
+  float* qcut = nullptr;         // per query (nqa): the cut, updated between launches
+  const double* qbkey = nullptr; // per query: the verification's bound B (x1_qcut)
+  int qcut_m = 0;                // the M of the verification
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
   const void* QH = nullptr;      // query plane, tile-major (self-join: the stored plane)
   int qtile0 = 0;                // QH's tile of query tile 0 (self-join: self0 / 256)
@@ -183,7 +186,7 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st,
                                  const float* qinv, const float* xinv, const float* qsc,
-                                 const int* qcount = nullptr);
+                                 const int* qcount = nullptr, const float* qcut = nullptr);
 // Flagged queries (flags[i] != 0) -> ascending qlist[0 .. *count), all on the
 // device; *total += count and *total_n += n when not null.
 hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
@@ -220,7 +223,16 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
                               const float* xinv, const float* qsc, const float* Dk,
-                              const int64_t* Ik, unsigned long long* sizes = nullptr);
+                              const int64_t* Ik, unsigned long long* sizes = nullptr,
+                              const float* qcut = nullptr);
+// Query cuts of the filter pass (vs_gemm_x1.hip, "Query cuts"): bkey[q] = the
+// verification's bound B of query q; x1_qcut_applies: the pass kernel of this
+// mode and plane applies X1Args::qcut (launch_gemm_topk_x1 then updates the
+// cuts between its launches, and the verification must get the same array).
+hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, int filter,
+                         const unsigned* stats, const float* qr2i8, int nq, double* bkey,
+                         hipStream_t st);
+bool x1_qcut_applies(int mode, int filter);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
 // (key, label) order, the per-shard half of an exact sharded merge).  With

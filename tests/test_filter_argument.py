@@ -250,3 +250,73 @@ def test_wide_threshold_from_first_check_exact_keys():
         tight.append(len(S))
         loose.append(sum(1 for r in entries if a[r] < min(T, aM + 2.000001 * B)))
     assert np.mean(tight) < 0.75 * np.mean(loose)
+
+
+def _stream_lists(a, owner, P, L, order, cut_at=None, B=None, M=None, late=0):
+    """Lane lists fed row by row in `order` (admission key < the list's last
+    entry, as the kernel's), optionally with a query cut set after the first
+    `cut_at` rows: cut = a_M(lists now) + 2.000001 B, and later rows are admitted
+    only below min(last, cut) (vs_gemm_x1.hip "Query cuts").  Returns the lists,
+    the cut (inf without one) and the number of rows admitted after row
+    `late` (= cut_at or the same point of the run without a cut)."""
+    lists = [[] for _ in range(P)]
+    cut = np.inf
+    admitted = 0
+    for i, r in enumerate(order):
+        if cut_at is not None and i == cut_at:
+            ent = np.array([a[x] for lst in lists for x in lst])
+            if len(ent) >= M:
+                cut = np.nextafter(np.float32(np.sort(ent)[M - 1] + 2.000001 * B),
+                                   np.float32(np.inf))
+        lst = lists[owner[r]]
+        lim = a[lst[-1]] if len(lst) == L else np.inf
+        if a[r] < min(lim, cut):
+            admitted += i >= late
+            lst.append(r)
+            lst.sort(key=lambda x: (a[x], x))
+            del lst[L:]
+    return [np.array(lst, dtype=np.int64) for lst in lists], float(cut), admitted
+
+
+def test_query_cut_keeps_both_checks_and_drops_admissions():
+    """A cut a_M(snapshot) + 2.000001 B taken between two launches of the pass
+    (the final a_M can only be lower) never changes what the checks decide: the
+    wide threshold T' is the same (T' <= a_M + 2B <= cut), the rescored set is
+    the same, the first check's outcome is the same; after the cut the lists
+    admit a fraction of the rows they would."""
+    rng = np.random.default_rng(5)
+    B, M, KF, P, L = 1e-3, 19, 32, 128, 8
+    fewer = []
+    for q in range(40):
+        n = 20000
+        e = rng.standard_normal(n) * 0.01
+        if q % 3 == 0:
+            e[rng.choice(n, 50, replace=False)] = -0.05 + rng.uniform(0, 4 * B, 50)
+        a = e + rng.uniform(-B, B, n)
+        owner = rng.integers(0, P, size=n)
+        order = rng.permutation(n)
+        res = []
+        for cut_at in (None, n // 8):
+            lists, cut, admitted = _stream_lists(a, owner, P, L, order, cut_at, B, M, n // 8)
+            full = [lst for lst in lists if len(lst) == L]
+            T = min((a[lst[-1]] for lst in full), default=np.inf)
+            T = min(T, cut)  # the verification's floor for the rows the cut dropped
+            entries = np.concatenate(lists)
+            srt = entries[np.lexsort((entries, a[entries]))]
+            aM = a[srt[M - 1]]
+            merged = srt[:KF]
+            T1 = min(a[merged[-1]] if len(merged) == KF else np.inf, T)
+            ok1, top1 = _accept(list(merged), T1, e, B, M)
+            Tp = min(T, aM + 2.000001 * B)
+            S = sorted(r for r in entries if a[r] < Tp)
+            ok2, top2 = _accept(S, Tp, e, B, M)
+            exact = np.lexsort((np.arange(n), e))[:M]
+            for ok, top in ((ok1, top1), (ok2, top2)):
+                if ok:
+                    np.testing.assert_array_equal(top, exact)
+            res.append((ok1, ok2, Tp, S, admitted, aM, cut))
+        (o1, o2, tp0, s0, n0, am0, _), (c1, c2, tp1, s1, n1, am1, cut) = res
+        assert am1 == am0 and cut >= am1 + 2 * B
+        assert (o1, o2) == (c1, c2) and tp0 == tp1 and s0 == s1
+        fewer.append(n1 / n0)
+    assert np.mean(fewer) < 0.3
