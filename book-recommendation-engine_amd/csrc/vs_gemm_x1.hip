@@ -83,6 +83,16 @@
 #ifndef VS_X1_SIDE
 #define VS_X1_SIDE 0
 #endif
+// lane-list insertion of the epilogue: 1 = list_insert_par (branch-free,
+// independent compares), 0 = list_insert (a chain of swaps)
+#ifndef VS_X1_PARINS
+#define VS_X1_PARINS 0
+#endif
+#if VS_X1_PARINS
+#define VS_X1_INSERT list_insert_par
+#else
+#define VS_X1_INSERT list_insert
+#endif
 // Diagnostic builds only (tools/x1_probe.sh; wrong results by design): drop the
 // LDS-DMA, the fragment reads, the mid-step barrier or the epilogue.
 #ifndef VS_X1_P_NODMA
@@ -654,7 +664,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 const int bi = __builtin_ctz(cm);
                 cm &= cm - 1;
                 const int row = rowof(rb, bi >> 2) + (bi & 3);
-                list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+                VS_X1_INSERT<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
               }
             } else {
               // the block's candidate rows (int8: sum above the block's integer
@@ -685,7 +695,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 }
                 const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
                                 key < fminf(lk[qb][KR - 1], tq[qb]);
-                if (ok) list_insert<KR, int>(lk[qb], li[qb], key, row);
+                if (ok) VS_X1_INSERT<KR, int>(lk[qb], li[qb], key, row);
               }
             }
           }
@@ -1926,11 +1936,27 @@ __global__ __launch_bounds__(64) void qcut_kernel(const float* __restrict__ lkey
   if (q >= nq) return;
   const int64_t base = (int64_t)q * P * LKP;
   const int n = P * L;
+  // order images (uint64; empty entries 2^32, never counted); up to 1024
+  // entries stay in registers, more are read again per count
+  constexpr int kR = 16;
+  uint64_t v[kR];
+  const bool regs = n <= 64 * kR;  // uniform
+  auto image = [&](int j) -> uint64_t {
+    const int64_t o = base + (int64_t)(j / L) * LKP + j % L;
+    return lid[o] >= 0 ? (uint64_t)key_order(lkey[o]) : (1ull << 32);
+  };
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
+    const int j = lane + 64 * i;
+    v[i] = regs && j < n ? image(j) : (1ull << 32);
+  }
   auto count_below = [&](uint64_t y) {  // entries with order image < y
     int c = 0;
-    for (int j = lane; j < n; j += 64) {
-      const int64_t o = base + (int64_t)(j / L) * LKP + j % L;
-      c += (lid[o] >= 0 && (uint64_t)key_order(lkey[o]) < y) ? 1 : 0;
+    if (regs) {
+#pragma unroll
+      for (int i = 0; i < kR; ++i) c += v[i] < y ? 1 : 0;
+    } else {
+      for (int j = lane; j < n; j += 64) c += image(j) < y ? 1 : 0;
     }
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     return c;
