@@ -88,6 +88,11 @@
 #ifndef VS_X1_PARINS
 #define VS_X1_PARINS 0
 #endif
+// candidate rows of a passing block: 0 = per lane, its candidates one at a time
+// (selects by the lane's row index); 1 = one uniform pass over the 16 rows
+#ifndef VS_X1_ROWLOOP
+#define VS_X1_ROWLOOP 0
+#endif
 #if VS_X1_PARINS
 #define VS_X1_INSERT list_insert_par
 #else
@@ -671,6 +676,39 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               // threshold; bf16: -sum below the last entry), then one at a time:
               // the exact key of the row and its admission
               const float last = fminf(lk[qb][KR - 1], tq[qb]);
+#if VS_X1_ROWLOOP
+              // A/B variant: one uniform pass over the block's 16 rows (the row
+              // index in a scalar register: the sum and the factor are indexed
+              // reads, no per-lane selects), a row skipped when no lane has it
+              int T = INT_MIN;
+              if constexpr (EL == FILTER_I8) {
+                const float c = qsc[qb] * fmx[rb];
+                T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
+              }
+#pragma unroll 1
+              for (int r = 0; r < 16; ++r) {
+                bool cand;
+                if constexpr (EL == FILTER_I8) cand = acc[rb][qb][r] > T;
+                else cand = -acc[rb][qb][r] < last;
+                if (__ballot(cand) == 0) continue;  // uniform
+                if (cand) {
+                  const int row = rowof(rb, r >> 2) + (r & 3);
+                  float key;
+                  if constexpr (EL == FILTER_I8) {
+                    f32x16 rvv;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) rvv[j] = rv[r2][j >> 2][j & 3];
+                    key = -((float)acc[rb][qb][r] * (qsc[qb] * rvv[r]));
+                  }
+                  else
+                    key = -acc[rb][qb][r];
+                  const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
+                                  key < fminf(lk[qb][KR - 1], tq[qb]);
+                  if (ok) VS_X1_INSERT<KR, int>(lk[qb], li[qb], key, row);
+                }
+              }
+              continue;
+#endif
               if constexpr (EL == FILTER_I8) {
                 const float c = qsc[qb] * fmx[rb];
                 const int T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
