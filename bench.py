@@ -565,7 +565,8 @@ def run_knn(args, ctx):
                                     "wide_rescored_mean": round(wr / fw, 1) if fw else 0.0,
                                     "to_bf16_stage": f2,
                                     "fallback_queries": ff,
-                                    "fallback_rate": round(ff / fq, 6), "exact_check": exact_check}
+                                    "fallback_rate": round(ff / fq, 6), "exact_check": exact_check,
+                                    "query_cuts": os.environ.get("VS_X1_QCUT", "default")}
         res["batch1"] = batch1
         res["cpu_baseline"] = cpu
         res["result_sane"] = sane
@@ -673,7 +674,8 @@ def run_selfjoin(args, ctx):
                                     "to_bf16_stage": f2,
                                     "fallback_students": ff,
                                     "fallback_rate": round(ff / fq, 6),
-                                    "exact_check": exact_check}
+                                    "exact_check": exact_check,
+                                    "query_cuts": os.environ.get("VS_X1_QCUT", "default")}
         res["result_sane"] = sane
         res["cpu_baseline"] = None
         return res
