@@ -93,6 +93,11 @@
 #ifndef VS_X1_ROWLOOP
 #define VS_X1_ROWLOOP 0
 #endif
+// query cuts in the pass kernels (x1_qcut; the host applies them when the
+// library is built with them and VS_X1_QCUT=1)
+#ifndef VS_X1_QCUT_K
+#define VS_X1_QCUT_K 0
+#endif
 #if VS_X1_PARINS
 #define VS_X1_INSERT list_insert_par
 #else
@@ -144,8 +149,12 @@ constexpr int kT = 256;
 constexpr int x1_sched(int el) { return VS_X1_SCHED ? VS_X1_SCHED : (el == FILTER_I8 ? 1 : 2); }
 constexpr bool x1_side(int el) { return VS_X1_SIDE && el == FILTER_I8 && x1_sched(el) == 1; }
 constexpr int x1_nbuf(int el) { return x1_side(el) ? 4 : VS_X1_NBUF; }
-// the kernels that apply a per-query cut (the others ignore it)
-constexpr bool x1_has_qcut(int mode, int el) { return el == FILTER_I8 || mode == MODE_IP; }
+// the kernels that apply a per-query cut (the others ignore it); builds with
+// VS_X1_QCUT_K=1 only (the default build keeps the measured kernels as they
+// are until the cuts are measured on the GPU)
+constexpr bool x1_has_qcut(int mode, int el) {
+  return VS_X1_QCUT_K && (el == FILTER_I8 || mode == MODE_IP);
+}
 constexpr int kSideSlots = 8;  // > steps in flight / steps per tile + 1 for every d
 constexpr int kSideSlotB = kT * 4 + 64;  // a tile's factors, then its 16 group maxima
 
@@ -317,6 +326,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 
   int gq[2], selfrow[2];
   float tq[2];
+  // a list's admission limit: its last entry, or the query's cut when lower
+#define VS_X1_LIM(qb) (x1_has_qcut(MODE, EL) ? fminf(lk[qb][KR - 1], tq[qb]) : lk[qb][KR - 1])
   float qa[2], qsc[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -548,7 +559,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int rb = 0; rb < 4; ++rb) {
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
-          const float last = fminf(lk[qb][KR - 1], tq[qb]);
+          const float last = VS_X1_LIM(qb);
           bool p;
           if constexpr (EL == FILTER_I8) {
             const float c = qsc[qb] * fmx[rb];
@@ -654,7 +665,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   key[jj * 4 + e] = MODE == MODE_L2 ? l2_from_ip(qa[qb], rv[r2][jj][e], v)
                                                     : -(v * (qa[qb] * rv[r2][jj][e]));
                 }
-              const float last = fminf(lk[qb][KR - 1], tq[qb]);
+              const float last = VS_X1_LIM(qb);
               cm = 0;
 #pragma unroll
               for (int r = 0; r < 16; ++r) cm |= (uint32_t)(key[r] < last) << r;
@@ -675,7 +686,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               // the block's candidate rows (int8: sum above the block's integer
               // threshold; bf16: -sum below the last entry), then one at a time:
               // the exact key of the row and its admission
-              const float last = fminf(lk[qb][KR - 1], tq[qb]);
+              const float last = VS_X1_LIM(qb);
 #if VS_X1_ROWLOOP
               // A/B variant: one uniform pass over the block's 16 rows (the row
               // index in a scalar register: the sum and the factor are indexed
@@ -703,7 +714,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   else
                     key = -acc[rb][qb][r];
                   const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
-                                  key < fminf(lk[qb][KR - 1], tq[qb]);
+                                  key < VS_X1_LIM(qb);
                   if (ok) VS_X1_INSERT<KR, int>(lk[qb], li[qb], key, row);
                 }
               }
@@ -732,7 +743,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   key = -sel16(acc[rb][qb], bi);
                 }
                 const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
-                                key < fminf(lk[qb][KR - 1], tq[qb]);
+                                key < VS_X1_LIM(qb);
                 if (ok) VS_X1_INSERT<KR, int>(lk[qb], li[qb], key, row);
               }
             }
