@@ -320,3 +320,43 @@ def test_query_cut_keeps_both_checks_and_drops_admissions():
         assert (o1, o2) == (c1, c2) and tp0 == tp1 and s0 == s1
         fewer.append(n1 / n0)
     assert np.mean(fewer) < 0.3
+
+
+def _order_image(k):
+    """vs_gemm_x1.hip key_order: float order as unsigned order."""
+    u = np.asarray(k, np.float32).view(np.uint32).astype(np.uint64)
+    return np.where(u & 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+
+
+def _mth_smallest_by_bits(keys, valid, M):
+    """qcut_kernel's selection restated: the largest x with fewer than M valid
+    images below it, built bit by bit from the top (empty entries: image 2^32)."""
+    img = np.where(valid, _order_image(keys), np.uint64(1 << 32))
+    if int((img < (1 << 32)).sum()) < M:
+        return None
+    x = 0
+    for b in range(31, -1, -1):
+        if int((img < x + (1 << b)).sum()) < M:
+            x += 1 << b
+    u = np.uint32(x)
+    back = np.uint32(u & 0x7FFFFFFF) if u & 0x80000000 else np.uint32(~u)
+    return np.array([back], np.uint32).view(np.float32)[0]
+
+
+def test_query_cut_selection_is_the_mth_smallest_key():
+    rng = np.random.default_rng(3)
+    for trial in range(200):
+        n = int(rng.integers(1, 300))
+        keys = (rng.standard_normal(n) * 10 ** rng.uniform(-3, 3)).astype(np.float32)
+        if trial % 5 == 0:
+            keys[: n // 2] = keys[0]                       # duplicates
+        if trial % 7 == 0:
+            keys[rng.random(n) < 0.2] = np.float32(-0.0)   # signed zeros
+        valid = rng.random(n) < 0.9
+        M = int(rng.integers(1, 40))
+        got = _mth_smallest_by_bits(keys, valid, M)
+        v = np.sort(keys[valid])
+        if len(v) < M:
+            assert got is None
+        else:
+            assert got == v[M - 1]  # -0.0 == 0.0: the order image ranks -0 first
