@@ -121,6 +121,10 @@ def parse(argv=None):
                         "clustered rows like text embeddings (1024 centroids, noise 0.5; "
                         "one GPU only) to measure the filter engine's fallback rate")
     p.add_argument("--batch1-steps", type=int, default=20)
+    p.add_argument("--wide-k", type=int, default=60,
+                   help="the service's k (service.py:529-531) for the wide-k leg")
+    p.add_argument("--wide-k-batch", type=int, default=256)
+    p.add_argument("--wide-k-steps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=1024)
@@ -221,7 +225,24 @@ def cpu_baseline(shard, args, xq_host):
             "kind": "port",
             "sample": f"1 query x {n1} rows, {dt1:.3f} s; extrapolated x{args.ntotal}/{n1} rows",
             "impl": "oracle/faiss_flat.c oracle_knn_seq: faiss's sequential branch (fp32 "
-                    "scalar sums + heap) on one thread, as faiss runs nq=1",
+                    "scalar sums + heap) on one thread, as faiss runs nq=1 (the parity "
+                    "oracle's strict summation order: slower than faiss)",
+        }
+        # faiss-speed stand-in: the same scan with faiss's reassociated SIMD sums
+        cfaiss.knn_seq_simd(xb[:1000], q1, args.k, metric)
+        t0 = time.perf_counter()
+        _, Is = cfaiss.knn_seq_simd(xb[:n1], q1, args.k, metric)
+        dts = time.perf_counter() - t0
+        _, Ic = cfaiss.knn_seq(xb[:n1], q1, args.k, metric)
+        ms_simd = dts * 1e3 * args.ntotal / n1
+        res["batch1"]["faiss_speed"] = {
+            "ms_per_query": round(ms_simd, 3), "qps": round(1e3 / ms_simd, 4), "cores": 1,
+            "kind": "port",
+            "sample": f"1 query x {n1} rows, {dts:.3f} s; extrapolated x{args.ntotal}/{n1} rows",
+            "impl": "oracle/faiss_flat_simd.c: faiss fvec_inner_product/L2sqr's reassociated "
+                    "AVX2 sums (16 lanes, FMA) + the same heap, one thread, -O3; the faiss-"
+                    "speed stand-in (timing only)",
+            "labels_match_scalar": bool((Is == Ic).all()),
         }
     return res
 
@@ -544,6 +565,27 @@ def run_knn(args, ctx):
                   "frac_hbm_peak": round(bytes1 / kern1 / 1e9 / HBM_PEAK_GBS, 4)
                   if kern1 > 0 else None}
 
+    # The service's wide searches (service.py:529-531: k = 60 over a coalesced
+    # batch): inner-product k > 32 is the two-page exact engine (vs_api.hip
+    # run_wide_k), not the filter pass; measured apart so that engine choice
+    # has a number beside the headline.  Not part of `value`.
+    wide = None
+    if (args.wide_k_steps > 0 and metric == vfaiss.METRIC_INNER_PRODUCT
+            and args.wide_k > 32 and not gemv):
+        bw = min(args.wide_k_batch, B)
+        qw = xq[:bw].contiguous()
+        tw, kw, nw, (Dw, Iw) = ctx.timed(
+            lambda i: index.search_device(qw, args.wide_k, stream=ctx.stream),
+            args.wide_k_steps, 1)
+        Iwh = Iw.cpu().numpy()
+        wide = {"k": args.wide_k, "batch": bw, "steps": args.wide_k_steps,
+                "ms_per_search": round(tw / args.wide_k_steps * 1e3, 3),
+                "queries_per_s": round(args.wide_k_steps * bw / tw, 1),
+                "kernel": ctx.lib.timer_kernel(),
+                "kernel_ms_per_dispatch": round(kw / max(1, nw), 3),
+                "result_sane": bool((Iwh >= 0).all() and (Iwh < args.ntotal).all()),
+                "note": "exact two-page engine (run_wide_k); the filter pass serves k <= 28"}
+
     if ctx.rank == 0:
         cpu = None
         if not args.no_cpu_baseline and ctx.world == 1 and args.dtype == "f32":
@@ -568,6 +610,7 @@ def run_knn(args, ctx):
                                     "fallback_rate": round(ff / fq, 6), "exact_check": exact_check,
                                     "query_cuts": os.environ.get("VS_X1_QCUT", "default")}
         res["batch1"] = batch1
+        res["wide_k"] = wide
         res["cpu_baseline"] = cpu
         res["result_sane"] = sane
         return res

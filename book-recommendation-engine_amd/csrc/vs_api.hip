@@ -130,6 +130,19 @@ struct ReaderMark {
         (void)hipEventRecord(r.second, st);
         return;
       }
+    // a new stream: first drop the marks that have completed (a caller with a
+    // stream per request would otherwise grow the list, and every writer's
+    // wait_readers, without bound)
+    for (size_t i = 0; i < idx->readers.size();) {
+      if (hipEventQuery(idx->readers[i].second) == hipSuccess) {
+        (void)hipEventDestroy(idx->readers[i].second);
+        idx->readers[i] = idx->readers.back();
+        idx->readers.pop_back();
+      } else {
+        ++i;
+      }
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
     hipEvent_t ev = nullptr;
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
       (void)hipGetLastError();
@@ -230,7 +243,9 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
     int pick = -1;
     for (size_t i = 0; i < g_chunk_idle.size(); ++i) {
       const ScratchChunk& c = g_chunk_idle[i];
-      if (c.dev != dev || c.size != sz) continue;
+      // the power-of-two chunk of this request, or an exact-size one (the OOM
+      // fallback below) that holds it
+      if (c.dev != dev || c.size < bytes || c.size > sz) continue;
       if (c.st == st || hipEventQuery(c.ev) == hipSuccess) {
         pick = (int)i;
         break;
@@ -242,7 +257,7 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
       *out = g_chunk_idle[pick];
       g_chunk_idle[pick] = g_chunk_idle.back();
       g_chunk_idle.pop_back();
-      g_chunk_idle_bytes -= sz;
+      g_chunk_idle_bytes -= out->size;
       return out->st == st ? hipSuccess : hipStreamWaitEvent(st, out->ev, 0);
     }
   }
@@ -254,11 +269,12 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out) {
     (void)hipGetLastError();
     std::lock_guard<std::mutex> g(g_chunk_mu);
     for (size_t i = 0; i < g_chunk_idle.size(); ++i) {
-      if (g_chunk_idle[i].dev == dev && g_chunk_idle[i].size == sz) {
+      if (g_chunk_idle[i].dev == dev && g_chunk_idle[i].size >= bytes &&
+          g_chunk_idle[i].size <= sz) {
         *out = g_chunk_idle[i];
         g_chunk_idle[i] = g_chunk_idle.back();
         g_chunk_idle.pop_back();
-        g_chunk_idle_bytes -= sz;
+        g_chunk_idle_bytes -= out->size;
         return hipStreamWaitEvent(st, out->ev, 0);
       }
     }

@@ -555,7 +555,8 @@ class ReferenceStoreError(ValueError):
 
 def migrate_reference_store(folder_path: str, texts: List[str], metadatas: List[dict],
                             embeddings=None, ids: Optional[List[str]] = None,
-                            index_name: str = "index", *, verify_sample: int = 0,
+                            index_name: str = "index", *, verify_sample: int = 8,
+                            verify_min_cosine: float = 0.999,
                             **kwargs: Any) -> "FAISS":
     """Migrates a store the reference wrote (``index.faiss`` + LangChain's pickled
     ``index.pkl``) WITHOUT re-embedding the catalogue: the vectors are read from
@@ -571,9 +572,19 @@ def migrate_reference_store(folder_path: str, texts: List[str], metadatas: List[
     count that differs from ``index.faiss``'s ntotal is refused.  ``ids``
     default to fresh uuid4 strings, as ``FAISS.from_texts`` assigns them
     (docstore ids are internal to the store: the reference's readers use
-    ``metadata["book_id"]``).  ``verify_sample`` > 0 embeds that many evenly
-    spaced texts with ``embeddings`` and checks them against the stored rows
-    (the label order check, at that many embedding calls instead of all).
+    ``metadata["book_id"]``).
+
+    The label order is checked by default: ``verify_sample`` (8) evenly spaced
+    texts are embedded with ``embeddings`` and each must point the same way as
+    its stored row (cosine >= ``verify_min_cosine``; a remote embedding API is
+    not bit-reproducible, so no element-wise comparison), at that many
+    embedding calls instead of the whole catalogue.  The reference's rebuild
+    query has no ORDER BY (book_vector/main.py:439), so the caller must give
+    the rows in the order that query returned them when the store was built;
+    a store that ``ensure_store`` seeded (main.py:121: ``from_texts(["dummy"],
+    metadatas=[{"book_id": "dummy"}])`` before the first ``add_texts``) holds
+    that row at label 0, and it must be passed too.  ``verify_sample=0`` skips
+    the check (only when the order is known by construction).
     Writes ``index.docstore.json`` beside the untouched ``index.faiss`` /
     ``index.pkl``; afterwards ``FAISS.load_local`` opens the directory."""
     path = Path(folder_path)
@@ -592,14 +603,21 @@ def migrate_reference_store(folder_path: str, texts: List[str], metadatas: List[
         raise ValueError("migrate_reference_store: ids must be n distinct strings")
     if verify_sample > 0 and n:
         if embeddings is None:
-            raise ValueError("migrate_reference_store: verify_sample needs embeddings")
+            raise ValueError("migrate_reference_store: the label-order check needs embeddings "
+                             "(or verify_sample=0 when the row order is known)")
         pick = sorted({int(i) for i in np.linspace(0, n - 1, min(verify_sample, n))})
-        got = np.asarray(embeddings.embed_documents([texts[i] for i in pick]), dtype=np.float32)
+        got = np.asarray(embeddings.embed_documents([texts[i] for i in pick]), dtype=np.float64)
         for j, i in enumerate(pick):
-            if not np.allclose(index.reconstruct(i), got[j], rtol=1e-5, atol=1e-6):
+            row = np.asarray(index.reconstruct(i), dtype=np.float64)
+            den = float(np.linalg.norm(row) * np.linalg.norm(got[j]))
+            cos = float(row @ got[j]) / den if den > 0 else (1.0 if not row.any() and
+                                                             not got[j].any() else 0.0)
+            if not cos >= verify_min_cosine:
                 raise ValueError(f"migrate_reference_store: row {i} of {index_name}.faiss is "
-                                 f"not the embedding of texts[{i}]: the rows are not in the "
-                                 "store's label order")
+                                 f"not the embedding of texts[{i}] (cosine {cos:.6f} < "
+                                 f"{verify_min_cosine}): the rows are not in the store's "
+                                 "label order (a store seeded by ensure_store holds its "
+                                 "'dummy' row at label 0)")
     docstore = InMemoryDocstore({_id: Document(page_content=t, metadata=m, id=_id)
                                  for t, m, _id in zip(texts, metadatas, ids)})
     store = FAISS(embeddings, index, docstore, dict(enumerate(ids)), **kwargs)

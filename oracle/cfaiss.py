@@ -11,7 +11,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "build", "liboracle_faiss.so")
+_SO_SIMD = os.path.join(_HERE, "build", "liboracle_faiss_simd.so")
 _lib = None
+_lib_simd = None
 
 
 def load():
@@ -52,4 +54,31 @@ def heap_select(scores, k: int, metric: int):
     D = np.empty((nq, k), dtype=np.float32)
     I = np.empty((nq, k), dtype=np.int64)
     load().oracle_heap_select(s.ctypes.data, nq, ny, k, metric, D.ctypes.data, I.ctypes.data)
+    return D, I
+
+
+def load_simd():
+    global _lib_simd
+    if _lib_simd is None:
+        if not os.path.exists(_SO_SIMD):
+            subprocess.run(["make", "-C", _HERE], check=True, capture_output=True)
+        lib = ctypes.CDLL(_SO_SIMD)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        lib.oracle_knn_seq_simd.argtypes = [vp, vp, i64, i64, i64, i64, ctypes.c_int, vp, vp]
+        lib.oracle_knn_seq_simd.restype = None
+        _lib_simd = lib
+    return _lib_simd
+
+
+def knn_seq_simd(xb, xq, k: int, metric: int):
+    """faiss-SPEED stand-in for the nq = 1 baseline (oracle/faiss_flat_simd.c:
+    reassociated 16-lane fp32 sums as faiss's FAISS_PRAGMA_IMPRECISE_LOOP
+    builds, one thread).  Not a parity oracle: its scores round differently."""
+    xb = np.ascontiguousarray(xb, dtype=np.float32)
+    xq = np.ascontiguousarray(xq, dtype=np.float32)
+    nq, d = xq.shape
+    D = np.empty((nq, k), dtype=np.float32)
+    I = np.empty((nq, k), dtype=np.int64)
+    load_simd().oracle_knn_seq_simd(xq.ctypes.data, xb.ctypes.data, d, nq, xb.shape[0], k,
+                                    metric, D.ctypes.data, I.ctypes.data)
     return D, I

@@ -135,21 +135,26 @@ def test_ties_match_faiss_heap(vf, metric, k):
 
 @pytest.mark.parametrize("nq", [1, 2, 5, 300])
 @pytest.mark.parametrize("k", [40, 60, 64])
-def test_ip_wide_k_duplicate_rows(vf, nq, k):
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_ip_wide_k_duplicate_rows(vf, nq, k, dtype):
     """Float rows with a block of 150 duplicates (the re-ingested book of
     book_vector/main.py:148, which add_texts appends again): the duplicates'
     run of equal keys fills the first page, and faiss's rule picks the k
     smallest of their labels (descending); checked against the C heap
-    restatement (labels exact, scores within the fp32 contract)."""
+    restatement (labels exact, scores within the fp32 contract).  The bf16
+    storage variant (C5) runs the same two pages on its own operands (qb16
+    queries, 2-byte rows): the oracle sees the bf16-rounded rows and queries."""
     d = 64
     xb = _rand(6000, d, 71)
     dup = _rand(1, d, 72)[0]
     pos = np.random.default_rng(73).choice(6000, 150, replace=False)
     xb[pos] = dup
     xq = _rand(nq, d, 74) * 0.05 + dup  # near the duplicated row
-    index = vf.IndexFlat(d, IP)
+    index = vf.IndexFlat(d, IP, dtype=dtype)
     index.add(xb)
     D, I = index.search(xq, k)
+    if dtype == "bf16":
+        xb, xq = flat.round_bf16(xb), flat.round_bf16(xq)
     Dc, Ic = cfaiss.knn_seq(xb, xq, k, IP)
     np.testing.assert_array_equal(I, Ic)
     np.testing.assert_allclose(D, Dc, rtol=1e-5, atol=1e-5)
@@ -157,13 +162,15 @@ def test_ip_wide_k_duplicate_rows(vf, nq, k):
 
 @pytest.mark.parametrize("nq", [1, 7, 200])
 @pytest.mark.parametrize("k", [65, 100, 127])
-def test_raw_search_beyond_64(vf, nq, k):
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_raw_search_beyond_64(vf, nq, k, dtype):
     """VS_RAW_ORDER inner-product searches of up to 2 * VS_MAX_K entries (a
     shard's half of a sharded k > 32 search): the lexicographic (key, label)
-    order, both pages, against the fp64 oracle; integer rows (exact scores)."""
+    order, both pages, against the fp64 oracle; integer rows (exact scores,
+    also in bf16 storage: small integers are bf16 values)."""
     xb = _rand(900, 4, 81, "int")
     xq = _rand(nq, 4, 82, "int")
-    index = vf.IndexFlat(4, IP)
+    index = vf.IndexFlat(4, IP, dtype=dtype)
     index.add(xb)
     D, I = index.search(xq, k, raw=True)
     Dr, Ir = flat.knn_lex(xb, xq, k, IP)

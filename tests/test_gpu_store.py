@@ -262,7 +262,8 @@ def test_reference_store_migration_without_reembedding_on_gpu(tmp_path, golden):
     (d / "index.pkl").write_bytes(b"\x80\x04cos\nsystem\n.")
     with pytest.raises(vlc.ReferenceStoreError):
         vlc.FAISS.load_local(str(d), NoEmbed(), allow_dangerous_deserialization=True)
-    vlc.migrate_reference_store(str(d), inputs["book_texts"], inputs["book_metadata"], NoEmbed())
+    vlc.migrate_reference_store(str(d), inputs["book_texts"], inputs["book_metadata"], NoEmbed(),
+                                verify_sample=0)
     store = vlc.FAISS.load_local(str(d), NoEmbed(), allow_dangerous_deserialization=True)
     assert isinstance(store.index, vfaiss.IndexFlat) and store.index.ntotal == 341
     pos = {m["book_id"]: i for i, m in enumerate(inputs["book_metadata"])}

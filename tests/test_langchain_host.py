@@ -210,6 +210,21 @@ def test_reference_store_migrates_without_reembedding(tmp_path, patched_indexes,
     with pytest.raises(ValueError):  # rows out of label order fail the sample check
         vlc.migrate_reference_store(str(ref_dir), texts[::-1], metas[::-1], counting,
                                     verify_sample=3, index_factory=factory)
+    with pytest.raises(ValueError):  # the order check is on by default
+        vlc.migrate_reference_store(str(ref_dir), texts[1:] + texts[:1], metas[1:] + metas[:1],
+                                    counting, index_factory=factory)
+    with pytest.raises(ValueError):  # and needs embeddings unless switched off
+        vlc.migrate_reference_store(str(ref_dir), texts, metas, None, index_factory=factory)
+
+    class Noisy(Counting):  # a remote API: the same text, not the same bits
+        def embed_documents(self, t):
+            self.calls += len(t)
+            e = np.asarray(emb.embed_documents(t), dtype=np.float64)
+            return (e * (1 + 1e-4 * np.cos(np.arange(e.shape[1])))).tolist()
+
+    noisy = Noisy()
+    vlc.migrate_reference_store(str(ref_dir), texts, metas, noisy, index_factory=factory)
+    assert noisy.calls == 8  # the default sample
     counting.calls = 0
     mig = vlc.migrate_reference_store(str(ref_dir), texts, metas, counting, verify_sample=4,
                                       index_factory=factory)

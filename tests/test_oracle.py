@@ -231,3 +231,18 @@ def test_strict_selfjoin_checker():
     S2[3, 2] += 2e-6
     assert flat.selfjoin_mismatches(S2, Ir, Sr, Ir, x, np.arange(400), strict=True)
     assert not flat.selfjoin_mismatches(S2, Ir, Sr, Ir, x, np.arange(400))
+
+
+@pytest.mark.parametrize("metric", [IP, L2])
+def test_simd_speed_standin_matches_scalar_labels(metric):
+    """oracle/faiss_flat_simd.c (the faiss-speed stand-in bench.py times for
+    nq = 1) scans the same rows with reassociated sums: on separated float
+    data its labels equal the scalar heap oracle's and its scores agree to
+    fp32 rounding."""
+    rng = np.random.default_rng(17)
+    xb = rng.standard_normal((3000, 100)).astype(np.float32)
+    xq = rng.standard_normal((3, 100)).astype(np.float32)
+    D, I = cfaiss.knn_seq(xb, xq, 10, metric)
+    Ds, Is = cfaiss.knn_seq_simd(xb, xq, 10, metric)
+    np.testing.assert_array_equal(Is, I)
+    np.testing.assert_allclose(Ds, D, rtol=1e-5, atol=1e-4)

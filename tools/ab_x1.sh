@@ -18,7 +18,7 @@ for round in 1 2; do
     lib=book-recommendation-engine_amd/vsearch/libvsearch_$name.so
     [ "$name" = base ] && lib=book-recommendation-engine_amd/vsearch/libvsearch.so
     env "${envs[@]}" VSEARCH_LIB=$PWD/$lib timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 \
-      --batch1-steps 0 --no-cpu-baseline "$@" > "$OUT/${v}_r${round}.log" 2>&1 || { echo "$v failed"; exit 1; }
+      --batch1-steps 0 --wide-k-steps 0 --no-cpu-baseline "$@" > "$OUT/${v}_r${round}.log" 2>&1 || { echo "$v failed"; exit 1; }
     python3 - "$OUT/${v}_r${round}.log" "$v" <<'PY'
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
