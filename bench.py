@@ -316,17 +316,29 @@ class Ctx:
             self.lib = None
             self.stream = 0
         else:
+            # Test hooks (tests/test_gpu_world2.py; the driver sets neither):
+            # VS_BENCH_DEVICE puts every rank on one device, VS_BENCH_BACKEND=gloo
+            # runs the collectives on host tensors (RCCL refuses two ranks on one
+            # GPU), so the N > 1 data path runs on a one-GPU box.
+            if os.environ.get("VS_BENCH_DEVICE") is not None:
+                self.local = int(os.environ["VS_BENCH_DEVICE"])
             torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", rank=self.rank, world_size=self.world,
-                                    device_id=torch.device("cuda", self.local))
+            if os.environ.get("VS_BENCH_BACKEND", "nccl") == "gloo":
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            else:
+                dist.init_process_group("nccl", rank=self.rank, world_size=self.world,
+                                        device_id=torch.device("cuda", self.local))
             from vsearch import _lib
 
             self.dev = torch.device("cuda", self.local)
             self.lib = _lib
             self.stream = torch.cuda.current_stream().cuda_stream
+        self.backend = dist.get_backend()
+        # collectives run on device tensors over RCCL, on host tensors over gloo
+        self.cdev = self.dev if self.backend == "nccl" else torch.device("cpu")
         # head-count over the collective itself: every rank reports (rank, device)
         me = torch.tensor([1, self.rank, -1 if self.dry else self.local], dtype=torch.int64,
-                          device=self.dev)
+                          device=self.cdev)
         allv = [torch.zeros_like(me) for _ in range(self.world)]
         dist.all_gather(allv, me)
         self.ranks_seen = int(sum(int(v[0]) for v in allv))
@@ -341,7 +353,7 @@ class Ctx:
         self.synchronize()
 
     def max_over_ranks(self, x: float) -> float:
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.cdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -643,8 +655,19 @@ def run_selfjoin(args, ctx):
     def step(i):
         index.selfjoin_device(k, lo, nq, D.data_ptr(), I.data_ptr(), stream=ctx.stream)
         if ctx.world > 1:  # the rows go to the one writer process
-            ctx.dist.gather(Dp, gD, dst=0)
-            ctx.dist.gather(Ip, gI, dst=0)
+            if ctx.backend == "nccl":
+                ctx.dist.gather(Dp, gD, dst=0)
+                ctx.dist.gather(Ip, gI, dst=0)
+            else:  # gloo (test hook): host tensors
+                hD = [t.cpu() for t in gD] if gD else None
+                hI = [t.cpu() for t in gI] if gI else None
+                ctx.dist.gather(Dp.cpu(), hD, dst=0)
+                ctx.dist.gather(Ip.cpu(), hI, dst=0)
+                if ctx.rank == 0:
+                    for t, h in zip(gD, hD):
+                        t.copy_(h)
+                    for t, h in zip(gI, hI):
+                        t.copy_(h)
         return None
 
     ctx.lib.filter_stats(reset=True)

@@ -126,6 +126,9 @@
 #ifndef VS_X1_P_NOWAIT  // no vmcnt wait in the loop (the DMA still issued)
 #define VS_X1_P_NOWAIT 0
 #endif
+#ifndef VS_X1_P_NOCAND  // the epilogue's phase 1 only: no block ever passes
+#define VS_X1_P_NOCAND 0
+#endif
 
 namespace vs {
 
@@ -583,6 +586,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         }
       }
       VS_X1_EMARK(6);
+#if VS_X1_P_NOCAND
+      asm volatile("" ::"v"(pass));
+      pass = 0;
+#endif
       // Phases 2 and 3 per half tile (rb pair): the per-row values (int8
       // factors; bf16 L2 / cosine norms) of the lane's 32 rows, when any lane of
       // the wave has a candidate in the pair — eight 16-B loads in ONE asm

@@ -154,6 +154,11 @@ class ShardedIndexFlat:
     def _gather(self, Dt, It):
         import torch
 
+        if Dt.device.type == "cuda" and self._dist.get_backend(self.group) != "nccl":
+            # gloo gathers host tensors only (its GPU support is broadcast and
+            # all-reduce): stage through the host, hand device tensors back
+            Dh, Ih = self._gather(Dt.cpu(), It.cpu())
+            return Dh.to(Dt.device), Ih.to(It.device)
         # flat (world*nq, k) outputs: the layout every backend accepts
         Dall = torch.empty((self.world * Dt.shape[0],) + tuple(Dt.shape[1:]), dtype=Dt.dtype,
                            device=Dt.device)

@@ -1,7 +1,8 @@
 """GPU, BASELINE config C3 at full size: 10M x 1536 fp32, k = 10, inner product
 (and L2), the DEFAULT engine, batch 4096 and batch 1 — the headline workload
-(bench.py) checked against the oracle on sampled queries from the first and
-last query tiles.
+(bench.py) checked against the oracle on 64 sampled queries spanning all 16 query tiles,
+plus the embedding-like clustered corpus bench.py --data clustered measures
+(unit-norm rows, 1024 centroids: the int8 -> bf16 -> deep bf16 hand-off).
 
 Oracle at this size (chunked, tests only): the rows are read back from the
 index (vs_reconstruct_n is bit-exact, test_gpu_parity.py) in 1M-row chunks;
@@ -29,7 +30,12 @@ from oracle import flat
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
 N, D_, K = 10_000_000, 1536, 10
-SAMPLE = [0, 1, 255, 256, 2047, 3839, 3840, 4095]  # first / last 256-query tiles
+# 64 queries: the first and last query of every 256-query tile, two more inside
+# each (every tile of the int8 pass, both ends of its lane lists' query blocks);
+# the proven-candidate oracle's cost is the 61 GB read-back, not the sample size
+SAMPLE = sorted({q for t in range(16) for q in (256 * t, 256 * t + 37, 256 * t + 160,
+                                                 256 * t + 255)})
+CL_SAMPLE = SAMPLE[::2] + [4095]  # clustered: 33 queries (m = 256 candidates each)
 
 
 @pytest.fixture(scope="module")
@@ -63,6 +69,44 @@ def test_c3_batch4096_sampled_against_oracle(c3, metric):
     assert (diffs <= 0).all() if metric == flat.METRIC_INNER_PRODUCT else (diffs >= 0).all()
     for row, q in enumerate(SAMPLE):
         assert_against_candidates(Db[q], Ib[q], cand[row], metric, K, D_, strict=True)
+
+
+@pytest.fixture(scope="module")
+def c3_clustered():
+    """bench.py's clustered corpus (ClusteredRows: normalize(c[i % 1024] + 0.5 n),
+    seed 1234, queries noise seed 5678) at 10M x 1536, inner product: the data
+    shape the reference's text-embedding-3-small vectors have (settings.py:16-18)
+    and the case where most queries leave the int8 stage."""
+    import torch
+
+    from bench import ClusteredRows
+    from vsearch import faiss as vfaiss
+
+    index = vfaiss.IndexFlat(D_, flat.METRIC_INNER_PRODUCT)
+    index.reserve(N)
+    gen = ClusteredRows(torch, D_, seed=1234)
+    for r0 in range(0, N, 1 << 20):
+        x = gen.rows(r0, min(1 << 20, N - r0))
+        index.add_device(x.data_ptr(), x.shape[0])
+        torch.cuda.synchronize()
+        del x
+    xq = ClusteredRows(torch, D_, seed=1234, noise_seed=5678).rows(0, 4096).cpu().numpy()
+    torch.cuda.empty_cache()
+    D, I = index.search(xq, K)
+    D2, I2 = index.search(xq, K)  # the adaptive order's second search (bf16 first)
+    cand = proven_candidates(index, xq[CL_SAMPLE], flat.METRIC_INNER_PRODUCT, N, K, m=256)
+    del index
+    return D, I, D2, I2, cand
+
+
+def test_c3_clustered_sampled_against_oracle(c3_clustered):
+    D, I, D2, I2, cand = c3_clustered
+    assert (I >= 0).all() and (I < N).all() and (np.diff(D, axis=1) <= 0).all()
+    for row, q in enumerate(CL_SAMPLE):
+        assert_against_candidates(D[q], I[q], cand[row], flat.METRIC_INNER_PRODUCT, K, D_,
+                                  strict=True)
+        assert_against_candidates(D2[q], I2[q], cand[row], flat.METRIC_INNER_PRODUCT, K, D_,
+                                  strict=True)
 
 
 @pytest.mark.parametrize("metric", [flat.METRIC_INNER_PRODUCT, flat.METRIC_L2])

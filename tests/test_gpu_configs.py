@@ -1,7 +1,7 @@
 """GPU, BASELINE configs C2 and C4 at full size with the DEFAULT engine (the
 staged int8 -> bf16 -> fp32 filter-and-verify path), checked against the fp64
-oracle on sampled queries / students from the first and last query tiles and
-across the self-join's 65,536-row chunks.
+oracle on 64 sampled queries / students spanning every query tile and the
+self-join's 65,536-row chunks.
 
 C2: 1M x 1536 fp32, batch 1024, top-10 inner product (bench.py --workload c2).
 C4: 1M x 1536 fp32, cosine top-50 self-join excluding self (bench.py --workload
@@ -39,7 +39,9 @@ def test_c2_batch1024_sampled_against_oracle():
     D, I = index.search(xq, k)
     assert I.shape == (1024, k) and (I >= 0).all() and (I < N).all()
     assert (np.diff(D, axis=1) <= 0).all()
-    sample = [0, 1, 255, 256, 511, 767, 768, 1023]
+    # 64 queries: 16 per query tile, both ends of each
+    sample = sorted({q for t in range(4) for q in [256 * t + j for j in range(0, 256, 17)]
+                     + [256 * t + 255]})
     xb = _rows(index)
     s = np.zeros((len(sample), N))
     q64 = xq[sample].astype(np.float64)
@@ -61,7 +63,11 @@ def test_c4_selfjoin_top50_sampled_against_oracle():
     S, I = index.selfjoin(k)
     assert I.shape == (N, k) and (I >= 0).all() and (I < N).all()
     assert not (I == np.arange(N)[:, None]).any()
-    sample = np.array([0, 1, 255, 256, 65535, 65536, 131071, 500000, 999743, 999999])
+    # 64 students: both sides of every 65,536-row chunk boundary and of query
+    # tiles inside chunks, plus the last rows
+    edges = [c * 65536 + o for c in range(16) for o in (-1, 0)] + [255, 256, 500000, 999743]
+    fill = np.linspace(1, N - 2, 64 - len(edges)).astype(np.int64).tolist()
+    sample = np.array(sorted({e for e in edges + fill + [N - 1] if 0 <= e < N}))
     xb = _rows(index)
     Sr, Ir = flat.pgvector_cosine_topk(xb, k, q_rows=sample)
     bad = flat.selfjoin_mismatches(S[sample], I[sample], Sr, Ir, xb, sample, strict=True)
