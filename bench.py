@@ -388,6 +388,13 @@ class Ctx:
         return self.max_over_ranks(t1 - t0), kms, nl, last
 
 
+def dump_record(d, o):
+    """The filter pass's dump launches over the timed steps (vs_gemm_x1.hip
+    header): blocks stored below the cuts and lane lists out of slots."""
+    return {"on": os.environ.get("VS_X1_DUMP", "1") != "0", "blocks_dumped": d,
+            "lists_out_of_slots": o}
+
+
 def base_result(args, ctx, value, elapsed, unit="queries/s"):
     return {
         "metric": METRIC_NAME,
@@ -514,6 +521,7 @@ def run_knn(args, ctx):
     fw = ctx.lib.filter_wide_stats()
     f2 = ctx.lib.filter_second_stats()
     we, wr = ctx.lib.filter_wide_sets()
+    dmp = ctx.lib.filter_dump_stats()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     sane = bool((Ih >= 0).all() and (Ih < args.ntotal).all())
@@ -620,7 +628,7 @@ def run_knn(args, ctx):
                                     "to_bf16_stage": f2,
                                     "fallback_queries": ff,
                                     "fallback_rate": round(ff / fq, 6), "exact_check": exact_check,
-                                    "query_cuts": os.environ.get("VS_X1_QCUT", "default")}
+                                    "dump_launches": dump_record(*dmp)}
         res["batch1"] = batch1
         res["wide_k"] = wide
         res["cpu_baseline"] = cpu
@@ -675,6 +683,7 @@ def run_selfjoin(args, ctx):
     fw = ctx.lib.filter_wide_stats()
     f2 = ctx.lib.filter_second_stats()
     we, wr = ctx.lib.filter_wide_sets()
+    dmp = ctx.lib.filter_dump_stats()
     fq, ff = ctx.lib.filter_stats(reset=True)
     Ih = I.cpu()
     sane = bool(((Ih >= 0) & (Ih < N)).all()) and not bool(
@@ -741,7 +750,7 @@ def run_selfjoin(args, ctx):
                                     "fallback_students": ff,
                                     "fallback_rate": round(ff / fq, 6),
                                     "exact_check": exact_check,
-                                    "query_cuts": os.environ.get("VS_X1_QCUT", "default")}
+                                    "dump_launches": dump_record(*dmp)}
         res["result_sane"] = sane
         res["cpu_baseline"] = None
         return res

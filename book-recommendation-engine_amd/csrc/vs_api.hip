@@ -367,8 +367,9 @@ const char* g_timer_kernel = "";
 // search): [0] queries, [1] flagged by the first check (given to the wide
 // check), [2] flagged by both (redone by the exact engine), [3] handed to a
 // second filter stage, [4] wide-set entries, [5] of them rescored (the rest
-// reuse the first check's keys).  One buffer per device.
-constexpr int kStatSlots = 6;
+// reuse the first check's keys), [6] blocks stored by dump launches, [7] lane
+// lists out of dump slots.  One buffer per device.
+constexpr int kStatSlots = 8;
 std::mutex g_stats_mu;
 std::vector<unsigned long long*> g_dev_stats;
 
@@ -685,11 +686,12 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
 //     once), whose rows overwrite theirs.
 // The host never waits: counts live in device memory.  `gl` / `gc` (stages
 // after the first): the batch is queries gl[0 .. *gc) of `a`.
-// query cuts in the filter pass (env VS_X1_QCUT=1 turns them on, for A/B)
-static bool qcut_enabled() {
+// dump launches in the filter pass (default; env VS_X1_DUMP=0 runs every
+// launch as a list launch, for A/B)
+static bool dump_enabled() {
   static const bool v = [] {
-    const char* e = getenv("VS_X1_QCUT");
-    return e && atoi(e) != 0;
+    const char* e = getenv("VS_X1_DUMP");
+    return !e || atoi(e) != 0;
   }();
   return v;
 }
@@ -824,22 +826,48 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   x.self0 = self_rows ? a.self0 : -1;
   x.qrow = qrow;
   x.qcount = gc;
-  if (!gathered && x1_qcut_applies(mode, plane) && qcut_enabled()) {
-    // query cuts (vs_gemm_x1.hip "Query cuts"): updated between the pass's
-    // launches, the verification's floor for the rows they drop
-    VS_HIP(scr.alloc((void**)&x.qcut, (size_t)qa_rows * sizeof(float)), "vs: scratch");
-    double* bk = nullptr;
-    VS_HIP(scr.alloc((void**)&bk, (size_t)qa_rows * sizeof(double)), "vs: scratch");
-    VS_HIP(hipMemsetD32Async((hipDeviceptr_t)x.qcut, 0x7f7fffff, (size_t)qa_rows, st), "vs: cuts");
-    VS_HIP(launch_qbound(mode, Q, idx->ld, qaux, plane, stats, qr2, qa_rows, bk, st), "vs: cuts");
-    x.qbkey = bk;
-    x.qcut_m = need;
+  if (!gathered && x1_dump_applies(mode, plane) && dump_enabled()) {
+    // query cuts + dump launches (vs_gemm_x1.hip header and "Query cuts"): the
+    // cuts are set after the pass's first launch and are the verification's
+    // floor for the rows the dump launches drop.  The dump slots: up to
+    // x1_dump_slots() per lane list within ~8 GB (C4's 65,536-student chunks:
+    // 15); fewer than 8 (or no memory): every launch is a list launch.
+    const int64_t lists = (int64_t)x.nq_pad * part.P;
+    const int dR = (int)std::min<int64_t>(x1_dump_slots(), (int64_t(8) << 30) / (lists * 68));
+    if (dR >= 8) {
+      int *dc = nullptr, *ds = nullptr, *dt = nullptr;
+      hipError_t e = scr.alloc((void**)&dc, (size_t)lists * sizeof(int));
+      if (e == hipSuccess) e = scr.alloc((void**)&ds, (size_t)lists * dR * 16 * sizeof(int));
+      if (e == hipSuccess) e = scr.alloc((void**)&dt, (size_t)lists * dR * sizeof(int));
+      if (e == hipSuccess) {
+        VS_HIP(scr.alloc((void**)&x.qcut, (size_t)qa_rows * sizeof(float)), "vs: scratch");
+        double* bk = nullptr;
+        VS_HIP(scr.alloc((void**)&bk, (size_t)qa_rows * sizeof(double)), "vs: scratch");
+        VS_HIP(hipMemsetD32Async((hipDeviceptr_t)x.qcut, 0x7f7fffff, (size_t)qa_rows, st),
+               "vs: cuts");
+        VS_HIP(hipMemsetAsync(dc, 0, (size_t)lists * sizeof(int), st), "vs: dumps");
+        VS_HIP(launch_qbound(mode, Q, idx->ld, qaux, plane, stats, qr2, qa_rows, bk, st),
+               "vs: cuts");
+        x.qbkey = bk;
+        x.qcut_m = need;
+        x.dump = true;
+        x.dcount = dc;
+        x.dsum = ds;
+        x.dtag = dt;
+        x.dR = dR;
+      } else {
+        (void)hipGetLastError();  // out of memory for the dumps: list launches
+      }
+    }
   }
   {
     KernelTimer tm(st, gathered ? nullptr : i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1");
     VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &tm.dispatches), "vs: gemm_topk_x1 launch");
     tm.stop();
   }
+  unsigned long long* dst = device_stats(idx->device);
+  if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
+  VS_HIP(launch_x1_replay(x, part, st, dst + 6), "vs: x1 replay");
   // approximate top-KF per query (plain lexicographic order: the L2 merge)
   float* Dk = nullptr;
   int64_t* Ik = nullptr;
@@ -868,8 +896,6 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
                                Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
                                st, qinv, xinv, qr2, gc, x.qcut),
          "vs: verify");
-  unsigned long long* dst = device_stats(idx->device);
-  if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
   // statistics: [0] queries (first stage), [1] flagged by a first check, [2]
   // redone by the exact engine, [3] handed to a second filter stage
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, gathered ? nullptr : dst + 0, st),
@@ -1828,6 +1854,16 @@ int vs_filter_wide_sets(int64_t* entries, int64_t* rescored) {
   if (rc) return rc;
   *entries = (int64_t)c[4];
   *rescored = (int64_t)c[5];
+  return VS_OK;
+}
+
+int vs_filter_dump_stats(int64_t* dumps, int64_t* overflows) {
+  if (!dumps || !overflows) return fail(VS_E_INVALID, "vs_filter_dump_stats: null output");
+  unsigned long long c[kStatSlots];
+  int rc = read_filter_stats(c, 0);
+  if (rc) return rc;
+  *dumps = (int64_t)c[6];
+  *overflows = (int64_t)c[7];
   return VS_OK;
 }
 

@@ -28,9 +28,23 @@
 // global_load_lds_dwordx4 (LDS-DMA) NBUF-1 steps ahead; see gemm_topk_x1
 // below for the step schedule.
 //
-// Epilogue per 256-row tile (rare work after the first tiles): the keys of a
-// lane's 16 rows of one 32-row block are reduced to their minimum; only when it
-// can enter the lane's list are they inserted one by one.
+// Two kinds of launch (template flag DUMP), per search:
+//  * list launches (the first launch of a pass, gathered batches, the bf16
+//    L2 / cosine kernels): the epilogue of every 256-row tile reduces each
+//    lane's 16 keys of a 32-row block to their maximum and, only when the
+//    block can enter the lane's list, inserts its rows one by one;
+//  * dump launches (every later launch of an int8 or bf16 inner-product
+//    pass): the lists stay in memory; the epilogue compares each block with
+//    the query's CUT (x1_qcut, set from the first launch's lists) and, for
+//    the rare block that may hold a row below it, stores the lane's 16 raw
+//    sums to a per-list dump slot; x1_replay (after the pass) admits the dumped
+//    rows into the lists exactly as a list launch would have — same keys, same
+//    order, same admission rule — so both kinds leave the same lists.
+// The lists are per lane, so a list launch pays for a wave's rows whenever ANY
+// of its 64 lanes admits one (an exec-masked insertion chain per block that
+// passes somewhere): about a sixth of the int8 pass (profiles/r04a/x1_probes.txt:
+// 3.45 ms per dispatch with the candidate work, 2.86 ms with the epilogue's
+// per-block test alone).  A dump costs five stores on the lanes that pass.
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -39,101 +53,19 @@
 
 #include "vs_device.h"
 
-// Static priority of one half of the waves (MI355X_MICROARCH.md, "Two waves
-// per SIMD" 4): 0 none, 1 waves 4-7, 2 waves 0-3.  With the stagger below none
-// measured fastest (profiles/r02h_ab_stagger.txt).
-#ifndef VS_X1_PRIO
-#define VS_X1_PRIO 0
+// Diagnostic builds only (tools/x1_probe.sh; wrong results by design): a mask
+// of ablations — 1 no LDS-DMA, 2 no fragment reads, 4 no mid-step barrier,
+// 8 no epilogue, 16 no database pieces, 32 no query pieces, 64 no vmcnt wait in
+// the loop, 128 the epilogue's per-block test alone (no block ever passes).
+#ifndef VS_X1_PROBE
+#define VS_X1_PROBE 0
 #endif
-// LDS images in the ring (5: 4 steps in flight, all 160 KB; 4: -1 %, profiles/r02y)
-#ifndef VS_X1_NBUF
-#define VS_X1_NBUF 5
-#endif
-#ifndef VS_X1_STAGGER
-#define VS_X1_STAGGER 1
-#endif
-// Round-2 schedule: 1 = the step's 4 LDS-DMA pieces split 2 + 2 over its two
-// halves, NBUF - 2 steps in flight (the first half writes the image of step
-// s-2, whose reads every wave has retired); 0 = all 4 in the second half,
-// NBUF - 1 steps in flight.
-#ifndef VS_X1_DMASPLIT
-#define VS_X1_DMASPLIT 0
-#endif
-// Step schedule: 1 = fragment reads half a step ahead, DMA pieces between the
-// MFMAs of each wave (round 2); 2 = separate load and matrix segments (below);
-// 3 = the same segments per half step;
-// 0 = per plane: int8 1, bf16 2 (the faster of the two on each, C3 uniform
-// int8 68.6k vs 65.9k queries/s, clustered bf16 34.4k vs 32.5k:
-// profiles/r03_ab_sched.txt).
-#ifndef VS_X1_SCHED
-#define VS_X1_SCHED 0
-#endif
-// A/B variant: the int8 fast reject with one factor bound per chunk (the
-// maximum of its tiles' group maxima, loaded once) instead of a scalar load of
-// the tile's group maxima in every epilogue.
-#ifndef VS_X1_XGCHUNK
-#define VS_X1_XGCHUNK 0
-#endif
-// int8 row factors through LDS: the 1 KB of factors of every database tile
-// rides the tile's first LDS-DMA step (8 lanes of each wave, into one of 8
-// side slots), and the epilogue reads them (its factor bounds and exact keys)
-// with ds_reads instead of scalar loads of the group maxima and vector loads
-// that retire with vmcnt(0) — a drain of the DMA ring each time.  The ring
-// drops to 4 images (128 KB + 8 KB of side slots).
-#ifndef VS_X1_SIDE
-#define VS_X1_SIDE 0
-#endif
-// lane-list insertion of the epilogue: 1 = list_insert_par (branch-free,
-// independent compares), 0 = list_insert (a chain of swaps)
-#ifndef VS_X1_PARINS
-#define VS_X1_PARINS 0
-#endif
-// candidate rows of a passing block: 0 = per lane, its candidates one at a time
-// (selects by the lane's row index); 1 = one uniform pass over the 16 rows
-#ifndef VS_X1_ROWLOOP
-#define VS_X1_ROWLOOP 0
-#endif
-// query cuts in the pass kernels (x1_qcut; the host applies them when the
-// library is built with them and VS_X1_QCUT=1)
-#ifndef VS_X1_QCUT_K
-#define VS_X1_QCUT_K 0
-#endif
-#if VS_X1_PARINS
-#define VS_X1_INSERT list_insert_par
-#else
-#define VS_X1_INSERT list_insert
-#endif
-// Diagnostic builds only (tools/x1_probe.sh; wrong results by design): drop the
-// LDS-DMA, the fragment reads, the mid-step barrier or the epilogue.
-#ifndef VS_X1_P_NODMA
-#define VS_X1_P_NODMA 0
-#endif
-#ifndef VS_X1_P_NOLDS
-#define VS_X1_P_NOLDS 0
-#endif
-#ifndef VS_X1_P_NOBAR
-#define VS_X1_P_NOBAR 0
-#endif
-#ifndef VS_X1_P_NOEPI
-#define VS_X1_P_NOEPI 0
-#endif
-#ifndef VS_X1_P_NODMA_X  // drop only the database (X) pieces
-#define VS_X1_P_NODMA_X 0
-#endif
-#ifndef VS_X1_P_NODMA_Q  // drop only the query (Q) pieces
-#define VS_X1_P_NODMA_Q 0
-#endif
-#ifndef VS_X1_P_NOWAIT  // no vmcnt wait in the loop (the DMA still issued)
-#define VS_X1_P_NOWAIT 0
-#endif
-#ifndef VS_X1_P_NOCAND  // the epilogue's phase 1 only: no block ever passes
-#define VS_X1_P_NOCAND 0
-#endif
+#define VS_X1_P(bit) ((VS_X1_PROBE & (bit)) != 0)
 
 namespace vs {
 
 // Diagnostic builds only (VS_X1_STAMP=1, tools/build_variant.sh): per-segment
-// s_memtime sums of the segmented schedule, [group (waves 0-3 | 4-7)][segment]
+// s_memtime sums of the step schedules, [group (waves 0-3 | 4-7)][segment]
 // (segments: load issue, vmcnt wait, barrier 1, matrix issue, barrier 2,
 // epilogue), added once per wave at the end; read by vs_x1_stamps.  The real
 // kernel has no stamp.
@@ -147,19 +79,19 @@ __device__ unsigned long long g_x1_stamps[kStampN];
 
 namespace {
 
-constexpr int kT = 256;
-// the step schedule, the side slots and the ring depth of a plane
-constexpr int x1_sched(int el) { return VS_X1_SCHED ? VS_X1_SCHED : (el == FILTER_I8 ? 1 : 2); }
-constexpr bool x1_side(int el) { return VS_X1_SIDE && el == FILTER_I8 && x1_sched(el) == 1; }
-constexpr int x1_nbuf(int el) { return x1_side(el) ? 4 : VS_X1_NBUF; }
-// the kernels that apply a per-query cut (the others ignore it); builds with
-// VS_X1_QCUT_K=1 only (the default build keeps the measured kernels as they
-// are until the cuts are measured on the GPU)
-constexpr bool x1_has_qcut(int mode, int el) {
-  return VS_X1_QCUT_K && (el == FILTER_I8 || mode == MODE_IP);
-}
-constexpr int kSideSlots = 8;  // > steps in flight / steps per tile + 1 for every d
-constexpr int kSideSlotB = kT * 4 + 64;  // a tile's factors, then its 16 group maxima
+constexpr int kT = 256;               // rows (and queries) per tile
+constexpr int kNbuf = 5;              // LDS images in the ring (4: -1 %, profiles/r02y)
+constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
+constexpr int kDumpMaxR = 32;         // dump slots per lane list per search (at most)
+// The step schedule of a plane (A/B: C3 uniform int8 68.6k vs 65.9k queries/s,
+// clustered bf16 34.4k vs 32.5k, profiles/r03_ab_sched.txt): 1 = fragment
+// reads half a step ahead, DMA pieces between the MFMAs (int8); 2 = separate
+// load and matrix segments (bf16).
+constexpr int x1_sched(int el) { return el == FILTER_I8 ? 1 : 2; }
+// the kernels with a dump form: every key of theirs follows from the raw sum
+// and per-row values the replay can read (int8: the row factor; bf16 inner
+// product: nothing); the bf16 L2 / cosine keys need the row norms in-kernel
+constexpr bool x1_has_dump(int mode, int el) { return el == FILTER_I8 || mode == MODE_IP; }
 
 __device__ __forceinline__ unsigned long long stamp_now() {
   unsigned long long t;
@@ -167,8 +99,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   __builtin_amdgcn_sched_barrier(0);
   return t;
-}               // rows (and queries) per tile
-constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
+}
 
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 __device__ __forceinline__ i32x4 as_i4(const uint4& u) { return __builtin_bit_cast(i32x4, u); }
@@ -213,6 +144,18 @@ __device__ __forceinline__ int tile_perm(int t) {
   return (int)(((uint32_t)t * 2654435761u) >> 24) & 0xFC;
 }
 
+// Row of value r (0..15) of the lane's 32-row block rb in tile t: slot
+// 128 wr + 32 rb + 8 jj + 4 h + e (jj = r >> 2, e = r & 3) holds row
+// t kT + (slot ^ f); the slot's fields are disjoint bits, so the XOR splits
+// into a uniform part (wr, rb, jj) and one lane part (h), and f leaves the low
+// two bits (e).  The list epilogue's rowof is the same formula with its
+// uniform parts hoisted; x1_replay uses this one.
+__device__ __forceinline__ int x1_row(int t, int wr, int rb, int h, int r) {
+  const int f = tile_perm(t);
+  return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * (r >> 2)) ^ (f & 0x18)) +
+         ((4 * h) ^ (f & 0x04)) + (r & 3);
+}
+
 __device__ __forceinline__ int sel16i(const i32x16& v, int i) {
   int r = v[0];
 #pragma unroll
@@ -247,6 +190,17 @@ __device__ __forceinline__ float sel16(const f32x16& v, int i) {
   return r;
 }
 
+// The approximate key of a row from its raw sum (int8: the exact int32 sum
+// times the two factors, three fp32 roundings, five with the cosine's folded
+// inverse norms — xs holds s_x (IP) or s_x / |x| (COS), qsc s_q or s_q / |q|;
+// bf16 inner product: -sum exactly).  One expression for the list epilogue and
+// the replay, so both produce the same bits.
+template <int EL>
+__device__ __forceinline__ float x1_key(int sum_bits, float qsc, float fx) {
+  if constexpr (EL == FILTER_I8) return -((float)sum_bits * (qsc * fx));
+  else return -__int_as_float(sum_bits);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -270,6 +224,9 @@ __device__ __forceinline__ float sel16(const f32x16& v, int i) {
 // group.  The first sub-step of every tile multiplies into a zero accumulator
 // (the MFMA's inline-constant C), so no register clearing between tiles.  Load
 // and position cursors are incremental (no divisions in the loop).
+// A dump launch's stores (rare: a block below the cut) are vector-memory
+// operations younger than the DMA pieces in flight: a counted wait after them
+// retires more than its step needs (over-waits), never less.
 //
 // XCD blocking (grids of 8 S workgroups; workgroup b runs on XCD b % 8, in slot
 // order b / 8 there): the S workgroups of an XCD take QG query tiles x DG
@@ -277,21 +234,21 @@ __device__ __forceinline__ float sel16(const f32x16& v, int i) {
 // slices (QG x 16 KB per step) and serves a database tile to QG workgroups;
 // slot / QG orders the splits, so with two rounds of workgroups per CU each
 // round covers its own DG / 2 splits.  Other grids: a plain dealing.
-template <int KR, int MODE, int NBUF, int EL>
+template <int KR, int MODE, bool DUMP, int EL>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ XH, const float* __restrict__ xs, const float* __restrict__ xaux,
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
     int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
     int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax,
-    const float* __restrict__ qcut) {
+    const float* __restrict__ qcut, int* __restrict__ dcount, int* __restrict__ dsum,
+    int* __restrict__ dtag, int dR) {
+  static_assert(!DUMP || x1_has_dump(MODE, EL), "dump form");
+  constexpr int NBUF = kNbuf;
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
-  // steps in flight (the round-2 schedule with split DMA keeps one fewer)
-  constexpr int D = (VS_X1_DMASPLIT && x1_sched(EL) == 1) ? NBUF - 2 : NBUF - 1;
-  constexpr bool kSide = x1_side(EL);
-  constexpr int kSideB = kSide ? kSideSlots * kSideSlotB : 0;
-  static_assert(NBUF * 2 * kStepB + kSideB <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB + kSideB];
+  constexpr int D = NBUF - 1;      // steps in flight
+  static_assert(NBUF * 2 * kStepB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * kStepB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -328,9 +285,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
 
   int gq[2], selfrow[2];
-  float tq[2];
-  // a list's admission limit: its last entry, or the query's cut when lower
-#define VS_X1_LIM(qb) (x1_has_qcut(MODE, EL) ? fminf(lk[qb][KR - 1], tq[qb]) : lk[qb][KR - 1])
   float qa[2], qsc[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -341,50 +295,47 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     qsc[qb] = 0.0f;
     if constexpr (EL == FILTER_I8) qsc[qb] = gq[qb] < nqa ? qs[gq[qb]] : 0.0f;
     selfrow[qb] = qrow ? (gq[qb] < nqa ? qrow[gq[qb]] : -1) : self0 >= 0 ? (int)(self0 + gq[qb]) : -1;
-    // the query's cut (x1_qcut): rows with keys at or above it are dropped
-    // (not on the bf16 L2 / cosine kernels: no register left; x1_has_qcut)
-    tq[qb] = x1_has_qcut(MODE, EL) && qcut && gq[qb] < nqa ? qcut[gq[qb]] : FLT_MAX;
   }
   const int P = nsplit * 4;
   const int pl = sp * 4 + wr * 2 + h;
-  float lk[2][KR];
-  int li[2][KR];
+  // List launches: the lane's sorted lists (admission limit: the last entry).
+  // Dump launches: the query's cut (padding queries: nothing passes) and the
+  // lane list's running dump count over the search's launches.
+  constexpr int KL = DUMP ? 1 : KR;  // dump launches keep no list (1: a dummy)
+  float lk[2][KL];
+  int li[2][KL];
+  float tq[2];
+  int dc[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
-    if (chunk == 0) {
-      list_init<KR, int>(lk[qb], li[qb]);
+    if constexpr (DUMP) {
+      tq[qb] = gq[qb] < nqa ? qcut[gq[qb]] : -FLT_MAX;
+      dc[qb] = dcount[(int64_t)gq[qb] * P + pl];
+      asm volatile("" ::"v"(tq[qb]), "v"(dc[qb]));
     } else {
+      const int64_t o = ((int64_t)gq[qb] * P + pl) * KP;
+      if (chunk == 0) {
+        list_init<KR, int>(lk[qb], li[qb]);
+      } else {
 #pragma unroll
-      for (int e = 0; e < KR; ++e) {
-        lk[qb][e] = pkey[o + e];
-        li[qb][e] = pid[o + e];
+        for (int e = 0; e < KR; ++e) {
+          lk[qb][e] = pkey[o + e];
+          li[qb][e] = pid[o + e];
+        }
       }
+#pragma unroll
+      for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
     }
-  }
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-#pragma unroll
-    for (int e = 0; e < KR; ++e) asm volatile("" ::"v"(lk[qb][e]), "v"(li[qb][e]));
     asm volatile("" ::"v"(qa[qb]));
     if constexpr (EL == FILTER_I8) asm volatile("" ::"v"(qsc[qb]));
-    if constexpr (x1_has_qcut(MODE, EL)) asm volatile("" ::"v"(tq[qb]));
   }
+  // a block's admission limit: the list's last entry, or the cut
+  auto lim = [&](int qb) -> float {
+    if constexpr (DUMP) return tq[qb];
+    else return lk[qb][KL - 1];
+  };
 
   if (t1 > t0) {  // uniform over the workgroup
-#if VS_X1_XGCHUNK
-    // A/B variant: one factor bound for the whole chunk (its tiles' group maxima)
-    float xgc = 0.0f;
-    if constexpr (EL == FILTER_I8) {
-      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      const int n = (t1 - t0) * (kT / 16);
-      const float* g = xgmax + (int64_t)t0 * (kT / 16);
-      for (int i = ln; i < n; i += 64) xgc = fmaxf(xgc, g[i]);
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) xgc = fmaxf(xgc, __shfl_xor(xgc, m));
-      xgc = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, xgc)));
-    }
-#endif
     // Planes are tile-major (vs_internal.h plane_offset): the 64-B step s of
     // the 256 rows of tile t is one contiguous 16-KB block, so a DMA piece (16
     // rows x 64 B) reads 1 KB of consecutive bytes — eight whole 128-B lines,
@@ -421,19 +372,19 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       const int co = ((2 * s2 + h) ^ fsw) * 16;
       const char* cX = base + (128 * wr + c32) * 64 + co;
       const char* cQ = base + kStepB + (64 * wq + c32) * 64 + co;
-#if !VS_X1_P_NOLDS
-      fb[0] = *(const uint4*)cQ;
-      fb[1] = *(const uint4*)(cQ + 32 * 64);
+      if constexpr (!VS_X1_P(2)) {
+        fb[0] = *(const uint4*)cQ;
+        fb[1] = *(const uint4*)(cQ + 32 * 64);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
-#else
-      auto opq = [](uint4& u) { asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w)); };
-      asm volatile("" ::"v"(cX), "v"(cQ));
-      opq(fb[0]);
-      opq(fb[1]);
+        for (int rb = 0; rb < 4; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
+      } else {
+        auto opq = [](uint4& u) { asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w)); };
+        asm volatile("" ::"v"(cX), "v"(cQ));
+        opq(fb[0]);
+        opq(fb[1]);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) opq(fa[rb]);
-#endif
+        for (int rb = 0; rb < 4; ++rb) opq(fa[rb]);
+      }
     };
     auto mfma_rb = [&](int rb, const uint4 (&fa)[4], const uint4 (&fb)[2]) {
       acc[rb][0] = mfma_blk<EL>(fa[rb], fb[0], acc[rb][0]);
@@ -453,32 +404,17 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                           (uint32_t)((32 * w + 16 * (i >> 1)) ^ xhi) * 64u;
       const char* qbase = qtile + (int64_t)lk_ * kStepB + (uint32_t)(16 * (i >> 1)) * 64u;
       const uint32_t lx = lds0 + (uint32_t)lbuf * (2 * kStepB) + (uint32_t)(2 * w) * 1024u;
-#if !VS_X1_P_NODMA
-      if constexpr (kSide) {
-        // the tile's factors with its first step, before the step's pieces (so
-        // every counted wait that retires the step retires them too; a younger
-        // side piece only makes a count wait for one piece more)
-        if (i == 0 && lk_ == 0) {  // uniform
-          const uint32_t sl = lds0 + (uint32_t)(NBUF * 2 * kStepB) +
-                              (uint32_t)((lt & (kSideSlots - 1)) * kSideSlotB);
-          if (lane < 8)
-            glds16(xs + (int64_t)lt * kT + 32 * w, (uint32_t)lane * 16u,
-                   __builtin_amdgcn_readfirstlane(sl + 128u * (uint32_t)w));
-          if (w == 0 && lane < 4)  // uniform w
-            glds16(xgmax + (int64_t)lt * (kT / 16), (uint32_t)lane * 16u,
-                   __builtin_amdgcn_readfirstlane(sl + (uint32_t)(kT * 4)));
+      if constexpr (!VS_X1_P(1)) {
+        if ((i & 1) == 0) {
+          if constexpr (!VS_X1_P(16))
+            glds16(xbase, xlane, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
+        } else {
+          if constexpr (!VS_X1_P(32))
+            glds16(qbase, soff, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
         }
-      }
-      if ((i & 1) == 0) {
-        if (!(VS_X1_P_NODMA_X))
-          glds16(xbase, xlane, __builtin_amdgcn_readfirstlane(lx + (i >> 1) * 1024u));
       } else {
-        if (!(VS_X1_P_NODMA_Q))
-          glds16(qbase, soff, __builtin_amdgcn_readfirstlane(lx + kStepB + (i >> 1) * 1024u));
+        asm volatile("" ::"v"(xlane), "v"(soff), "s"(xbase), "s"(qbase), "s"(lx));
       }
-#else
-      asm volatile("" ::"v"(xlane), "v"(soff), "s"(xbase), "s"(qbase), "s"(lx));
-#endif
     };
     auto advance_cursor = [&]() {
       if (ls + 1 < nsteps) {
@@ -504,32 +440,22 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // uniform: every row of the tile exists and none is excluded
       const bool plain = self0 < 0 && !qrow && (t + 1) * kT <= ntotal;
       const int f = tile_perm(t);
-      // slot 128 wr + 32 rb + 8 jj + 4 h + e holds row t kT + (slot ^ f) + e; the
-      // slot's fields are disjoint bits, so the XOR splits into a uniform part
-      // (wr, rb, jj) and one lane part (h), and f leaves the low two bits (e)
       const int fh = (4 * h) ^ (f & 0x04);
+      // x1_row with the uniform parts hoisted
       auto rowof = [&](int rb, int jj) {
         return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh;
       };
-      // side slots: the factors of the lane's rows (rb, jj, 0..3) of tile t
-      const char* sb = smem + NBUF * 2 * kStepB + (t & (kSideSlots - 1)) * kSideSlotB;
-      auto side_f4 = [&](int rb, int jj) {
-        return *(const f32x4*)(sb + 4 * (((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh));
-      };
-      // Phase 1: the candidate rows of every (rb, qb) block, a 16-bit mask per
-      // lane, against each list's last entry before any insertion of this
-      // tile (the last entry only tightens, so the masks are a superset).
+      // Phase 1: the candidate rows of every (rb, qb) block, one bit per block,
+      // against each block's limit before any insertion of this tile (a list's
+      // last entry only tightens, so the bits are a superset).
       //  * int8: a row's score fl(fl(float(sum)) * fl(f_q * f_x)) is monotone
       //    in the sum and in f_x (factors >= 0), so with the lane's largest
       //    factor over its 16 rows (xgmax: the maximum per 32-row group and
-      //    bit 2 of the row, a SCALAR load) a row can beat the list only if
+      //    bit 2 of the row, a SCALAR load) a row can beat the limit only if
       //    its int32 sum exceeds one integer threshold per block (i8_threshold):
-      //    16 integer compares, no conversion;
-      //  * bf16 inner product: the key is -sum, exactly: 16 float compares;
+      //    a maximum and one compare;
+      //  * bf16 inner product: the key is -sum, exactly: a maximum and a compare;
       //  * bf16 L2 / cosine: every row (the key needs the row's norm).
-      // pass: bit 2 rb + qb set when the block may hold a candidate (phase 1
-      // is per block: a maximum and one compare; the 16-row masks are built
-      // in phase 3 for the blocks that pass only)
       uint32_t pass = 0;
       float fmx[4];  // int8: the lane's factor bound per row block
 #if VS_X1_STAMP
@@ -538,17 +464,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         fmx[rb] = 0.0f;
-        if constexpr (kSide) {  // the group maximum of the lane's 16 rows
-          const int g = ((128 * wr + 32 * rb) ^ (f & 0xE0)) >> 5;
-          fmx[rb] = *(const float*)(sb + kT * 4 + 4 * (2 * g + ((fh >> 2) & 1)));
-        } else if constexpr (EL == FILTER_I8) {
-#if VS_X1_XGCHUNK
-          fmx[rb] = xgc;
-#else
+        if constexpr (EL == FILTER_I8) {
           const int grp = (t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0))) >> 5;  // uniform
           const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
           fmx[rb] = (fh & 4) ? g1 : g0;
-#endif
         }
       }
 #if VS_X1_STAMP
@@ -562,7 +481,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int rb = 0; rb < 4; ++rb) {
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
-          const float last = VS_X1_LIM(qb);
+          const float last = lim(qb);
           bool p;
           if constexpr (EL == FILTER_I8) {
             const float c = qsc[qb] * fmx[rb];
@@ -586,10 +505,36 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         }
       }
       VS_X1_EMARK(6);
-#if VS_X1_P_NOCAND
-      asm volatile("" ::"v"(pass));
-      pass = 0;
-#endif
+      if constexpr (VS_X1_P(128)) {
+        asm volatile("" ::"v"(pass));
+        pass = 0;
+      }
+      if constexpr (DUMP) {
+        // Dump launch: the lane's 16 raw sums of every block that passed, with
+        // the block's (tile, row block), to the lane list's next slot; a list
+        // past its dR slots counts on (the replay fails its query).
+        if (__ballot(pass != 0) == 0) return;  // uniform: the usual case
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+            if (pass & (1u << (2 * rb + qb))) {
+              const int c = dc[qb]++;
+              if (c < dR) {
+                const int64_t slot = ((int64_t)gq[qb] * P + pl) * dR + c;
+                i32x4* d = (i32x4*)(dsum + slot * 16);
+                const i32x16 v = __builtin_bit_cast(i32x16, acc[rb][qb]);
+                d[0] = i32x4{v[0], v[1], v[2], v[3]};
+                d[1] = i32x4{v[4], v[5], v[6], v[7]};
+                d[2] = i32x4{v[8], v[9], v[10], v[11]};
+                d[3] = i32x4{v[12], v[13], v[14], v[15]};
+                dtag[slot] = t * 4 + rb;
+              }
+            }
+          }
+        }
+        VS_X1_EMARK(8);
+      } else {
       // Phases 2 and 3 per half tile (rb pair): the per-row values (int8
       // factors; bf16 L2 / cosine norms) of the lane's 32 rows, when any lane of
       // the wave has a candidate in the pair — eight 16-B loads in ONE asm
@@ -617,12 +562,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
           for (int jj = 0; jj < 4; ++jj) rv[r2][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
         const uint32_t any = (pass >> (2 * G * hp)) & ((1u << (2 * G)) - 1u);
         if (__ballot(any != 0) == 0) continue;  // uniform
-        if constexpr (kSide) {
-#pragma unroll
-          for (int r2 = 0; r2 < G; ++r2)
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) rv[r2][jj] = side_f4(G * hp + r2, jj);
-        } else if constexpr (kRows) {
+        if constexpr (kRows) {
           const float* src = EL == FILTER_I8 ? xs : xaux;
           if constexpr (G == 2) {
             const float* a[8];
@@ -672,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   key[jj * 4 + e] = MODE == MODE_L2 ? l2_from_ip(qa[qb], rv[r2][jj][e], v)
                                                     : -(v * (qa[qb] * rv[r2][jj][e]));
                 }
-              const float last = VS_X1_LIM(qb);
+              const float last = lim(qb);
               cm = 0;
 #pragma unroll
               for (int r = 0; r < 16; ++r) cm |= (uint32_t)(key[r] < last) << r;
@@ -687,46 +627,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 const int bi = __builtin_ctz(cm);
                 cm &= cm - 1;
                 const int row = rowof(rb, bi >> 2) + (bi & 3);
-                VS_X1_INSERT<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
+                list_insert<KR, int>(lk[qb], li[qb], sel16(key, bi), row);
               }
             } else {
               // the block's candidate rows (int8: sum above the block's integer
               // threshold; bf16: -sum below the last entry), then one at a time:
               // the exact key of the row and its admission
-              const float last = VS_X1_LIM(qb);
-#if VS_X1_ROWLOOP
-              // A/B variant: one uniform pass over the block's 16 rows (the row
-              // index in a scalar register: the sum and the factor are indexed
-              // reads, no per-lane selects), a row skipped when no lane has it
-              int T = INT_MIN;
-              if constexpr (EL == FILTER_I8) {
-                const float c = qsc[qb] * fmx[rb];
-                T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
-              }
-#pragma unroll 1
-              for (int r = 0; r < 16; ++r) {
-                bool cand;
-                if constexpr (EL == FILTER_I8) cand = acc[rb][qb][r] > T;
-                else cand = -acc[rb][qb][r] < last;
-                if (__ballot(cand) == 0) continue;  // uniform
-                if (cand) {
-                  const int row = rowof(rb, r >> 2) + (r & 3);
-                  float key;
-                  if constexpr (EL == FILTER_I8) {
-                    f32x16 rvv;
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) rvv[j] = rv[r2][j >> 2][j & 3];
-                    key = -((float)acc[rb][qb][r] * (qsc[qb] * rvv[r]));
-                  }
-                  else
-                    key = -acc[rb][qb][r];
-                  const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
-                                  key < VS_X1_LIM(qb);
-                  if (ok) VS_X1_INSERT<KR, int>(lk[qb], li[qb], key, row);
-                }
-              }
-              continue;
-#endif
+              const float last = lim(qb);
               if constexpr (EL == FILTER_I8) {
                 const float c = qsc[qb] * fmx[rb];
                 const int T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
@@ -741,26 +648,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                 cm &= cm - 1;
                 const int row = rowof(rb, bi >> 2) + (bi & 3);
                 float key;
-                if constexpr (EL == FILTER_I8) {
-                  // the exact int32 sum times the two factors (three fp32
-                  // roundings, five with the cosine's folded inverse norms); xs
-                  // holds s_x (IP) or s_x / |x| (COS), qsc s_q or s_q / |q|
-                  key = -((float)sel16i(acc[rb][qb], bi) * (qsc[qb] * sel4x4(rv[r2], bi)));
-                } else {
+                if constexpr (EL == FILTER_I8)
+                  key = x1_key<EL>(sel16i(acc[rb][qb], bi), qsc[qb], sel4x4(rv[r2], bi));
+                else
                   key = -sel16(acc[rb][qb], bi);
-                }
-                const bool ok = (plain || (row < ntotal && row != selfrow[qb])) &&
-                                key < VS_X1_LIM(qb);
-                if (ok) VS_X1_INSERT<KR, int>(lk[qb], li[qb], key, row);
+                const bool ok = (plain || (row < ntotal && row != selfrow[qb])) && key < lim(qb);
+                if (ok) list_insert<KR, int>(lk[qb], li[qb], key, row);
               }
             }
           }
         }
         VS_X1_EMARK(8);
       }
+      }
     };
 
-    if ((VS_X1_PRIO == 1 && w >= 4) || (VS_X1_PRIO == 2 && w < 4)) __builtin_amdgcn_s_setprio(1);
     constexpr int kSched = x1_sched(EL);
     if constexpr (kSched == 1) {
 
@@ -771,10 +673,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int j = 0; j < 4; ++j) stage_piece(j);
       advance_cursor();
     }
-    // step 0 of the D in flight
-    if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // step 0 of the D in flight
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd(0, 0, fa0, fb0);
@@ -782,14 +681,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // The instruction order inside a step is pinned with sched_barrier(0): hipcc
     // would otherwise move the MFMAs across the barrier and the fragment reads
     // next to their first use, undoing the half-step lookahead.
-    // Stagger (VS_X1_STAGGER): waves 4-7 take the step's barrier at its start
-    // instead of its middle, so they run half a step behind their SIMD
-    // partners (the LDS-DMA issue of one wave beside the other's MFMAs).
-    // Every condition above still holds for them: they retire DMA(s+1) before
-    // barrier s and read image s+1 only after it, and their last reads of
-    // image s-1 are consumed before barrier s, after which DMA(s+D) may
-    // overwrite it.
-    const bool lag = VS_X1_STAGGER && w >= 4;
+    // Stagger: waves 4-7 take the step's barrier at its start instead of its
+    // middle, so they run half a step behind their SIMD partners (the LDS-DMA
+    // issue of one wave beside the other's MFMAs).  Every condition above
+    // still holds for them: they retire DMA(s+1) before barrier s and read
+    // image s+1 only after it, and their last reads of image s-1 are consumed
+    // before barrier s, after which DMA(s+D) may overwrite it.
+    const bool lag = w >= 4;
 #if VS_X1_STAMP
     tA = stamp_now();
 #define VS_X1_MARK1(i) (tB = stamp_now(), sg[i] += tB - tA, tA = tB)
@@ -801,11 +699,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // this wave's pieces of step s+1: the steps s+2 .. s+D-1 stay in flight
       // (the lagging waves wait before this step's first pieces, the others
       // after them)
-      constexpr int kSplit = VS_X1_DMASPLIT ? 2 : 0;  // pieces in the first half
       if (lag) {  // uniform
-        if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -829,25 +724,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         mfma_rb(3, fa0, fb0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (kSplit) {  // into the image of step s-2 (see above)
-        stage_piece(0);
-        __builtin_amdgcn_sched_barrier(0);
-        stage_piece(1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
       VS_X1_MARK1(0);
       // retire step s+1 (this wave's pieces); the younger D-2 steps stay in flight
       if (!lag) {  // uniform
-#if !VS_X1_P_NOWAIT
-        if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if constexpr (D == 3 && kSplit) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if constexpr (kSplit) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#if !VS_X1_P_NOBAR
-        __builtin_amdgcn_s_barrier();
-#endif
+        if constexpr (!VS_X1_P(64)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if constexpr (!VS_X1_P(4)) __builtin_amdgcn_s_barrier();
       }
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK1(1);
@@ -860,21 +741,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       for (int i = 0; i < 4; ++i) {
         mfma_rb(i, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
-        if (i >= kSplit) stage_piece(i);  // compile-time
+        stage_piece(i);
         __builtin_amdgcn_sched_barrier(0);
       }
       advance_cursor();
       VS_X1_MARK1(3);
       if (++ks == nksteps) {
         ks = 0;
-#if !VS_X1_P_NOEPI
-        epilogue(t);
-#else
+        if constexpr (!VS_X1_P(8)) {
+          epilogue(t);
+        } else {
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+          for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
-#endif
+            for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+        }
         ++t;
       }
       VS_X1_MARK1(5);
@@ -904,7 +785,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     }
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step 0
     __builtin_amdgcn_s_barrier();
-    const bool lag = VS_X1_STAGGER && w >= 4;
+    const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
     int buf = 0, t = t0, ks = 0;
 #if VS_X1_STAMP
@@ -914,44 +795,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #define VS_X1_MARK(i) ((void)0)
 #endif
     for (int s = 0; s < nsteps; ++s) {
-      if constexpr (kSched == 3) {
-      // half-step segments (VS_X1_SCHED=3): sub-step 0 reads + 2 pieces |
-      // its 8 MFMAs | sub-step 1 reads + 2 pieces + the wait for step s+1 |
-      // its 8 MFMAs, four barriers per step (the 8-phase template's finer
-      // interleave); the same images, distances and counted wait as above
-      __builtin_amdgcn_sched_barrier(0);
-      rd(buf, 0, fa0, fb0);
-      __builtin_amdgcn_sched_barrier(0);
-      stage_piece(0);
-      stage_piece(1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, fb0);
-      } else {
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa0, fb0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      rd(buf, 1, fa1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      stage_piece(2);
-      stage_piece(3);
-      advance_cursor();
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step s+1
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      } else {
       __builtin_amdgcn_sched_barrier(0);
       rd(buf, 0, fa0, fb0);
       rd(buf, 1, fa1, fb1);
@@ -981,23 +824,22 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(4);
-      }
       if (++ks == nksteps) {  // beside the partner's matrix segment
         ks = 0;
-#if !VS_X1_P_NOEPI
-        epilogue(t);
-#else
+        if constexpr (!VS_X1_P(8)) {
+          epilogue(t);
+        } else {
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+          for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
-#endif
+            for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+        }
         ++t;
       }
       VS_X1_MARK(5);
       buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
-    if (!lag && VS_X1_STAGGER) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
+    if (!lag) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
 #undef VS_X1_MARK
     }
 #if VS_X1_STAMP
@@ -1022,16 +864,90 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   const int pl0 = sp * 4 + wr * 2 + (ln >> 5);
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const int64_t o = ((int64_t)(qt * kT + 64 * wq + 32 * qb + (ln & 31)) * P + pl0) * KP;
+    const int64_t g = (int64_t)(qt * kT + 64 * wq + 32 * qb + (ln & 31)) * P + pl0;
+    if constexpr (DUMP) {
+      dcount[g] = dc[qb];
+    } else {
+      const int64_t o = g * KP;
 #pragma unroll
-    for (int e = 0; e < KR; ++e) {
-      pkey[o + e] = lk[qb][e];
-      pid[o + e] = li[qb][e];
+      for (int e = 0; e < KR; ++e) {
+        pkey[o + e] = lk[qb][e];
+        pid[o + e] = li[qb][e];
+      }
+      for (int e = KR; e < KP; ++e) {
+        pkey[o + e] = FLT_MAX;
+        pid[o + e] = -1;
+      }
     }
-    for (int e = KR; e < KP; ++e) {
-      pkey[o + e] = FLT_MAX;
-      pid[o + e] = -1;
+  }
+}
+
+// The replay of a pass's dumps (after its last dump launch): one thread per
+// lane list (query q, list pl = 4 sp + 2 wr + h).  The list as the first
+// launch left it, then every dumped block in dump order (the order the lane
+// met them: tiles ascending, launch after launch), each of its 16 rows with
+// the key the list epilogue computes (x1_key, the same expression) and the
+// same admission: key < min(last entry, cut), the row inside the corpus and not
+// the query's own.  A list with more dumps than slots lost some: its query's
+// cut becomes -FLT_MAX, which fails both checks of the verification (the query
+// goes to the next stage).
+template <int KR, int EL>
+__global__ __launch_bounds__(256) void x1_replay_kernel(
+    const int* __restrict__ dcount, const int* __restrict__ dsum, const int* __restrict__ dtag,
+    float* __restrict__ pkey, int* __restrict__ pid, int P, int KP, int nqa,
+    const float* __restrict__ qs, const float* __restrict__ xs, int64_t self0, int ntotal,
+    int dR, float* __restrict__ qcut, unsigned long long* __restrict__ stats) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cnt = i < (int64_t)nqa * P ? dcount[i] : 0;
+  {  // statistics: one atomic per wave
+    unsigned long long a = (unsigned long long)cnt, b = cnt > dR ? 1ull : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o);
+      b += __shfl_xor(b, o);
     }
+    if ((threadIdx.x & 63) == 0 && a) {
+      atomicAdd(stats, a);
+      if (b) atomicAdd(stats + 1, b);
+    }
+  }
+  if (cnt == 0) return;
+  const int q = (int)(i / P), pl = (int)(i % P);
+  if (cnt > dR) {
+    qcut[q] = -FLT_MAX;
+    return;
+  }
+  const float cut = qcut[q];
+  const float qsc = EL == FILTER_I8 ? qs[q] : 0.0f;
+  const int wr = (pl >> 1) & 1, h = pl & 1;
+  const int selfrow = self0 >= 0 ? (int)(self0 + q) : -1;
+  float lk[KR];
+  int li[KR];
+  const int64_t o = i * KP;
+#pragma unroll
+  for (int e = 0; e < KR; ++e) {
+    lk[e] = pkey[o + e];
+    li[e] = pid[o + e];
+  }
+  for (int c = 0; c < cnt; ++c) {
+    const int64_t slot = i * dR + c;
+    const int tag = dtag[slot];
+    const int t = tag >> 2, rb = tag & 3;
+    const i32x4* src = (const i32x4*)(dsum + slot * 16);
+    const i32x4 v4[4] = {src[0], src[1], src[2], src[3]};
+    const bool plain = self0 < 0 && (t + 1) * kT <= ntotal;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = x1_row(t, wr, rb, h, r);
+      if (!(plain || (row < ntotal && row != selfrow))) continue;
+      const float fx = EL == FILTER_I8 ? xs[row] : 0.0f;
+      const float key = x1_key<EL>(v4[r >> 2][r & 3], qsc, fx);
+      if (key < fminf(lk[KR - 1], cut)) list_insert<KR, int>(lk, li, key, row);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < KR; ++e) {
+    pkey[o + e] = lk[e];
+    pid[o + e] = li[e];
   }
 }
 
@@ -1064,20 +980,35 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   const int qg = a.qcount ? nqt : x1_qg();
   // a gathered later stage (usually empty: its tiles exit at once) is one launch
   int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
-  const bool cut = a.qcut && x1_has_qcut(MODE, EL) && !a.qcount && a.qbkey && a.qcut_m > 0;
-  // with a cut, at least two launches when the splits are long enough (the
-  // second runs under the cut the first one's lists give)
-  if (cut && nchunk == 1 && per_block >= 16) nchunk = 2;
+  // Dump launches after the first: its lists set the cuts (x1_qcut), the rest
+  // of the pass stores only the blocks below them, and x1_replay (called by the
+  // host after this function returns, outside the pass's timer) folds the dumps
+  // into the lists.  At most 1/8 of a split in the first launch when the
+  // splits are long enough (C2: 31 tiles -> 3 launches, C4: 122 -> 8).
+  const bool dump = a.dump && x1_has_dump(MODE, EL) && !a.qcount && a.qcut && a.qbkey &&
+                    a.qcut_m > 0 && a.dcount && a.dsum && a.dtag && a.dR > 0;
+  if (dump) nchunk = std::max(nchunk, std::min(8, per_block / 8));
+  const bool dumping = dump && nchunk > 1;
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
-    hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, x1_nbuf(EL), EL>), dim3(nqt * a.nsplit), dim3(512), 0, st,
-                       (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux, a.nqa,
-                       (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0, a.self0, a.qrow,
-                       a.qcount, c, nchunk, part.KP, qg, part.key, part.id, a.xgmax, a.qcut);
+    if (dumping && c > 0) {
+      if constexpr (x1_has_dump(MODE, EL))
+        hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, true, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
+                           st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
+                           a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
+                           a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
+                           a.xgmax, a.qcut, a.dcount, a.dsum, a.dtag, a.dR);
+    } else {
+      hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
+                         st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
+                         a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
+                         a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
+                         a.xgmax, nullptr, nullptr, nullptr, nullptr, 0);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (cut && c + 1 < nchunk) {
+    if (dumping && c == 0) {
       e = launch_qcut(a, part, st);
       if (e != hipSuccess) return e;
     }
@@ -1087,6 +1018,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
 }
 
 int x1_lane_len() { return 8; }
+int x1_dump_slots() { return kDumpMaxR; }
 
 hipError_t x1_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_stamps), sizeof(g_x1_stamps));
@@ -1127,6 +1059,27 @@ hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStre
     return x1_dispatch<FILTER_I8>(mode, a, part, st, ndispatch);
   }
   return x1_dispatch<FILTER_BF16>(mode, a, part, st, ndispatch);
+}
+
+bool x1_dump_applies(int mode, int filter) { return x1_has_dump(mode, filter); }
+
+// The replay of launch_gemm_topk_x1's dumps (a no-op when the pass had none to
+// make: the counts stay zero).
+hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st,
+                            unsigned long long* stats) {
+  if (!a.dump || !a.dcount || a.nqa <= 0) return hipSuccess;
+  if (part.KP < x1_lane_len()) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)a.nqa * part.P;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (a.filter == FILTER_I8)
+    hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_I8>), grid, dim3(256), 0, st, a.dcount, a.dsum,
+                       a.dtag, part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs, a.self0,
+                       a.ntotal, a.dR, a.qcut, stats);
+  else
+    hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_BF16>), grid, dim3(256), 0, st, a.dcount,
+                       a.dsum, a.dtag, part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs,
+                       a.self0, a.ntotal, a.dR, a.qcut, stats);
+  return hipGetLastError();
 }
 
 // Filter-pass candidate count: the merged approximate candidates for `need`
@@ -1944,16 +1897,18 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
 // T' = min(T, a_M + 2.000001 B, ...) (wide check) or passes iff T - B > E_M with
 // E_M <= a_M + B (first check).  Every row with approximate key >= a_M + 2 B
 // is therefore useless to both, and a_M, the M-th smallest key over a query's
-// lane lists, only falls while the pass runs.  Between two launches of the
-// filter pass, x1_qcut sets cut[q] = min(cut[q], a_M(now) + 2.000001 B) (rounded
-// up); the next launches drop every row whose key is not below the cut (the
-// kernel's admission limit becomes min(list last, cut)), and the verification
-// takes T = min(T, cut) as the floor of the rows dropped that way.  Since the
-// final a_M <= a_M(now), the cut is never below the verification's own
-// a_M + 2B: no check changes its outcome, and the lists only lose rows that
+// lane lists, only falls while the pass runs.  After the first launch of a
+// pass, x1_qcut sets cut[q] = min(cut[q], a_M(now) + 2.000001 B) (rounded up);
+// the dump launches that follow keep only the blocks that may hold a row below
+// the cut, x1_replay admits their rows against min(list last, cut), and the
+// verification takes T = min(T, cut) as the floor of the rows dropped that way.
+// Since the final a_M <= a_M(now), the cut is never below the verification's
+// own a_M + 2B: no check changes its outcome, and the lists only lose rows that
 // could never enter the rescored set.  What it saves: a lane list admits rows
 // against its own 8th entry (the 8th best of a 1/128 slice of the corpus at C3);
-// the cut is the M-th best over all of them plus 2B.
+// the cut is the M-th best over all of them plus 2B, so a dump launch finds a
+// block below it only for ~1 in 40 (lane, block) pairs — rare enough that a
+// wave almost never waits on one (tests/test_filter_argument.py models it).
 
 // bkey[q]: the bound B of query q (bound_key over its split norms, the same
 // double the verification computes).
@@ -2058,7 +2013,6 @@ static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st) {
   return hipGetLastError();
 }
 
-bool x1_qcut_applies(int mode, int filter) { return x1_has_qcut(mode, filter); }
 
 BoundArgs make_bound_args(int64_t ld, int filter) {
   BoundArgs ba;

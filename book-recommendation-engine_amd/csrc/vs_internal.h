@@ -101,9 +101,16 @@ struct X1Args {
   const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
   const float* xgmax = nullptr;  // int8: launch_group_max of xs (capacity rows)
-  float* qcut = nullptr;         // per query (nqa): the cut, updated between launches
+  // Dump launches (vs_gemm_x1.hip header): after the pass's first launch the
+  // cuts are set and the later launches store the blocks below them
+  bool dump = false;
+  float* qcut = nullptr;         // per query (nqa): the cut, set after the first launch
   const double* qbkey = nullptr; // per query: the verification's bound B (x1_qcut)
   int qcut_m = 0;                // the M of the verification
+  int* dcount = nullptr;         // [nq_pad][P] dumps per lane list (zeroed before the pass)
+  int* dsum = nullptr;           // [nq_pad][P][dR][16] raw sums of the dumped blocks
+  int* dtag = nullptr;           // [nq_pad][P][dR] tile * 4 + row block of each dump
+  int dR = 0;                    // dump slots per lane list
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
   const void* QH = nullptr;      // query plane, tile-major (self-join: the stored plane)
   int qtile0 = 0;                // QH's tile of query tile 0 (self-join: self0 / 256)
@@ -225,14 +232,19 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const float* xinv, const float* qsc, const float* Dk,
                               const int64_t* Ik, unsigned long long* sizes = nullptr,
                               const float* qcut = nullptr);
-// Query cuts of the filter pass (vs_gemm_x1.hip, "Query cuts"): bkey[q] = the
-// verification's bound B of query q; x1_qcut_applies: the pass kernel of this
-// mode and plane applies X1Args::qcut (launch_gemm_topk_x1 then updates the
-// cuts between its launches, and the verification must get the same array).
+// Query cuts and dump launches of the filter pass (vs_gemm_x1.hip, "Query
+// cuts"): bkey[q] = the verification's bound B of query q; x1_dump_applies:
+// the pass of this mode and plane has a dump form (launch_gemm_topk_x1 then
+// sets the cuts after its first launch and dumps in the others; the host runs
+// launch_x1_replay after it, and the verification must get the same cuts).
 hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, int filter,
                          const unsigned* stats, const float* qr2i8, int nq, double* bkey,
                          hipStream_t st);
-bool x1_qcut_applies(int mode, int filter);
+bool x1_dump_applies(int mode, int filter);
+int x1_dump_slots();  // the most dump slots per lane list worth allocating
+// stats[0] += dumps replayed, stats[1] += lane lists out of slots
+hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st,
+                            unsigned long long* stats);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
 // (key, label) order, the per-shard half of an exact sharded merge).  With

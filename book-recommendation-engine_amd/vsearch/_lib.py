@@ -80,6 +80,7 @@ SIGNATURES = {
     "vs_filter_wide_stats": (_c_int, [_i64p]),
     "vs_filter_second_stats": (_c_int, [_i64p]),
     "vs_filter_wide_sets": (_c_int, [_i64p, _i64p]),
+    "vs_filter_dump_stats": (_c_int, [_i64p, _i64p]),
 }
 
 _lock = threading.Lock()
@@ -224,3 +225,13 @@ def filter_second_stats() -> int:
     v = ctypes.c_int64(0)
     check(load().vs_filter_second_stats(ctypes.byref(v)))
     return v.value
+
+
+def filter_dump_stats():
+    """(dumps, overflows): blocks the filter pass's dump launches stored and
+    lane lists that ran out of dump slots (their queries went to the next
+    stage) since the last filter_stats reset (read them before that reset)."""
+    d = ctypes.c_int64(0)
+    o = ctypes.c_int64(0)
+    check(load().vs_filter_dump_stats(ctypes.byref(d), ctypes.byref(o)))
+    return d.value, o.value

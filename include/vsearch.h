@@ -222,6 +222,11 @@ int vs_filter_second_stats(int64_t* second);
  * were read from HBM and rescored (the rest reuse the first check's exact keys),
  * since the last vs_filter_stats reset.  Diagnostic only: no reference interface. */
 int vs_filter_wide_sets(int64_t* entries, int64_t* rescored);
+/* Blocks the filter pass's dump launches stored (a lane's 16 sums that may
+ * hold a row below its query's cut) and lane lists that ran out of dump slots
+ * (their queries went to the next stage), since the last vs_filter_stats
+ * reset.  Diagnostic only: no reference interface. */
+int vs_filter_dump_stats(int64_t* dumps, int64_t* overflows);
 int vs_timer_reset(void);
 /* Diagnostic only (no reference interface): the filter pass's per-segment
  * cycle sums of a stamp build (VS_X1_STAMP=1; zeros otherwise), 26 values:

@@ -1,0 +1,114 @@
+"""GPU: the filter pass's dump launches (vs_gemm_x1.hip header).
+
+A pass of an int8 or bf16 inner-product filter over splits of at least 16
+tiles runs its first launch as a list launch, sets each query's cut from those
+lists (x1_qcut), and runs the rest as dump launches whose blocks below the cut
+x1_replay folds into the lists.  The small parity tests never reach that
+length (their splits are a few tiles), so these searches are sized for it:
+4,096 queries (16 query tiles, 32 splits) over 300,000 rows (37 tiles per
+split: one list launch + three dump launches), checked STRICTLY against the
+fp64 oracle on 512 sampled queries (every query tile), with the dump counters
+showing that dump launches ran.  Also: lane lists that run out of dump slots
+(a block of 12,000 duplicated rows next to the queries: ~94 dumps per list >
+32 slots) hand their queries to the next stage and the answer stays exact;
+the bf16 plane's dump form; and the cosine self-join (C4's path)."""
+
+import numpy as np
+import pytest
+
+from oracle import flat
+
+pytestmark = pytest.mark.gpu
+
+IP = flat.METRIC_INNER_PRODUCT
+N, D_, B = 300_000, 128, 4096
+SAMPLE = np.array(sorted({q for t in range(16) for q in range(256 * t, 256 * t + 256, 8)}))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from vsearch import _lib
+
+    assert _lib.device_count() >= 1
+    return _lib
+
+
+def _search_checked(lib, xb, xq, k, engine="auto"):
+    from vsearch import faiss as vfaiss
+
+    index = vfaiss.IndexFlat(xb.shape[1], IP)
+    index.add(xb)
+    index.set_engine(engine)
+    lib.filter_stats(reset=True)
+    D, I = index.search(xq, k)
+    dumps, over = lib.filter_dump_stats()
+    fq, ff = lib.filter_stats(reset=True)
+    Dr, Ir = flat.knn_exact(xb, xq[SAMPLE], k, IP)
+    bad = flat.mismatches(D[SAMPLE], I[SAMPLE], Dr, Ir, IP, xb, xq[SAMPLE], strict=True)
+    assert not bad, bad[:5]
+    return dumps, over, fq, ff
+
+
+@pytest.mark.parametrize("k", [1, 10, 28])
+def test_dump_launches_uniform_rows(lib, k):
+    rng = np.random.default_rng(31 + k)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
+    dumps, over, fq, ff = _search_checked(lib, xb, xq, k)
+    assert fq == B
+    assert dumps > 0 and over == 0, (dumps, over)
+
+
+def test_dump_launches_clustered_unit_rows(lib):
+    """Embedding-like rows (unit norm, 64 centroids): the int8 cut sits close
+    to the top, the bf16 stage takes what int8 cannot settle."""
+    rng = np.random.default_rng(5)
+    c = rng.standard_normal((64, D_)).astype(np.float32)
+    xb = c[rng.integers(0, 64, N)] + 0.5 * rng.standard_normal((N, D_)).astype(np.float32)
+    xb /= np.linalg.norm(xb, axis=1, keepdims=True)
+    xq = c[rng.integers(0, 64, B)] + 0.5 * rng.standard_normal((B, D_)).astype(np.float32)
+    xq /= np.linalg.norm(xq, axis=1, keepdims=True)
+    dumps, over, fq, _ = _search_checked(lib, xb, xq, 10)
+    assert fq == B and dumps > 0
+
+
+def test_dump_slot_overflow_hands_queries_on(lib):
+    """12,000 copies of one row beside every query: each lane list meets ~94
+    blocks below the cut, more than its 32 slots; its query is failed by the
+    verification (cut = -FLT_MAX) and answered by the next stage — exactly."""
+    rng = np.random.default_rng(77)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    dup = rng.uniform(-1, 1, D_).astype(np.float32)
+    xb[rng.choice(N, 12_000, replace=False)] = dup
+    xq = (dup[None, :] + 0.3 * rng.uniform(-1, 1, (B, D_))).astype(np.float32)
+    dumps, over, fq, _ = _search_checked(lib, xb, xq, 10)
+    assert over > 0, (dumps, over)
+
+
+def test_dump_launches_bf16_plane(lib):
+    rng = np.random.default_rng(9)
+    xb = rng.standard_normal((N, D_)).astype(np.float32)
+    xq = rng.standard_normal((B, D_)).astype(np.float32)
+    dumps, over, fq, _ = _search_checked(lib, xb, xq, 10, engine="bf16v")
+    assert dumps > 0 and over == 0
+
+
+def test_dump_launches_cosine_selfjoin(lib):
+    """C4's path at reduced size: 300,000 students (65,536-student chunks, 32
+    splits of 37 tiles), cosine top-15 excluding self, strict on 256 rows."""
+    from vsearch import faiss as vfaiss
+
+    rng = np.random.default_rng(13)
+    x = rng.standard_normal((N, D_)).astype(np.float32)
+    index = vfaiss.IndexFlatIP(D_)
+    index.add(x)
+    lib.filter_stats(reset=True)
+    S, I = index.selfjoin(15)
+    dumps, over = lib.filter_dump_stats()
+    lib.filter_stats(reset=True)
+    assert dumps > 0 and over == 0
+    rows = np.array(sorted({r for c in range(0, N, 65536) for r in (c, c + 1, c + 65535)
+                            if r < N} | set(range(0, N, N // 200))))
+    Sr, Ir = flat.pgvector_cosine_topk(x, 15, q_rows=rows)
+    bad = flat.selfjoin_mismatches(S[rows], I[rows], Sr, Ir, x, rows, strict=True)
+    assert not bad, bad[:5]
