@@ -360,3 +360,48 @@ def test_query_cut_selection_is_the_mth_smallest_key():
             assert got is None
         else:
             assert got == v[M - 1]  # -0.0 == 0.0: the order image ranks -0 first
+
+
+def test_dump_and_replay_leave_the_lists_of_in_kernel_admission():
+    """The dump launches (vs_gemm_x1.hip header) restated: after the first
+    launch sets the cut, a lane stores a whole 16-row block whenever its block
+    test says a row may be below the cut (a superset: here the block's
+    smallest key), in the order it meets them, and x1_replay admits the
+    stored rows in that order against min(list last, cut).  The lists equal
+    those of admitting every row in-kernel against min(list last, cut), and a
+    list whose dumps exceed its slots is reported (its query is then failed)."""
+    rng = np.random.default_rng(11)
+    B, M, P, L, R = 1e-3, 19, 64, 8, 32
+    for trial in range(30):
+        n = 16 * 2048
+        a = (rng.standard_normal(n) * 0.01).astype(np.float64)
+        if trial % 4 == 0:  # near-duplicates: many rows just above the top
+            a[rng.choice(n, 400, replace=False)] = -0.04 + rng.uniform(0, B, 400)
+        owner = np.repeat(rng.integers(0, P, size=n // 16), 16)  # blocks of 16 rows
+        order = np.arange(n)
+        cut_at = n // 8
+        ref, cut, _ = _stream_lists(a, owner, P, L, order, cut_at, B, M, cut_at)
+        # the first launch as a list launch, then dumps + replay
+        first, _, _ = _stream_lists(a[:cut_at], owner[:cut_at], P, L, np.arange(cut_at),
+                                    None, B, M, cut_at)
+        lists = [list(lst) for lst in first]
+        dumps = [[] for _ in range(P)]
+        for b0 in range(cut_at, n, 16):
+            blk = np.arange(b0, b0 + 16)
+            if a[blk].min() < cut:  # the block test (a superset of rows below the cut)
+                dumps[owner[b0]].append(blk)
+        overflow = [len(d) > R for d in dumps]
+        for p in range(P):
+            if overflow[p]:
+                continue
+            lst = lists[p]
+            for blk in dumps[p]:
+                for r in blk:
+                    lim = a[lst[-1]] if len(lst) == L else np.inf
+                    if a[r] < min(lim, cut):
+                        lst.append(r)
+                        lst.sort(key=lambda x: (a[x], x))
+                        del lst[L:]
+        for p in range(P):
+            if not overflow[p]:
+                np.testing.assert_array_equal(np.array(lists[p], dtype=np.int64), ref[p])
