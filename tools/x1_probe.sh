@@ -1,6 +1,6 @@
 #!/bin/bash
-# Ablation probes of the x1e filter kernel (run through gpurun after building
-# the variants here with tools/build_variant.sh):
+# Ablation probes of the x1 filter kernel (run through gpurun after building
+# the variants here with tools/build_variant.sh <name> -DVS_X1_PROBE=<mask>):
 #   tools/x1_probe.sh <variant>...   (variant "base" = the default library)
 # Mean x1e dispatch time per variant from rocprofv3 --kernel-trace --stats.
 set -u
