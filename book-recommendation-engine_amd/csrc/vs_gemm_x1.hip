@@ -86,12 +86,19 @@ constexpr int kDumpMaxR = 32;         // dump slots per lane list per search (at
 // The step schedule of a plane (A/B: C3 uniform int8 68.6k vs 65.9k queries/s,
 // clustered bf16 34.4k vs 32.5k, profiles/r03_ab_sched.txt): 1 = fragment
 // reads half a step ahead, DMA pieces between the MFMAs (int8); 2 = separate
-// load and matrix segments (bf16).
-constexpr int x1_sched(int el) { return el == FILTER_I8 ? 1 : 2; }
-// the kernels with a dump form: every key of theirs follows from the raw sum
-// and per-row values the replay can read (int8: the row factor; bf16 inner
-// product: nothing); the bf16 L2 / cosine keys need the row norms in-kernel
-constexpr bool x1_has_dump(int mode, int el) { return el == FILTER_I8 || mode == MODE_IP; }
+// load and matrix segments (bf16).  VS_X1_SCHED_I8: A/B builds only.
+#ifndef VS_X1_SCHED_I8
+#define VS_X1_SCHED_I8 1
+#endif
+constexpr int x1_sched(int el) { return el == FILTER_I8 ? VS_X1_SCHED_I8 : 2; }
+// The passes with a dump form: inner product on either plane (every key
+// follows from the raw sum and, for int8, the row factor the replay reads).
+// Not the cosine: its bound is relative (B ~ 2 rho, ~0.02 at d = 1536 for
+// int8), wide beside the similarity spread of high-dimensional rows, so the
+// cut sits behind the lists' own floors and the dumps would overflow (a
+// d = 128 self-join of Gaussian rows: 31 dumps per list); the bf16 L2 /
+// cosine keys also need the row norms in the kernel.
+constexpr bool x1_has_dump(int mode, int el) { return mode == MODE_IP; }
 
 __device__ __forceinline__ unsigned long long stamp_now() {
   unsigned long long t;
@@ -309,7 +316,13 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     if constexpr (DUMP) {
-      tq[qb] = gq[qb] < nqa ? qcut[gq[qb]] : -FLT_MAX;
+      // the cut, or the list's own last entry after the first launch when
+      // that is lower (a row at or above it can never enter this list: its
+      // last entry only falls)
+      const int64_t o = ((int64_t)gq[qb] * P + pl) * KP + KR - 1;
+      float tl = qcut[gq[qb]];
+      if (pid[o] >= 0) tl = fminf(tl, pkey[o]);
+      tq[qb] = gq[qb] < nqa ? tl : -FLT_MAX;
       dc[qb] = dcount[(int64_t)gq[qb] * P + pl];
       asm volatile("" ::"v"(tq[qb]), "v"(dc[qb]));
     } else {
