@@ -855,6 +855,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
         x.dsum = ds;
         x.dtag = dt;
         x.dR = dR;
+        x.dstats = device_stats(idx->device) ? device_stats(idx->device) + 6 : nullptr;
       } else {
         (void)hipGetLastError();  // out of memory for the dumps: list launches
       }
@@ -865,9 +866,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &tm.dispatches), "vs: gemm_topk_x1 launch");
     tm.stop();
   }
-  unsigned long long* dst = device_stats(idx->device);
-  if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
-  VS_HIP(launch_x1_replay(x, part, st, dst + 6), "vs: x1 replay");
+
   // approximate top-KF per query (plain lexicographic order: the L2 merge)
   float* Dk = nullptr;
   int64_t* Ik = nullptr;
@@ -896,6 +895,8 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
                                Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
                                st, qinv, xinv, qr2, gc, x.qcut),
          "vs: verify");
+  unsigned long long* dst = device_stats(idx->device);
+  if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
   // statistics: [0] queries (first stage), [1] flagged by a first check, [2]
   // redone by the exact engine, [3] handed to a second filter stage
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, gathered ? nullptr : dst + 0, st),

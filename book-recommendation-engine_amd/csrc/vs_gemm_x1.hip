@@ -895,18 +895,19 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 }
 
-// The replay of a pass's dumps (after its last dump launch): one thread per
-// lane list (query q, list pl = 4 sp + 2 wr + h).  The list as the first
-// launch left it, then every dumped block in dump order (the order the lane
-// met them: tiles ascending, launch after launch), each of its 16 rows with
-// the key the list epilogue computes (x1_key, the same expression) and the
-// same admission: key < min(last entry, cut), the row inside the corpus and not
-// the query's own.  A list with more dumps than slots lost some: its query's
-// cut becomes -FLT_MAX, which fails both checks of the verification (the query
-// goes to the next stage).
+// The replay of a segment of dump launches: one thread per lane list (query
+// q, list pl = 4 sp + 2 wr + h).  The list as the previous launches left it,
+// then every block dumped since in dump order (the order the lane met them:
+// tiles ascending, launch after launch), each of its 16 rows with the key the
+// list epilogue computes (x1_key, the same expression) and the same
+// admission: key < min(last entry, cut), the row inside the corpus and not the
+// query's own; the count restarts at zero for the next segment.  A list with
+// more dumps than slots lost some: its query's cut becomes -FLT_MAX, which
+// fails both checks of the verification (the query goes to the next stage)
+// and stops the query's dumps.
 template <int KR, int EL>
 __global__ __launch_bounds__(256) void x1_replay_kernel(
-    const int* __restrict__ dcount, const int* __restrict__ dsum, const int* __restrict__ dtag,
+    int* __restrict__ dcount, const int* __restrict__ dsum, const int* __restrict__ dtag,
     float* __restrict__ pkey, int* __restrict__ pid, int P, int KP, int nqa,
     const float* __restrict__ qs, const float* __restrict__ xs, int64_t self0, int ntotal,
     int dR, float* __restrict__ qcut, unsigned long long* __restrict__ stats) {
@@ -918,12 +919,13 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
       a += __shfl_xor(a, o);
       b += __shfl_xor(b, o);
     }
-    if ((threadIdx.x & 63) == 0 && a) {
+    if ((threadIdx.x & 63) == 0 && a && stats) {
       atomicAdd(stats, a);
       if (b) atomicAdd(stats + 1, b);
     }
   }
   if (cnt == 0) return;
+  dcount[i] = 0;  // the next segment's dumps start at slot 0
   const int q = (int)(i / P), pl = (int)(i % P);
   if (cnt > dR) {
     qcut[q] = -FLT_MAX;
@@ -1025,6 +1027,18 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
       e = launch_qcut(a, part, st);
       if (e != hipSuccess) return e;
     }
+    // Segments of dump launches end where the data seen doubles (after
+    // launches 1, 3, 7, 15, ... and the last): a dump launch's threshold is
+    // min(cut, list last entry at its start), and the replay between segments
+    // lowers the last entries, so a lane list meets ~8 blocks below its own
+    // floor per segment whatever the data (a top-8 list over n rows is beaten
+    // by ~8 of the next n) — the cut alone is too wide when 2B spans
+    // thousands of rows (C3: ~5k, 63 % of the lists out of 32 slots in one
+    // segment, profiles/r04b).
+    if (dumping && c > 0 && (((c + 1) & c) == 0 || c + 1 == nchunk)) {
+      e = launch_x1_replay(a, part, st);
+      if (e != hipSuccess) return e;
+    }
   }
   if (ndispatch) *ndispatch = nchunk;
   return hipSuccess;
@@ -1078,8 +1092,8 @@ bool x1_dump_applies(int mode, int filter) { return x1_has_dump(mode, filter); }
 
 // The replay of launch_gemm_topk_x1's dumps (a no-op when the pass had none to
 // make: the counts stay zero).
-hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st,
-                            unsigned long long* stats) {
+hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st) {
+  unsigned long long* stats = a.dstats;
   if (!a.dump || !a.dcount || a.nqa <= 0) return hipSuccess;
   if (part.KP < x1_lane_len()) return hipErrorInvalidValue;
   const int64_t n = (int64_t)a.nqa * part.P;

@@ -111,6 +111,7 @@ struct X1Args {
   int* dsum = nullptr;           // [nq_pad][P][dR][16] raw sums of the dumped blocks
   int* dtag = nullptr;           // [nq_pad][P][dR] tile * 4 + row block of each dump
   int dR = 0;                    // dump slots per lane list
+  unsigned long long* dstats = nullptr;  // [2] dumps replayed, lists out of slots
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
   const void* QH = nullptr;      // query plane, tile-major (self-join: the stored plane)
   int qtile0 = 0;                // QH's tile of query tile 0 (self-join: self0 / 256)
@@ -242,9 +243,9 @@ hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, 
                          hipStream_t st);
 bool x1_dump_applies(int mode, int filter);
 int x1_dump_slots();  // the most dump slots per lane list worth allocating
-// stats[0] += dumps replayed, stats[1] += lane lists out of slots
-hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st,
-                            unsigned long long* stats);
+// a.dstats[0] += dumps replayed, a.dstats[1] += lane lists out of slots
+// (launch_gemm_topk_x1 calls it between its segments of dump launches)
+hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st);
 // Lists -> final (D, I) rows of k entries each (row stride ldo), labels offset by id_base.
 // Inner product applies faiss's tie rule unless `raw` (plain lexicographic
 // (key, label) order, the per-shard half of an exact sharded merge).  With

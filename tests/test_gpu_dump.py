@@ -9,8 +9,8 @@ length (their splits are a few tiles), so these searches are sized for it:
 split: one list launch + three dump launches), checked STRICTLY against the
 fp64 oracle on 512 sampled queries (every query tile), with the dump counters
 showing that dump launches ran.  Also: lane lists that run out of dump slots
-(12,000 ever-better copies of a row next to the queries: ~70 dumps per list >
-32 slots) hand their queries to the next stage and the answer stays exact;
+(90,000 ever-better copies of a row next to the queries: ~150 dumps per list
+and segment > 32 slots) hand their queries to the next stage and the answer stays exact;
 the bf16 plane's dump form; and the cosine self-join (C4's path), which keeps
 list launches."""
 
@@ -74,15 +74,15 @@ def test_dump_launches_clustered_unit_rows(lib):
 
 
 def test_dump_slot_overflow_hands_queries_on(lib):
-    """12,000 scaled copies of one row beside every query, each a little better
-    than every copy at a lower row: every lane list meets ~70 of them after the
-    first launch, each below its cut and its own last entry — more blocks than
-    its 32 dump slots.  The query is failed by the verification (cut =
+    """90,000 scaled copies of one row beside every query, each a little better
+    than every copy at a lower row: in every segment of dump launches a lane
+    list meets ~150 of them below its cut and its own last entry — more blocks
+    than its 32 dump slots.  The query is failed by the verification (cut =
     -FLT_MAX) and answered by the next stage: exactly."""
     rng = np.random.default_rng(77)
     xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
     dup = rng.uniform(-1, 1, D_).astype(np.float32)
-    pos = np.sort(rng.choice(N, 12_000, replace=False))
+    pos = np.sort(rng.choice(N, 90_000, replace=False))
     xb[pos] = dup[None, :] * (1.0 + 1e-3 * pos[:, None] / N).astype(np.float32)
     xq = (dup[None, :] + 0.3 * rng.uniform(-1, 1, (B, D_))).astype(np.float32)
     dumps, over, fq, _ = _search_checked(lib, xb, xq, 10)
