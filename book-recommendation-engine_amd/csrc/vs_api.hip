@@ -826,7 +826,8 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   x.self0 = self_rows ? a.self0 : -1;
   x.qrow = qrow;
   x.qcount = gc;
-  if (!gathered && x1_dump_applies(mode, plane) && dump_enabled()) {
+  if (!gathered && x1_dump_applies(mode, plane) && dump_enabled() &&
+      x1_pass_dumps(ntotal, x.nsplit)) {
     // query cuts + dump launches (vs_gemm_x1.hip header and "Query cuts"): the
     // cuts are set after the pass's first launch and are the verification's
     // floor for the rows the dump launches drop.  The dump slots: up to

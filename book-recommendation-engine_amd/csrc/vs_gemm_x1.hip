@@ -83,12 +83,15 @@ constexpr int kT = 256;               // rows (and queries) per tile
 constexpr int kNbuf = 5;              // LDS images in the ring (4: -1 %, profiles/r02y)
 constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
 constexpr int kDumpMaxR = 32;         // dump slots per lane list per search (at most)
-// The step schedule of a plane (A/B: C3 uniform int8 68.6k vs 65.9k queries/s,
-// clustered bf16 34.4k vs 32.5k, profiles/r03_ab_sched.txt): 1 = fragment
-// reads half a step ahead, DMA pieces between the MFMAs (int8); 2 = separate
-// load and matrix segments (bf16).  VS_X1_SCHED_I8: A/B builds only.
+// The step schedule of a plane: 1 = fragment reads half a step ahead, DMA
+// pieces between the MFMAs; 2 = separate load and matrix segments.  Round 3
+// (list launches only: the heavy epilogue) measured int8 faster on 1 (C3 68.6k
+// vs 65.9k queries/s) and bf16 on 2 (clustered 34.4k vs 32.5k,
+// profiles/r03_ab_sched.txt); with dump launches int8 is faster on 2 as well
+// (C3 72.3k vs 70.1k, profiles/r04a/r04d_sched_c2_cl_ab.txt).
+// VS_X1_SCHED_I8: A/B builds only.
 #ifndef VS_X1_SCHED_I8
-#define VS_X1_SCHED_I8 1
+#define VS_X1_SCHED_I8 2
 #endif
 constexpr int x1_sched(int el) { return el == FILTER_I8 ? VS_X1_SCHED_I8 : 2; }
 // The passes with a dump form: inner product on either plane (every key
@@ -996,14 +999,14 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // a gathered later stage (usually empty: its tiles exit at once) is one launch
   int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   // Dump launches after the first: its lists set the cuts (x1_qcut), the rest
-  // of the pass stores only the blocks below them, and x1_replay (called by the
-  // host after this function returns, outside the pass's timer) folds the dumps
-  // into the lists.  At most 1/8 of a split in the first launch when the
-  // splits are long enough (C2: 31 tiles -> 3 launches, C4: 122 -> 8).
+  // of the pass stores only the blocks below them, and x1_replay folds the
+  // dumps into the lists between segments (below).  Only passes of at least
+  // 4 launches (C3: 20): cutting a short pass into more launches costs more
+  // than it saves (C2 forced to 3 launches: 308k vs 394k queries/s,
+  // profiles/r04a/r04d_sched_c2_cl_ab.txt).
   const bool dump = a.dump && x1_has_dump(MODE, EL) && !a.qcount && a.qcut && a.qbkey &&
                     a.qcut_m > 0 && a.dcount && a.dsum && a.dtag && a.dR > 0;
-  if (dump) nchunk = std::max(nchunk, std::min(8, per_block / 8));
-  const bool dumping = dump && nchunk > 1;
+  const bool dumping = dump && nchunk >= 4;  // x1_pass_dumps
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
@@ -1046,6 +1049,11 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
 
 int x1_lane_len() { return 8; }
 int x1_dump_slots() { return kDumpMaxR; }
+bool x1_pass_dumps(int ntotal, int nsplit) {
+  const int ntiles = (ntotal + kT - 1) / kT;
+  const int per_block = (ntiles + nsplit - 1) / nsplit;
+  return (per_block + kX1ChunkTiles - 1) / kX1ChunkTiles >= 4;
+}
 
 hipError_t x1_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_stamps), sizeof(g_x1_stamps));

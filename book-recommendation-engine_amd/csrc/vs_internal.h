@@ -243,6 +243,7 @@ hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, 
                          hipStream_t st);
 bool x1_dump_applies(int mode, int filter);
 int x1_dump_slots();  // the most dump slots per lane list worth allocating
+bool x1_pass_dumps(int ntotal, int nsplit);  // a pass this long has dump launches
 // a.dstats[0] += dumps replayed, a.dstats[1] += lane lists out of slots
 // (launch_gemm_topk_x1 calls it between its segments of dump launches)
 hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st);
