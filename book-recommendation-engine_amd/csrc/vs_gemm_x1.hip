@@ -93,6 +93,10 @@ constexpr int kDumpMaxR = 32;         // dump slots per lane list per search (at
 #ifndef VS_X1_SCHED_I8
 #define VS_X1_SCHED_I8 2
 #endif
+// steps in flight of the segmented schedule (3; 4 for A/B builds)
+#ifndef VS_X1_SEG_D
+#define VS_X1_SEG_D 3
+#endif
 constexpr int x1_sched(int el) { return el == FILTER_I8 ? VS_X1_SCHED_I8 : 2; }
 // The passes with a dump form: inner product on either plane (every key
 // follows from the raw sum and, for int8, the row factor the replay reads).
@@ -792,14 +796,20 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // wave (reads retired by the lgkmcnt wait that opens the reader's matrix
     // segment); an image is read only after the barrier that follows every
     // wave's counted wait for its pieces.
-    static_assert(NBUF == 5, "segmented schedule: 3 steps in flight over 5 images");
+    // VS_X1_SEG_D = 4 (A/B): 4 steps in flight, the image a DMA refills read
+    // ONE barrier earlier, which every reader's reads have retired at (an
+    // lgkmcnt(0) closes each load segment).
+    constexpr int SD = VS_X1_SEG_D;
+    static_assert(NBUF == 5 && (SD == 3 || SD == 4), "segmented schedule: steps in flight");
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < SD; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) stage_piece(j);
       advance_cursor();
     }
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step 0
+    // this wave's pieces of step 0
+    if constexpr (SD == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
@@ -820,8 +830,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       advance_cursor();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(0);
-      // this wave's pieces of step s+1 (the younger steps s+2, s+3 stay in flight)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      // this wave's pieces of step s+1 (the younger steps stay in flight)
+      if constexpr (SD == 4) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       VS_X1_MARK(1);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
