@@ -83,21 +83,19 @@ constexpr int kT = 256;               // rows (and queries) per tile
 constexpr int kNbuf = 5;              // LDS images in the ring (4: -1 %, profiles/r02y)
 constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
 constexpr int kDumpMaxR = 32;         // dump slots per lane list per search (at most)
-// The step schedule of a plane: 1 = fragment reads half a step ahead, DMA
-// pieces between the MFMAs; 2 = separate load and matrix segments.  Round 3
-// (list launches only: the heavy epilogue) measured int8 faster on 1 (C3 68.6k
-// vs 65.9k queries/s) and bf16 on 2 (clustered 34.4k vs 32.5k,
-// profiles/r03_ab_sched.txt); with dump launches int8 is faster on 2 as well
-// (C3 72.3k vs 70.1k, profiles/r04a/r04d_sched_c2_cl_ab.txt).
-// VS_X1_SCHED_I8: A/B builds only.
+// The step schedule of a launch: 1 = fragment reads half a step ahead, DMA
+// pieces between the MFMAs; 2 = separate load and matrix segments.  Measured
+// per plane and launch kind (A/B builds: VS_X1_SCHED_I8 forces one for every
+// int8 launch): int8 list launches are faster on 1 (C2 390k vs 337k
+// queries/s, C4 465k vs 437k students/s), int8 dump launches on 2 (C3 70.8k
+// vs 68.9k; profiles/r04a/r04e_sched_dump_ab.txt), bf16 on 2 (clustered
+// 34.4k vs 32.5k, profiles/r03_ab_sched.txt).
 #ifndef VS_X1_SCHED_I8
-#define VS_X1_SCHED_I8 2
+#define VS_X1_SCHED_I8 0
 #endif
-// steps in flight of the segmented schedule (3; 4 for A/B builds)
-#ifndef VS_X1_SEG_D
-#define VS_X1_SEG_D 3
-#endif
-constexpr int x1_sched(int el) { return el == FILTER_I8 ? VS_X1_SCHED_I8 : 2; }
+constexpr int x1_sched(int el, bool dump) {
+  return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump ? 2 : 1;
+}
 // The passes with a dump form: inner product on either plane (every key
 // follows from the raw sum and, for int8, the row factor the replay reads).
 // Not the cosine: its bound is relative (B ~ 2 rho, ~0.02 at d = 1536 for
@@ -572,7 +570,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // row blocks per load group: 2 under the segmented schedule; 1 under the
       // round-2 schedule, whose next-step fragments stay live across the
       // epilogue (registers)
-      constexpr int G = x1_sched(EL) != 1 ? 2 : 1;
+      constexpr int G = x1_sched(EL, DUMP) != 1 ? 2 : 1;
 #pragma unroll
       for (int hp = 0; hp < 4 / G; ++hp) {
         f32x4 rv[G][4];
@@ -683,7 +681,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
     };
 
-    constexpr int kSched = x1_sched(EL);
+    constexpr int kSched = x1_sched(EL, DUMP);
     if constexpr (kSched == 1) {
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
@@ -796,20 +794,17 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // wave (reads retired by the lgkmcnt wait that opens the reader's matrix
     // segment); an image is read only after the barrier that follows every
     // wave's counted wait for its pieces.
-    // VS_X1_SEG_D = 4 (A/B): 4 steps in flight, the image a DMA refills read
-    // ONE barrier earlier, which every reader's reads have retired at (an
-    // lgkmcnt(0) closes each load segment).
-    constexpr int SD = VS_X1_SEG_D;
-    static_assert(NBUF == 5 && (SD == 3 || SD == 4), "segmented schedule: steps in flight");
+    // (4 steps in flight, each load segment closed by an lgkmcnt(0) so the
+    // image a DMA refills could be the one read a barrier earlier: C3 70.2k vs
+    // 70.8k queries/s, C2 -3 %, C4 -2 %: not shipped)
+    static_assert(NBUF == 5, "segmented schedule: 3 steps in flight over 5 images");
 #pragma unroll
-    for (int i = 0; i < SD; ++i) {
+    for (int i = 0; i < 3; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) stage_piece(j);
       advance_cursor();
     }
-    // this wave's pieces of step 0
-    if constexpr (SD == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step 0
     __builtin_amdgcn_s_barrier();
     const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
@@ -831,8 +826,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(0);
       // this wave's pieces of step s+1 (the younger steps stay in flight)
-      if constexpr (SD == 4) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       VS_X1_MARK(1);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
