@@ -986,15 +986,20 @@ static int x1_qg() {
 
 static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
 
+// Database tiles per workgroup per launch (env VS_X1_CHUNK_TILES overrides the
+// default, read at every search: A/B runs, and tests that need multi-launch
+// passes on small indexes)
+static int x1_chunk_tiles() {
+  const char* e = getenv("VS_X1_CHUNK_TILES");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : kX1ChunkTiles;
+}
+
 template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
   const int nqt = a.nq_pad / kT;
-  static const int chunk_tiles = [] {
-    const char* e = getenv("VS_X1_CHUNK_TILES");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : kX1ChunkTiles;
-  }();
+  const int chunk_tiles = x1_chunk_tiles();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   // A gathered later stage holds its few queries in the first query tile(s):
   // every XCD takes every query tile there (QG = nqt), so the working
@@ -1057,7 +1062,7 @@ int x1_dump_slots() { return kDumpMaxR; }
 bool x1_pass_dumps(int ntotal, int nsplit) {
   const int ntiles = (ntotal + kT - 1) / kT;
   const int per_block = (ntiles + nsplit - 1) / nsplit;
-  return (per_block + kX1ChunkTiles - 1) / kX1ChunkTiles >= 4;
+  return (per_block + x1_chunk_tiles() - 1) / x1_chunk_tiles() >= 4;
 }
 
 hipError_t x1_stamps(unsigned long long* out, int reset) {

@@ -6,7 +6,8 @@ lists (x1_qcut), and runs the rest as dump launches whose blocks below the cut
 x1_replay folds into the lists.  The small parity tests never reach that
 length (their splits are a few tiles), so these searches are sized for it:
 4,096 queries (16 query tiles, 32 splits) over 300,000 rows (37 tiles per
-split: one list launch + three dump launches), checked STRICTLY against the
+split, launches of 8 tiles: one list launch + four dump launches in three
+segments), checked STRICTLY against the
 fp64 oracle on 512 sampled queries (every query tile), with the dump counters
 showing that dump launches ran.  Also: lane lists that run out of dump slots
 (90,000 ever-better copies of a row next to the queries: ~150 dumps per list
@@ -28,10 +29,21 @@ SAMPLE = np.array(sorted({q for t in range(16) for q in range(256 * t, 256 * t +
 
 @pytest.fixture(scope="module")
 def lib():
+    """Launches of 8 tiles per workgroup (VS_X1_CHUNK_TILES, read at every
+    search): 37-tile splits become a 5-launch pass, which has dump launches
+    (a pass needs at least 4; at the default 64 tiles that takes ~1.6M rows)."""
+    import os
+
     from vsearch import _lib
 
     assert _lib.device_count() >= 1
-    return _lib
+    old = os.environ.get("VS_X1_CHUNK_TILES")
+    os.environ["VS_X1_CHUNK_TILES"] = "8"
+    yield _lib
+    if old is None:
+        del os.environ["VS_X1_CHUNK_TILES"]
+    else:
+        os.environ["VS_X1_CHUNK_TILES"] = old
 
 
 def _search_checked(lib, xb, xq, k, engine="auto"):
