@@ -76,21 +76,30 @@ def x1_dominant(ctx, work_total, kms, nl):
     """The filter engine's first stage runs on the int8 or the bf16 plane per
     search (the library's adaptive order).  Returns the plane that took most of
     the timed kernel time: (timer name, its share of the algorithmic work, its
-    kernel ms, its dispatches, per-plane record).  Both planes' launches are the
-    same grid over the same batch, so the work per dispatch is the same."""
+    kernel ms, its dispatches, per-plane record).  A pass whose later launches
+    are dump launches times its first (list) launch apart ("<name>_list"): the
+    roofline is the dump kernel's own time.  Every launch of a pass covers the
+    same share of the database tiles (even chunks), so the work per dispatch
+    is the same for all of them."""
     mi, ni = ctx.lib.timer_read_kernel("gemm_topk_x1_i8")
+    mil, nil = ctx.lib.timer_read_kernel("gemm_topk_x1_i8_list")
     mb, nb = ctx.lib.timer_read_kernel("gemm_topk_x1")
-    per = work_total / max(1, ni + nb)
+    mbl, nbl = ctx.lib.timer_read_kernel("gemm_topk_x1_list")
+    per = work_total / max(1, ni + nil + nb + nbl)
     split = {"i8": {"dispatches": ni, "kernel_ms": round(mi, 3)},
-             "bf16": {"dispatches": nb, "kernel_ms": round(mb, 3)}}
-    if mi >= mb:
+             "i8_list_launches": {"dispatches": nil, "kernel_ms": round(mil, 3)},
+             "bf16": {"dispatches": nb, "kernel_ms": round(mb, 3)},
+             "bf16_list_launches": {"dispatches": nbl, "kernel_ms": round(mbl, 3)}}
+    if mi + mil >= mb + mbl:
         return "gemm_topk_x1_i8", per * ni, mi, ni, split
     return "gemm_topk_x1", per * nb, mb, nb, split
 
 
 def rocprof_prefix(kname: str):
-    """rocprof's name of a timed kernel: gemm_topk_x1<KR, MODE, NBUF, EL> with EL
-    1 = int8, 0 = bf16 (the plane is the last template argument)."""
+    """rocprof's name of a timed kernel: gemm_topk_x1<KR, MODE, DUMP, EL> with EL
+    1 = int8, 0 = bf16 (the plane is the last template argument); the PMC
+    lookup takes the instantiation with the most dispatches (the dump launches
+    where a pass has them)."""
     if kname == "gemm_topk_x1_i8":
         return "void vs::gemm_topk_x1<", ", 1>("
     if kname == "gemm_topk_x1":

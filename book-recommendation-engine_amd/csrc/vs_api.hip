@@ -421,6 +421,28 @@ struct KernelTimer {
   }
 };
 
+// The filter pass's per-launch spans: dump launches (and every launch of a
+// pass without dumps) under the pass's timer name, the list launch of a pass
+// with dumps under "<name>_list" (bench.py: the roofline is the dominant
+// kernel's own time; the cut and replay kernels between launches are in no
+// span).
+struct X1SpanTimer : X1Timing {
+  const char* name;
+  const char* list_name;
+  KernelTimer* cur = nullptr;
+  X1SpanTimer(const char* n, const char* ln) : name(n), list_name(ln) {}
+  void begin(hipStream_t st, bool dominant) override {
+    cur = new KernelTimer(st, dominant ? name : list_name);
+  }
+  void end(hipStream_t) override {
+    if (!cur) return;
+    cur->stop();
+    delete cur;
+    cur = nullptr;
+  }
+  ~X1SpanTimer() override { end(nullptr); }
+};
+
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
@@ -863,9 +885,12 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     }
   }
   {
-    KernelTimer tm(st, gathered ? nullptr : i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1");
-    VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &tm.dispatches), "vs: gemm_topk_x1 launch");
-    tm.stop();
+    X1SpanTimer tm(i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1",
+                   i8 ? "gemm_topk_x1_i8_list" : "gemm_topk_x1_list");
+    if (!gathered) x.timing = &tm;
+    int nd = 0;
+    VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &nd), "vs: gemm_topk_x1 launch");
+    x.timing = nullptr;
   }
 
   // approximate top-KF per query (plain lexicographic order: the L2 merge)

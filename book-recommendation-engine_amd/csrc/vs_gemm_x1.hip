@@ -958,12 +958,19 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
     const i32x4* src = (const i32x4*)(dsum + slot * 16);
     const i32x4 v4[4] = {src[0], src[1], src[2], src[3]};
     const bool plain = self0 < 0 && (t + 1) * kT <= ntotal;
+    // the block's rows come in 4 runs of 4 consecutive rows: one 16-B factor
+    // load per run (16 scattered 4-B loads cost a line each)
+    f32x4 fx4[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      fx4[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (EL == FILTER_I8) fx4[jj] = *(const f32x4*)(xs + x1_row(t, wr, rb, h, 4 * jj));
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = x1_row(t, wr, rb, h, r);
       if (!(plain || (row < ntotal && row != selfrow))) continue;
-      const float fx = EL == FILTER_I8 ? xs[row] : 0.0f;
-      const float key = x1_key<EL>(v4[r >> 2][r & 3], qsc, fx);
+      const float key = x1_key<EL>(v4[r >> 2][r & 3], qsc, fx4[r >> 2][r & 3]);
       if (key < fminf(lk[KR - 1], cut)) list_insert<KR, int>(lk, li, key, row);
     }
   }
@@ -1020,6 +1027,9 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
+    // the timed span of this launch alone (the cut and replay kernels between
+    // launches stay outside the spans)
+    if (a.timing) a.timing->begin(st, !dumping || c > 0);
     if (dumping && c > 0) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, true, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
@@ -1034,6 +1044,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
                          a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
                          a.xgmax, nullptr, nullptr, nullptr, nullptr, 0);
     }
+    if (a.timing) a.timing->end(st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (dumping && c == 0) {

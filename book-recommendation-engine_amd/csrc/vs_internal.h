@@ -96,7 +96,16 @@ inline int filter_bytes(int filter) { return filter == FILTER_I8 ? 1 : 2; }
 __host__ __device__ inline int64_t plane_offset(int64_t row, int64_t byte, int64_t ldb) {
   return ((row >> 8) * (ldb >> 6) + (byte >> 6)) * 16384 + (row & 255) * 64 + (byte & 63);
 }
+// Per-launch timing hook of the filter pass (vs_api.hip): x1_launch brackets
+// every pass launch with begin/end; `dominant` is false for the list launch of
+// a pass that dumps (its spans are named apart from the dump launches').
+struct X1Timing {
+  virtual void begin(hipStream_t st, bool dominant) = 0;
+  virtual void end(hipStream_t st) = 0;
+  virtual ~X1Timing() = default;
+};
 struct X1Args {
+  X1Timing* timing = nullptr;
   int filter = FILTER_BF16;
   const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
