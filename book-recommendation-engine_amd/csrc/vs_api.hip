@@ -853,15 +853,14 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     // query cuts + dump launches (vs_gemm_x1.hip header and "Query cuts"): the
     // cuts are set after the pass's first launch and are the verification's
     // floor for the rows the dump launches drop.  The dump slots: up to
-    // x1_dump_slots() per lane list within ~8 GB (C4's 65,536-student chunks:
-    // 15); fewer than 8 (or no memory): every launch is a list launch.
+    // x1_dump_slots() candidate rows per lane list and segment within ~4 GB;
+    // fewer than 16 (or no memory): every launch is a list launch.
     const int64_t lists = (int64_t)x.nq_pad * part.P;
-    const int dR = (int)std::min<int64_t>(x1_dump_slots(), (int64_t(8) << 30) / (lists * 68));
-    if (dR >= 8) {
-      int *dc = nullptr, *ds = nullptr, *dt = nullptr;
+    const int dR = (int)std::min<int64_t>(x1_dump_slots(), (int64_t(4) << 30) / (lists * 8));
+    if (dR >= 16) {
+      int *dc = nullptr, *ds = nullptr;
       hipError_t e = scr.alloc((void**)&dc, (size_t)lists * sizeof(int));
-      if (e == hipSuccess) e = scr.alloc((void**)&ds, (size_t)lists * dR * 16 * sizeof(int));
-      if (e == hipSuccess) e = scr.alloc((void**)&dt, (size_t)lists * dR * sizeof(int));
+      if (e == hipSuccess) e = scr.alloc((void**)&ds, (size_t)lists * dR * 2 * sizeof(int));
       if (e == hipSuccess) {
         VS_HIP(scr.alloc((void**)&x.qcut, (size_t)qa_rows * sizeof(float)), "vs: scratch");
         double* bk = nullptr;
@@ -875,8 +874,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
         x.qcut_m = need;
         x.dump = true;
         x.dcount = dc;
-        x.dsum = ds;
-        x.dtag = dt;
+        x.dslot = ds;
         x.dR = dR;
         x.dstats = device_stats(idx->device) ? device_stats(idx->device) + 6 : nullptr;
       } else {

@@ -8,6 +8,7 @@ namespace vs {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define VS_LDS(p) ((__attribute__((address_space(3))) void*)(p))
@@ -48,25 +49,6 @@ __device__ __forceinline__ void list_insert(float (&lk)[KP], IdT (&li)[KP], floa
       li[j - 1] = sw ? ia : ib;
     }
   }
-}
-
-// The same insertion, branch-free: every entry is compared with the new one at
-// once (independent compares instead of a chain of dependent swaps; bitwise
-// and/or, so no exec-mask branches), then each slot takes its left neighbour,
-// the new entry or itself.  The flags are monotone in j (the list is sorted),
-// so the result equals list_insert's.
-template <int KP, typename IdT>
-__device__ __forceinline__ void list_insert_par(float (&lk)[KP], IdT (&li)[KP], float key, IdT id) {
-  bool c[KP];
-#pragma unroll
-  for (int j = 0; j < KP; ++j) c[j] = (key < lk[j]) | ((key == lk[j]) & (id < li[j]));
-#pragma unroll
-  for (int j = KP - 1; j > 0; --j) {
-    lk[j] = c[j - 1] ? lk[j - 1] : (c[j] ? key : lk[j]);
-    li[j] = c[j - 1] ? li[j - 1] : (c[j] ? id : li[j]);
-  }
-  lk[0] = c[0] ? key : lk[0];
-  li[0] = c[0] ? id : li[0];
 }
 
 __device__ __forceinline__ float l2_from_ip(float qn, float xn, float ip) {

@@ -82,7 +82,7 @@ namespace {
 constexpr int kT = 256;               // rows (and queries) per tile
 constexpr int kNbuf = 5;              // LDS images in the ring (4: -1 %, profiles/r02y)
 constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
-constexpr int kDumpMaxR = 32;         // dump slots per lane list per search (at most)
+constexpr int kDumpMaxR = 64;         // dump slots (candidate rows) per lane list and segment
 // The step schedule of a launch: 1 = fragment reads half a step ahead, DMA
 // pieces between the MFMAs; 2 = separate load and matrix segments.  Measured
 // per plane and launch kind (A/B builds: VS_X1_SCHED_I8 forces one for every
@@ -154,18 +154,6 @@ __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_
 // check's floor T toward the top and failing its bound.
 __device__ __forceinline__ int tile_perm(int t) {
   return (int)(((uint32_t)t * 2654435761u) >> 24) & 0xFC;
-}
-
-// Row of value r (0..15) of the lane's 32-row block rb in tile t: slot
-// 128 wr + 32 rb + 8 jj + 4 h + e (jj = r >> 2, e = r & 3) holds row
-// t kT + (slot ^ f); the slot's fields are disjoint bits, so the XOR splits
-// into a uniform part (wr, rb, jj) and one lane part (h), and f leaves the low
-// two bits (e).  The list epilogue's rowof is the same formula with its
-// uniform parts hoisted; x1_replay uses this one.
-__device__ __forceinline__ int x1_row(int t, int wr, int rb, int h, int r) {
-  const int f = tile_perm(t);
-  return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * (r >> 2)) ^ (f & 0x18)) +
-         ((4 * h) ^ (f & 0x04)) + (r & 3);
 }
 
 __device__ __forceinline__ int sel16i(const i32x16& v, int i) {
@@ -253,8 +241,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
     int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax,
-    const float* __restrict__ qcut, int* __restrict__ dcount, int* __restrict__ dsum,
-    int* __restrict__ dtag, int dR) {
+    const float* __restrict__ qcut, int* __restrict__ dcount, int* __restrict__ dslot, int dR) {
   static_assert(!DUMP || x1_has_dump(MODE, EL), "dump form");
   constexpr int NBUF = kNbuf;
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
@@ -459,7 +446,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       const bool plain = self0 < 0 && !qrow && (t + 1) * kT <= ntotal;
       const int f = tile_perm(t);
       const int fh = (4 * h) ^ (f & 0x04);
-      // x1_row with the uniform parts hoisted
+      // slot 128 wr + 32 rb + 8 jj + 4 h + e holds row t kT + (slot ^ f); the
+      // slot's fields are disjoint bits, so the XOR splits into a uniform part
+      // (wr, rb, jj) and one lane part (h), and f leaves the low two bits (e)
       auto rowof = [&](int rb, int jj) {
         return t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0)) + ((8 * jj) ^ (f & 0x18)) + fh;
       };
@@ -528,25 +517,42 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         pass = 0;
       }
       if constexpr (DUMP) {
-        // Dump launch: the lane's 16 raw sums of every block that passed, with
-        // the block's (tile, row block), to the lane list's next slot; a list
-        // past its dR slots counts on (the replay fails its query).
+        // Dump launch: every row of a block that passed whose sum clears the
+        // block's limit (int8: above the block's integer threshold, the list
+        // test's phase 3; bf16: -sum below the limit) goes to the lane list's
+        // next slot as (row, raw sum): one 8-B store per candidate row (the
+        // stores queue behind the DMA pieces like everything in the vector
+        // memory path: a whole block's 16 sums took five stores and ~4 % of a
+        // C3 step, profiles/r04f/stamp_c3_dump.txt).  A list past its dR slots
+        // counts on (the replay fails its query).
         if (__ballot(pass != 0) == 0) return;  // uniform: the usual case
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
 #pragma unroll
           for (int qb = 0; qb < 2; ++qb) {
             if (pass & (1u << (2 * rb + qb))) {
-              const int c = dc[qb]++;
-              if (c < dR) {
-                const int64_t slot = ((int64_t)gq[qb] * P + pl) * dR + c;
-                i32x4* d = (i32x4*)(dsum + slot * 16);
-                const i32x16 v = __builtin_bit_cast(i32x16, acc[rb][qb]);
-                d[0] = i32x4{v[0], v[1], v[2], v[3]};
-                d[1] = i32x4{v[4], v[5], v[6], v[7]};
-                d[2] = i32x4{v[8], v[9], v[10], v[11]};
-                d[3] = i32x4{v[12], v[13], v[14], v[15]};
-                dtag[slot] = t * 4 + rb;
+              const float last = lim(qb);
+              uint32_t cm = 0;
+              if constexpr (EL == FILTER_I8) {
+                const float c = qsc[qb] * fmx[rb];
+                const int T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > T) << r;
+              } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cm |= (uint32_t)(-acc[rb][qb][r] < last) << r;
+              }
+              while (cm) {
+                const int bi = __builtin_ctz(cm);
+                cm &= cm - 1;
+                const int c = dc[qb]++;
+                if (c < dR) {
+                  int sum;
+                  if constexpr (EL == FILTER_I8) sum = sel16i(acc[rb][qb], bi);
+                  else sum = __float_as_int(sel16(acc[rb][qb], bi));
+                  const int64_t slot = ((int64_t)gq[qb] * P + pl) * dR + c;
+                  *(i32x2*)(dslot + slot * 2) = i32x2{rowof(rb, bi >> 2) + (bi & 3), sum};
+                }
               }
             }
           }
@@ -905,20 +911,20 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 
 // The replay of a segment of dump launches: one thread per lane list (query
 // q, list pl = 4 sp + 2 wr + h).  The list as the previous launches left it,
-// then every block dumped since in dump order (the order the lane met them:
-// tiles ascending, launch after launch), each of its 16 rows with the key the
-// list epilogue computes (x1_key, the same expression) and the same
-// admission: key < min(last entry, cut), the row inside the corpus and not the
-// query's own; the count restarts at zero for the next segment.  A list with
-// more dumps than slots lost some: its query's cut becomes -FLT_MAX, which
-// fails both checks of the verification (the query goes to the next stage)
-// and stops the query's dumps.
+// then every row dumped since in dump order (the order the lane met them:
+// tiles ascending, launch after launch) with the key the list epilogue
+// computes (x1_key, the same expression) and the same admission: key <
+// min(last entry, cut), the row inside the corpus and not the query's own; the
+// count restarts at zero for the next segment.  A list with more dumps than
+// slots lost some: its query's cut becomes -FLT_MAX, which fails both checks
+// of the verification (the query goes to the next stage) and stops the
+// query's dumps.
 template <int KR, int EL>
 __global__ __launch_bounds__(256) void x1_replay_kernel(
-    int* __restrict__ dcount, const int* __restrict__ dsum, const int* __restrict__ dtag,
-    float* __restrict__ pkey, int* __restrict__ pid, int P, int KP, int nqa,
-    const float* __restrict__ qs, const float* __restrict__ xs, int64_t self0, int ntotal,
-    int dR, float* __restrict__ qcut, unsigned long long* __restrict__ stats) {
+    int* __restrict__ dcount, const int* __restrict__ dslot, float* __restrict__ pkey,
+    int* __restrict__ pid, int P, int KP, int nqa, const float* __restrict__ qs,
+    const float* __restrict__ xs, int64_t self0, int ntotal, int dR, float* __restrict__ qcut,
+    unsigned long long* __restrict__ stats) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int cnt = i < (int64_t)nqa * P ? dcount[i] : 0;
   {  // statistics: one atomic per wave
@@ -934,14 +940,13 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
   }
   if (cnt == 0) return;
   dcount[i] = 0;  // the next segment's dumps start at slot 0
-  const int q = (int)(i / P), pl = (int)(i % P);
+  const int q = (int)(i / P);
   if (cnt > dR) {
     qcut[q] = -FLT_MAX;
     return;
   }
   const float cut = qcut[q];
   const float qsc = EL == FILTER_I8 ? qs[q] : 0.0f;
-  const int wr = (pl >> 1) & 1, h = pl & 1;
   const int selfrow = self0 >= 0 ? (int)(self0 + q) : -1;
   float lk[KR];
   int li[KR];
@@ -951,28 +956,13 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
     lk[e] = pkey[o + e];
     li[e] = pid[o + e];
   }
+  const i32x2* sl = (const i32x2*)(dslot + i * dR * 2);
   for (int c = 0; c < cnt; ++c) {
-    const int64_t slot = i * dR + c;
-    const int tag = dtag[slot];
-    const int t = tag >> 2, rb = tag & 3;
-    const i32x4* src = (const i32x4*)(dsum + slot * 16);
-    const i32x4 v4[4] = {src[0], src[1], src[2], src[3]};
-    const bool plain = self0 < 0 && (t + 1) * kT <= ntotal;
-    // the block's rows come in 4 runs of 4 consecutive rows: one 16-B factor
-    // load per run (16 scattered 4-B loads cost a line each)
-    f32x4 fx4[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      fx4[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (EL == FILTER_I8) fx4[jj] = *(const f32x4*)(xs + x1_row(t, wr, rb, h, 4 * jj));
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = x1_row(t, wr, rb, h, r);
-      if (!(plain || (row < ntotal && row != selfrow))) continue;
-      const float key = x1_key<EL>(v4[r >> 2][r & 3], qsc, fx4[r >> 2][r & 3]);
-      if (key < fminf(lk[KR - 1], cut)) list_insert<KR, int>(lk, li, key, row);
-    }
+    const i32x2 e = sl[c];
+    const int row = e[0];
+    if (!(row < ntotal && row != selfrow)) continue;
+    const float key = x1_key<EL>(e[1], qsc, EL == FILTER_I8 ? xs[row] : 0.0f);
+    if (key < fminf(lk[KR - 1], cut)) list_insert<KR, int>(lk, li, key, row);
   }
 #pragma unroll
   for (int e = 0; e < KR; ++e) {
@@ -1022,7 +1012,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // than it saves (C2 forced to 3 launches: 308k vs 394k queries/s,
   // profiles/r04a/r04d_sched_c2_cl_ab.txt).
   const bool dump = a.dump && x1_has_dump(MODE, EL) && !a.qcount && a.qcut && a.qbkey &&
-                    a.qcut_m > 0 && a.dcount && a.dsum && a.dtag && a.dR > 0;
+                    a.qcut_m > 0 && a.dcount && a.dslot && a.dR > 0;
   const bool dumping = dump && nchunk >= 4;  // x1_pass_dumps
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
@@ -1036,13 +1026,13 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
                            st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                            a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                            a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
-                           a.xgmax, a.qcut, a.dcount, a.dsum, a.dtag, a.dR);
+                           a.xgmax, a.qcut, a.dcount, a.dslot, a.dR);
     } else {
       hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                          st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                          a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                          a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
-                         a.xgmax, nullptr, nullptr, nullptr, nullptr, 0);
+                         a.xgmax, nullptr, nullptr, nullptr, 0);
     }
     if (a.timing) a.timing->end(st);
     hipError_t e = hipGetLastError();
@@ -1128,13 +1118,13 @@ hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st) {
   const int64_t n = (int64_t)a.nqa * part.P;
   const dim3 grid((unsigned)((n + 255) / 256));
   if (a.filter == FILTER_I8)
-    hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_I8>), grid, dim3(256), 0, st, a.dcount, a.dsum,
-                       a.dtag, part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs, a.self0,
-                       a.ntotal, a.dR, a.qcut, stats);
+    hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_I8>), grid, dim3(256), 0, st, a.dcount, a.dslot,
+                       part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs, a.self0, a.ntotal,
+                       a.dR, a.qcut, stats);
   else
     hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_BF16>), grid, dim3(256), 0, st, a.dcount,
-                       a.dsum, a.dtag, part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs,
-                       a.self0, a.ntotal, a.dR, a.qcut, stats);
+                       a.dslot, part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs, a.self0,
+                       a.ntotal, a.dR, a.qcut, stats);
   return hipGetLastError();
 }
 

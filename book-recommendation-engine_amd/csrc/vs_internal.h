@@ -117,9 +117,8 @@ struct X1Args {
   const double* qbkey = nullptr; // per query: the verification's bound B (x1_qcut)
   int qcut_m = 0;                // the M of the verification
   int* dcount = nullptr;         // [nq_pad][P] dumps per lane list (zeroed before the pass)
-  int* dsum = nullptr;           // [nq_pad][P][dR][16] raw sums of the dumped blocks
-  int* dtag = nullptr;           // [nq_pad][P][dR] tile * 4 + row block of each dump
-  int dR = 0;                    // dump slots per lane list
+  int* dslot = nullptr;          // [nq_pad][P][dR][2] dumped (row, raw sum) pairs
+  int dR = 0;                    // dump slots per lane list and segment
   unsigned long long* dstats = nullptr;  // [2] dumps replayed, lists out of slots
   const float* xaux = nullptr;   // per-row norms (L2) or 1/|x| (COS)
   const void* QH = nullptr;      // query plane, tile-major (self-join: the stored plane)

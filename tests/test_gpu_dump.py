@@ -10,8 +10,8 @@ split, launches of 8 tiles: one list launch + four dump launches in three
 segments), checked STRICTLY against the
 fp64 oracle on 512 sampled queries (every query tile), with the dump counters
 showing that dump launches ran.  Also: lane lists that run out of dump slots
-(90,000 ever-better copies of a row next to the queries: ~150 dumps per list
-and segment > 32 slots) hand their queries to the next stage and the answer stays exact;
+(90,000 ever-better copies of a row next to the queries: ~140 candidate rows
+per list and segment > 64 slots) hand their queries to the next stage and the answer stays exact;
 the bf16 plane's dump form; and the cosine self-join (C4's path), which keeps
 list launches."""
 
@@ -87,9 +87,9 @@ def test_dump_launches_clustered_unit_rows(lib):
 
 def test_dump_slot_overflow_hands_queries_on(lib):
     """90,000 scaled copies of one row beside every query, each a little better
-    than every copy at a lower row: in every segment of dump launches a lane
-    list meets ~150 of them below its cut and its own last entry — more blocks
-    than its 32 dump slots.  The query is failed by the verification (cut =
+    than every copy at a lower row: in a segment of dump launches a lane list
+    meets ~140 of them below its cut and its own last entry — more candidate
+    rows than its 64 dump slots.  The query is failed by the verification (cut =
     -FLT_MAX) and answered by the next stage: exactly."""
     rng = np.random.default_rng(77)
     xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
