@@ -369,6 +369,26 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     };
     set_xoff(t0);
 
+    // int8 dump launches: one integer threshold per list for the whole launch
+    // (its floor is fixed, and the factor bound is the launch's: the maximum
+    // of its tiles' group maxima), so the per-block test is a maximum and a
+    // compare with no per-tile loads or threshold arithmetic
+    int Tq[2] = {0, 0};
+    if constexpr (DUMP && EL == FILTER_I8) {
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      float fm = 0.0f;
+      for (int g = 16 * t0 + ln; g < 16 * t1; g += 64) fm = fmaxf(fm, xgmax[g]);
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) fm = fmaxf(fm, __shfl_xor(fm, m));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const float c = qsc[qb] * fm, last = tq[qb];
+        Tq[qb] = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c)
+                 : (c > 0.0f || -0.0f < last) ? INT_MIN : INT_MAX;
+        asm volatile("" ::"v"(Tq[qb]));
+      }
+    }
+
     AccT<EL> acc[4][2];
     // fragments of one sub-step: A (database rows) x4, B (queries) x2
     uint4 fa0[4], fb0[2], fa1[4], fb1[2];
@@ -471,7 +491,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         fmx[rb] = 0.0f;
-        if constexpr (EL == FILTER_I8) {
+        if constexpr (EL == FILTER_I8 && !DUMP) {
           const int grp = (t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0))) >> 5;  // uniform
           const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
           fmx[rb] = (fh & 4) ? g1 : g0;
@@ -490,7 +510,12 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         for (int qb = 0; qb < 2; ++qb) {
           const float last = lim(qb);
           bool p;
-          if constexpr (EL == FILTER_I8) {
+          if constexpr (EL == FILTER_I8 && DUMP) {
+            int amax = acc[rb][qb][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
+            p = amax > Tq[qb];
+          } else if constexpr (EL == FILTER_I8) {
             const float c = qsc[qb] * fmx[rb];
             if (c > 0.0f && -last >= 0.0f) {
               int amax = acc[rb][qb][0];
@@ -518,8 +543,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
       if constexpr (DUMP) {
         // Dump launch: every row of a block that passed whose sum clears the
-        // block's limit (int8: above the block's integer threshold, the list
-        // test's phase 3; bf16: -sum below the limit) goes to the lane list's
+        // limit (int8: above the launch's integer threshold; bf16: -sum below
+        // the limit) goes to the lane list's
         // next slot as (row, raw sum): one 8-B store per candidate row (the
         // stores queue behind the DMA pieces like everything in the vector
         // memory path: a whole block's 16 sums took five stores and ~4 % of a
@@ -534,10 +559,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               const float last = lim(qb);
               uint32_t cm = 0;
               if constexpr (EL == FILTER_I8) {
-                const float c = qsc[qb] * fmx[rb];
-                const int T = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c) : INT_MIN;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > T) << r;
+                for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > Tq[qb]) << r;
               } else {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) cm |= (uint32_t)(-acc[rb][qb][r] < last) << r;
