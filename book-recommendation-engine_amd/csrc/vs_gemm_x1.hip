@@ -93,6 +93,9 @@ constexpr int kDumpMaxR = 64;         // dump slots (candidate rows) per lane li
 #ifndef VS_X1_SCHED_I8
 #define VS_X1_SCHED_I8 0
 #endif
+#ifndef VS_X1_PRIO_SEG
+#define VS_X1_PRIO_SEG 0
+#endif
 constexpr int x1_sched(int el, bool dump) {
   return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump ? 2 : 1;
 }
@@ -837,6 +840,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     __builtin_amdgcn_s_barrier();
     const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
+    // A/B builds only: a static priority for one half (1 = the lagging waves
+    // 4-7, 2 = waves 0-3; MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+    if ((VS_X1_PRIO_SEG == 1 && lag) || (VS_X1_PRIO_SEG == 2 && !lag)) __builtin_amdgcn_s_setprio(1);
     int buf = 0, t = t0, ks = 0;
 #if VS_X1_STAMP
     tA = stamp_now();
