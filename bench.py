@@ -779,29 +779,36 @@ def run_c5(args, ctx):
     N, d, k, B = args.ntotal, args.d, args.k, args.batch
     index = ShardedIndexFlat(d, metric, device=ctx.local, dtype=args.dtype)
     index.add_synthetic(N, seed=1234)
-    gen = np.arange(N, dtype=np.int64)  # generator row of every current label
-    next_gen = N
     rng = np.random.default_rng(91011)
     xq = ctx.queries(max(B, args.recall_queries), d)
     nmut = max(1, N // 100)
     mut_time = 0.0
+    # The workload's mutations are inputs: every removal list (labels of the
+    # N-row index; each round removes and appends nmut, so the size stays N)
+    # is drawn before the timed region, and the harness's record of which
+    # generator row every label holds (for recall) is replayed after it.
+    muts = [np.sort(rng.choice(N, nmut, replace=False)).astype(np.int64)
+            for i in range(args.steps) if i % 10 == 9]
+    done = []
 
     def step(i):
-        nonlocal gen, next_gen, mut_time
+        nonlocal mut_time
         if i >= 0 and i % 10 == 9:  # 1 % removes + 1 % appends every 10 batches
             t0 = time.perf_counter()
-            rm = np.sort(rng.choice(gen.size, nmut, replace=False)).astype(np.int64)
+            rm = muts[len(done)]
             index.remove_ids(rm)
-            gen = np.delete(gen, rm)
-            add = np.arange(next_gen, next_gen + nmut, dtype=np.int64)
-            next_gen += nmut
-            index.append_synthetic_ids(add, seed=1234)
-            gen = np.concatenate([gen, add])
+            g0 = N + len(done) * nmut
+            index.append_synthetic_ids(np.arange(g0, g0 + nmut, dtype=np.int64), seed=1234)
+            done.append(rm)
             mut_time += time.perf_counter() - t0
         j = (max(i, 0) * B) % (xq.shape[0] - B + 1)
         return index.search_device(xq[j:j + B], k, stream=ctx.stream)
 
     elapsed, kms, nl, _ = ctx.timed(step, args.steps, args.warmup)
+    gen = np.arange(N, dtype=np.int64)  # generator row of every current label
+    for r, rm in enumerate(done):
+        g0 = N + r * nmut
+        gen = np.concatenate([np.delete(gen, rm), np.arange(g0, g0 + nmut, dtype=np.int64)])
     assert index.ntotal == gen.size
     n_shard = index.shard.ntotal
     esz = 2 if args.dtype == "bf16" else 4

@@ -1694,24 +1694,39 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
   VS_HIP(scr.alloc((void**)&drm, (size_t)nrem * sizeof(int64_t)), "vs_remove_ids: scratch");
   VS_HIP(hipMemcpyAsync(drm, rm.data(), (size_t)nrem * sizeof(int64_t), hipMemcpyHostToDevice, st),
          "vs_remove_ids: upload");
-  // Chunked stable compaction from the first removed row on: each chunk's kept
-  // rows are packed into scratch, then copied down to their final position.
-  // Destinations never exceed the chunk's own source range, and earlier chunks
-  // are already consumed, so the in-place move is safe with O(chunk) scratch.
+  // Chunked stable compaction from the first removed row on.  A chunk whose
+  // rows move down by at least its own length (`before`, the removed rows
+  // below it, >= its row count) is packed straight to its final position: its
+  // destinations lie below its sources, in rows earlier chunks have already
+  // consumed (stream order).  Otherwise (near the first removed row, where the
+  // shift is small) the kept rows are packed into scratch, then copied down.
+  // Once the shift reaches kDirectMin rows, chunks are cut to the shift so
+  // every later chunk takes the direct path (half the bytes moved).
   const int64_t chunk = std::max<int64_t>(1024, (int64_t)(256ull << 20) / idx->rowbytes());
+  constexpr int64_t kDirectMin = 16384;
   char* tmp = nullptr;
   float* tmpn = nullptr;
-  VS_HIP(scr.alloc((void**)&tmp, (size_t)chunk * idx->rowbytes()), "vs_remove_ids: scratch");
-  VS_HIP(scr.alloc((void**)&tmpn, (size_t)chunk * sizeof(float)), "vs_remove_ids: scratch");
   const int64_t first = rm[0];
-  for (int64_t s0 = first; s0 < idx->ntotal; s0 += chunk) {
-    const int64_t cn = std::min(chunk, idx->ntotal - s0);
+  for (int64_t s0 = first, cn = 0; s0 < idx->ntotal; s0 += cn) {
     const int64_t before = std::lower_bound(rm.begin(), rm.end(), s0) - rm.begin();
+    cn = std::min(chunk, idx->ntotal - s0);
+    const bool direct = before >= cn || before >= kDirectMin;
+    if (direct) cn = std::min(cn, before);
     const int64_t in_chunk = std::lower_bound(rm.begin(), rm.end(), s0 + cn) - rm.begin() - before;
     const int64_t kept = cn - in_chunk;
     const int64_t dst = s0 - before;
-    VS_HIP(launch_gather_kept(idx->codes, idx->norms, idx->rowbytes(), s0, cn, drm, nrem, tmp, tmpn,
-                              st),
+    if (direct) {
+      VS_HIP(launch_gather_kept(idx->codes, idx->norms, idx->rowbytes(), s0, cn, drm + before,
+                                in_chunk, idx->row(dst), idx->norms + dst, st),
+             "vs_remove_ids: move rows");
+      continue;
+    }
+    if (!tmp) {
+      VS_HIP(scr.alloc((void**)&tmp, (size_t)chunk * idx->rowbytes()), "vs_remove_ids: scratch");
+      VS_HIP(scr.alloc((void**)&tmpn, (size_t)chunk * sizeof(float)), "vs_remove_ids: scratch");
+    }
+    VS_HIP(launch_gather_kept(idx->codes, idx->norms, idx->rowbytes(), s0, cn, drm + before,
+                              in_chunk, tmp, tmpn, st),
            "vs_remove_ids: gather");
     if (kept > 0) {
       VS_HIP(hipMemcpyAsync(idx->row(dst), tmp, (size_t)kept * idx->rowbytes(),

@@ -93,18 +93,8 @@ constexpr int kDumpMaxR = 64;         // dump slots (candidate rows) per lane li
 #ifndef VS_X1_SCHED_I8
 #define VS_X1_SCHED_I8 0
 #endif
-#ifndef VS_X1_PRIO_SEG
-#define VS_X1_PRIO_SEG 0
-#endif
-// 3 = the segmented schedule with the query fragments in registers (A/B:
-// VS_X1_QREG mask, 1 = int8 dump launches, 2 = bf16 dump launches)
-#ifndef VS_X1_QREG
-#define VS_X1_QREG 0
-#endif
 constexpr int x1_sched(int el, bool dump) {
-  return el != FILTER_I8 ? ((dump && (VS_X1_QREG & 2)) ? 3 : 2)
-         : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8
-         : dump ? ((VS_X1_QREG & 1) ? 3 : 2) : 1;
+  return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump ? 2 : 1;
 }
 // The passes with a dump form: inner product on either plane (every key
 // follows from the raw sum and, for int8, the row factor the replay reads).
@@ -819,91 +809,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       buf = nbuf;
     }
 #undef VS_X1_MARK1
-    } else if constexpr (kSched == 3) {
-    // Register-Q schedule: the segmented schedule below with each lane's query
-    // fragments loaded from the tile-major query plane straight into registers
-    // (four 16-B loads per lane and step: chunks h and 2 + h of rows 64 wq + c32
-    // and + 32), one step ahead into the other of two register sets, instead
-    // of staged through LDS — two LDS-DMA pieces per wave and step instead of
-    // four, eight fragment reads instead of twelve.  The loads are inline asm
-    // like the DMA pieces (hipcc counts neither), retired by the same counted
-    // wait: in issue order a step issues Q(s+1) then X(s+3), so vmcnt(8) (the
-    // younger X(s+2), Q(s+1), X(s+3)) retires Q(s) and X(s+1).  The register
-    // set a load refills was last read by the previous step's MFMAs, issued
-    // before that step's closing barrier.
-    static_assert(NBUF == 5, "3 steps in flight over 5 images");
-    const char* qsrc = QH + (int64_t)(qtile0 + qt) * nksteps * kStepB;
-    const uint32_t qoff = (uint32_t)(64 * wq + c32) * 64u + (uint32_t)h * 16u;
-    int qk = 0;  // the K step of the next query load
-    i32x4 qr0[4], qr1[4];
-    auto qload = [&](i32x4 (&q)[4]) {
-      const char* b = qsrc + (int64_t)qk * kStepB;
-      asm volatile(
-          "global_load_dwordx4 %0, %4, %5\n\t"
-          "global_load_dwordx4 %1, %4, %5 offset:32\n\t"
-          "global_load_dwordx4 %2, %4, %5 offset:2048\n\t"
-          "global_load_dwordx4 %3, %4, %5 offset:2080"
-          : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3])
-          : "v"(qoff), "s"(b)
-          : "memory");
-      if (++qk == nksteps) qk = 0;
-    };
-    auto rdx = [&](int buf, int s2, uint4 (&fa)[4]) {
-      const char* cX = smem + buf * 2 * kStepB + (128 * wr + c32) * 64 + ((2 * s2 + h) ^ fsw) * 16;
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
-    };
-    auto stage_x = [&]() {
-      stage_piece(0);
-      stage_piece(2);
-      advance_cursor();
-    };
-    stage_x();      // X(0)
-    stage_x();      // X(1)
-    qload(qr0);     // Q(0)
-    stage_x();      // X(2)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // X(0)
-    __builtin_amdgcn_s_barrier();
-    const bool lag = w >= 4;
-    if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
-    int buf = 0, t = t0, ks = 0;
-    auto step = [&](const i32x4 (&qc)[4], i32x4 (&qn)[4]) {
-      __builtin_amdgcn_sched_barrier(0);
-      rdx(buf, 0, fa0);
-      rdx(buf, 1, fa1);
-      __builtin_amdgcn_sched_barrier(0);
-      qload(qn);  // Q(s+1)
-      stage_x();  // X(s+3)
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Q(s), X(s+1)
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      const uint4 q0[2] = {__builtin_bit_cast(uint4, qc[0]), __builtin_bit_cast(uint4, qc[2])};
-      const uint4 q1[2] = {__builtin_bit_cast(uint4, qc[1]), __builtin_bit_cast(uint4, qc[3])};
-      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, q0);
-      } else {
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa0, q0);
-      }
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, q1);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (++ks == nksteps) {  // beside the partner's matrix segment
-        ks = 0;
-        epilogue(t);
-        ++t;
-      }
-      buf = buf + 1 == NBUF ? 0 : buf + 1;
-    };
-    for (int s = 0; s < nsteps; s += 2) {
-      step(qr0, qr1);
-      if (s + 1 < nsteps) step(qr1, qr0);  // uniform
-    }
-    if (!lag) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
     } else {
     // Segmented schedule: every step of a wave is a LOAD segment (the step's 12
     // fragment reads, the 4 LDS-DMA pieces of step s+3, the wait for this
@@ -920,7 +825,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // wave's counted wait for its pieces.
     // (4 steps in flight, each load segment closed by an lgkmcnt(0) so the
     // image a DMA refills could be the one read a barrier earlier: C3 70.2k vs
-    // 70.8k queries/s, C2 -3 %, C4 -2 %: not shipped)
+    // 70.8k queries/s, C2 -3 %, C4 -2 %: not shipped.  The query fragments
+    // loaded straight into registers, one step ahead, instead of through LDS
+    // (half the DMA pieces, two thirds of the fragment reads): C3 +0.3 %, so
+    // the cost is the bytes entering the CU, not the LDS path; s_setprio on
+    // either half: -0.1 %; profiles/r04n/ab_qreg_prio.txt: not shipped)
     static_assert(NBUF == 5, "segmented schedule: 3 steps in flight over 5 images");
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -932,9 +841,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     __builtin_amdgcn_s_barrier();
     const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
-    // A/B builds only: a static priority for one half (1 = the lagging waves
-    // 4-7, 2 = waves 0-3; MI355X_MICROARCH.md "Two waves per SIMD" item 4)
-    if ((VS_X1_PRIO_SEG == 1 && lag) || (VS_X1_PRIO_SEG == 2 && !lag)) __builtin_amdgcn_s_setprio(1);
     int buf = 0, t = t0, ks = 0;
 #if VS_X1_STAMP
     tA = stamp_now();

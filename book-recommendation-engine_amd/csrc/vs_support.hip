@@ -690,36 +690,37 @@ __device__ __forceinline__ int64_t count_less(const int64_t* a, int64_t n, int64
   return lo;
 }
 
-// One wave per source row: kept rows of [src0, src0+n) are packed, in order,
-// into tmp (and their norms into tmp_norms).
+// One wave per source row: the kept rows of [src0, src0+n) are packed, in
+// order, into out (and their norms into out_norms).  removed holds the sorted
+// removed rows of that range only (a slice of the whole list), so a row's
+// packed position is i minus the removed rows below it in the slice.
 __global__ __launch_bounds__(256) void gather_kept_kernel(const char* __restrict__ X,
                                                           const float* __restrict__ norms,
                                                           int64_t rowbytes, int64_t src0,
                                                           int64_t n,
                                                           const int64_t* __restrict__ removed,
-                                                          int64_t nrem, char* __restrict__ tmp,
-                                                          float* __restrict__ tmp_norms) {
+                                                          int64_t nrem, char* __restrict__ out,
+                                                          float* __restrict__ out_norms) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const int64_t row = src0 + i;
-  const int64_t before_row = count_less(removed, nrem, row);
-  if (before_row < nrem && removed[before_row] == row) return;  // removed
-  const int64_t before_src0 = count_less(removed, nrem, src0);
-  const int64_t dst = i - (before_row - before_src0);
+  const int64_t b = count_less(removed, nrem, row);
+  if (b < nrem && removed[b] == row) return;  // removed
+  const int64_t dst = i - b;
   const uint4* s = (const uint4*)(X + row * rowbytes);
-  uint4* dd = (uint4*)(tmp + dst * rowbytes);
+  uint4* dd = (uint4*)(out + dst * rowbytes);
   for (int64_t c = lane; c < (rowbytes >> 4); c += 64) dd[c] = s[c];
-  if (lane == 0) tmp_norms[dst] = norms[row];
+  if (lane == 0) out_norms[dst] = norms[row];
 }
 
 hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbytes, int64_t src0,
-                              int64_t n, const int64_t* removed, int64_t nrem, void* tmp,
-                              float* tmp_norms, hipStream_t st) {
+                              int64_t n, const int64_t* removed, int64_t nrem, void* out,
+                              float* out_norms, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st,
-                     (const char*)X, norms, rowbytes, src0, n, removed, nrem, (char*)tmp,
-                     tmp_norms);
+                     (const char*)X, norms, rowbytes, src0, n, removed, nrem, (char*)out,
+                     out_norms);
   return hipGetLastError();
 }
 

@@ -325,6 +325,34 @@ def test_remove_many_chunks(vf):
         np.testing.assert_array_equal(index.reconstruct(r), synthetic_rows(keep[r], 1, d, 77)[0])
 
 
+def test_remove_packs_in_place_once_the_shift_covers_a_chunk(vf):
+    """The compaction's two forms (vs_remove_ids): a dense run of 24,000
+    removed rows first (scratch chunk of 43,690 rows: the shift is smaller
+    than the chunk), then every 9th row, moved straight to their final rows
+    in chunks cut to the shift.  Every kept row, its norm (L2 keys) and the
+    int8 plane (re-derived from the moved rows) are checked."""
+    d, n = 1536, 120_000
+    rng = np.random.default_rng(41)
+    xb = rng.standard_normal((n, d), dtype=np.float32)
+    index = vf.IndexFlatL2(d)
+    index.add(xb)
+    rm = np.concatenate([np.arange(500, 24_500), np.arange(24_500, n, 9)]).astype(np.int64)
+    assert index.remove_ids(rm[::-1].copy()) == rm.size
+    xr, nr = flat.remove_ids(xb, rm)
+    assert nr == rm.size and index.ntotal == n - rm.size
+    np.testing.assert_array_equal(index.reconstruct_n(0, index.ntotal), xr)
+    xq = rng.standard_normal((16, d), dtype=np.float32)
+    D, I = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xr, xq, 10, L2)
+    assert not flat.mismatches(D, I, Dr, Ir, L2, xr, xq)
+    ip = vf.IndexFlatIP(d)
+    ip.add(xb)
+    ip.remove_ids(rm)
+    D, I = ip.search(xq, 10)  # the filter engine on the re-derived int8 plane
+    Dr, Ir = flat.knn_exact(xr, xq, 10, flat.METRIC_INNER_PRODUCT)
+    assert not flat.mismatches(D, I, Dr, Ir, flat.METRIC_INNER_PRODUCT, xr, xq)
+
+
 def test_synthetic_generator_matches_host(vf):
     from vsearch.synth import synthetic_rows
 
