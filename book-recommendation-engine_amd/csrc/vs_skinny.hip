@@ -10,15 +10,19 @@
 //
 // Geometry (16x16 C/D layout: column = lane & 15, row = 4 * (lane >> 4) + reg):
 //   A = 16 database rows, B = 16 queries.  A workgroup (4 waves) owns a tile of
-//   256 rows (64 per wave = 4 row groups of 16) against all the batch's queries
-//   and walks K in 128-B slices: global_load_lds_dwordx4 stages 8 rows x 128 B per
-//   wave instruction (whole cache lines, double-buffered), and fragments are read
-//   from LDS with the same XOR swizzle as the GEMM (16-B chunk c of row r at
-//   c ^ ((r >> 1) & 7): conflict-free ds_read_b128).  Per 64-B k-chunk, lane l
+//   128 rows (32 per wave = 2 row groups of 16) against all the batch's queries
+//   and walks K in 128-B slices: LDS-DMA (global_load_lds_dwordx4) stages 8 rows
+//   x 128 B per wave instruction (whole cache lines) into a ring of NB slice
+//   images, NB - 1 slices in flight (two workgroups per CU: ~110 KB of loads in
+//   flight per CU, what HBM needs at this latency; the round-2 form, 256-row
+//   tiles double-buffered, held 64 KB and reached 0.78 of HBM at C5).  Fragments
+//   are read from LDS with the same XOR swizzle as the GEMM (16-B chunk c of
+//   row r at c ^ ((r >> 1) & 7): conflict-free ds_read_b128).  Per 64-B
+//   k-chunk, lane l
 //   takes the 16 B at chunk offset 16 * (l >> 4) of row l & 15 — of the X row for
 //   A, of query row l & 15 for B.  fp32: the 4 floats feed 4 MFMAs (instruction t
 //   uses element t, so lane group g covers k = 4g + t); bf16: the 8 bf16 are the
-//   operand (k = 8g + j).  Each query fragment serves all 4 row groups.
+//   operand (k = 8g + j).  Each query fragment serves both row groups.
 //   After the K loop lane l holds, for query l & 15 (+16 for the second query
 //   group), the scores of rows rowbase + 16 * grp + 4 * (l >> 4) + reg: 4 lanes
 //   share a query, each with its own register list; the block folds its 16
@@ -29,6 +33,28 @@ namespace vs {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// LDS-DMA of 16 B per lane into the wave-uniform LDS byte address `lds` (M0 set
+// and restored inside the statement), from a uniform base plus a 32-bit lane
+// offset.  hipcc does not count it: the K loop retires the slices with counted
+// waits of its own (the builtin form would make hipcc drain vmcnt to 0 before
+// every LDS read, i.e. one slice in flight).
+__device__ __forceinline__ void skinny_glds(const void* sbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+
+constexpr int kSkinnyRows = 128;  // database rows per tile (32 per wave)
+
+// slice images in the ring: 4 for one query group (4 x 18 KB per workgroup),
+// 3 for two (4 x 20 KB would not leave two workgroups per CU)
+template <int NQG>
+constexpr int skinny_nbuf() { return NQG == 1 ? 4 : 3; }
+
 template <int KP, int MODE, typename T, int NQG>
 __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
                                                       const float* __restrict__ xaux,
@@ -38,14 +64,18 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
                                                       float* __restrict__ pkey,
                                                       int* __restrict__ pid) {
   static_assert(KP <= 32, "skinny path keeps at most 32 entries per list");
-  // LDS, three lives: [2 buffers][256 X rows + 16*NQG query rows][128 B] during
-  // the K loop; per-thread key parking (16 x 256 floats) in the epilogue; the
-  // per-query list fold ([16 queries][16 lists][KP] keys + ids) at the end.
-  constexpr int kRowsPerBuf = 256 + 16 * NQG;
-  constexpr int kStageWords = 2 * kRowsPerBuf * 32;
+  constexpr int NB = skinny_nbuf<NQG>();
+  constexpr int R = kSkinnyRows;
+  // LDS, three lives: [NB images][128 X rows + 16*NQG query rows][128 B] during
+  // the K loop; per-thread key parking (8 x 256 floats) in the epilogue (every
+  // slice retired by then); the per-query list fold ([16 queries][16 lists][KP]
+  // keys + ids) at the end.
+  constexpr int kRowsPerBuf = R + 16 * NQG;
+  constexpr int kStageWords = NB * kRowsPerBuf * 32;
   constexpr int kFold = 16 * 16 * KP;
   constexpr int kWords0 = kStageWords > 2 * kFold ? kStageWords : 2 * kFold;
-  constexpr int kWords = kWords0 > 16 * 256 ? kWords0 : 16 * 256;
+  constexpr int kWords = kWords0 > 8 * 256 ? kWords0 : 8 * 256;
+  static_assert(2 * kWords * 4 <= 160 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) float lds[kWords];
   float* spark = lds;
   float* mk = lds;
@@ -53,11 +83,12 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int w = tid >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;  // lane group: 16-B offset inside a 64-B k-chunk
   const int c16 = lane & 15;
   const int nslice = (int)(ld * (int64_t)sizeof(T) / 128);
   const uint32_t ldb = (uint32_t)(ld * (int64_t)sizeof(T));
+  const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(lds);
 
   float qa[NQG];
   int qcol[NQG];
@@ -75,7 +106,7 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
 
   const int rb0 = blockIdx.x * rows_per_block;
   const int rb1 = min(rb0 + rows_per_block, (ntotal + 255) & ~255);
-  // glds geometry: lane L of a wave instruction moves 16 B of row (L >> 3) of an
+  // DMA geometry: lane L of a wave instruction moves 16 B of row (L >> 3) of an
   // 8-row group; the swizzle depends on the group only through its parity.
   const int srow = lane >> 3;
   uint32_t soff[2];
@@ -85,54 +116,59 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
     soff[par] = (uint32_t)srow * ldb + (uint32_t)((lane & 7) ^ ((row >> 1) & 7)) * 16u;
   }
   const int fsw = (c16 >> 1) & 7;  // fragment rows 16*grp + c16 share (row >> 1) & 7
+  // the query piece this wave stages per slice: 2 NQG pieces of 8 rows over the
+  // 4 waves, every wave one (NQG = 1: two waves per piece, identical bytes to
+  // identical LDS addresses), so every wave issues 5 loads per slice and one
+  // counted wait serves all of them
+  const int qpc = NQG == 1 ? (w & 1) : w;
 
-  for (int tb = rb0; tb < rb1; tb += 256) {
-    f32x4v acc[NQG][4];
+  for (int tb = rb0; tb < rb1; tb += R) {
+    f32x4v acc[NQG][2];
 #pragma unroll
     for (int qg = 0; qg < NQG; ++qg)
 #pragma unroll
-      for (int grp = 0; grp < 4; ++grp) acc[qg][grp] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-    const char* xt = (const char*)(X + (int64_t)(tb + 64 * w) * ld);
+      for (int grp = 0; grp < 2; ++grp) acc[qg][grp] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+    const char* xt = (const char*)(X + (int64_t)(tb + 32 * w) * ld);
 
-    auto stage = [&](int buf, int sl) {
-      float* base = lds + buf * kRowsPerBuf * 32;
+    auto stage = [&](int sl) {
+      const uint32_t base = lds0 + (uint32_t)((sl % NB) * kRowsPerBuf * 128);
       const char* xs = xt + sl * 128;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)  // this wave's 64 rows
-        __builtin_amdgcn_global_load_lds(xs + soff[i & 1] + (uint32_t)(i * 8) * ldb,
-                                         VS_LDS(base + (64 * w + 8 * i) * 32), 16, 0, 0);
-      // query rows: 2 instructions per query group, spread over the waves
-#pragma unroll
-      for (int i = 0; i < 2 * NQG; ++i) {
-        if (w == (i & 3)) {
-          const char* qs = (const char*)Q + sl * 128;
-          __builtin_amdgcn_global_load_lds(qs + soff[i & 1] + (uint32_t)(i * 8) * ldb,
-                                           VS_LDS(base + (256 + 8 * i) * 32), 16, 0, 0);
-        }
-      }
+      for (int i = 0; i < 4; ++i)  // this wave's 32 rows
+        skinny_glds(xs, soff[i & 1] + (uint32_t)(i * 8) * ldb,
+                    __builtin_amdgcn_readfirstlane(base + (uint32_t)(32 * w + 8 * i) * 128u));
+      skinny_glds((const char*)Q + sl * 128, soff[qpc & 1] + (uint32_t)(qpc * 8) * ldb,
+                  __builtin_amdgcn_readfirstlane(base + (uint32_t)(R + 8 * qpc) * 128u));
     };
 
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // slices 0 .. NB-2 in flight, then retire slice 0
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i)
+      if (i < nslice) stage(i);  // uniform
+    if (nslice >= 3 && NB >= 4) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (nslice >= 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int sl = 0; sl < nslice; ++sl) {
-      if (sl + 1 < nslice) stage((sl + 1) & 1, sl + 1);
-      const float* cb = lds + (sl & 1) * kRowsPerBuf * 32;
+      // slice sl+NB-1 into the image slice sl-1 used (every wave passed the
+      // barrier after reading it)
+      if (sl + NB - 1 < nslice) stage(sl + NB - 1);
+      const float* cb = lds + (sl % NB) * kRowsPerBuf * 32;
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int coff = ((4 * c + g) ^ fsw) * 4;  // in floats
         f32x4v qf[NQG];
 #pragma unroll
         for (int qg = 0; qg < NQG; ++qg)
-          qf[qg] = *(const f32x4v*)(cb + (256 + 16 * qg + c16) * 32 + coff);
-        f32x4v xf[4];
+          qf[qg] = *(const f32x4v*)(cb + (R + 16 * qg + c16) * 32 + coff);
+        f32x4v xf[2];
 #pragma unroll
-        for (int grp = 0; grp < 4; ++grp)
-          xf[grp] = *(const f32x4v*)(cb + (64 * w + 16 * grp + c16) * 32 + coff);
+        for (int grp = 0; grp < 2; ++grp)
+          xf[grp] = *(const f32x4v*)(cb + (32 * w + 16 * grp + c16) * 32 + coff);
 #pragma unroll
         for (int qg = 0; qg < NQG; ++qg) {
 #pragma unroll
-          for (int grp = 0; grp < 4; ++grp) {
+          for (int grp = 0; grp < 2; ++grp) {
             if constexpr (sizeof(T) == 4) {
 #pragma unroll
               for (int t = 0; t < 4; ++t)
@@ -146,12 +182,16 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
           }
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // retire slice sl+1: the slices issued after it stay in flight
+      const int younger = min(sl + NB - 1, nslice - 1) - (sl + 1);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
 
-    // Epilogue: keys, 16-bit candidate mask per query group, park + insert.
-    const int r = tb + 64 * w;
+    // Epilogue: keys, 8-bit candidate mask per query group, park + insert.
+    const int r = tb + 32 * w;
 #pragma unroll
     for (int qg = 0; qg < NQG; ++qg) {
       const float tk = lk[qg][KP - 1];
@@ -159,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
       const bool qvalid = qcol[qg] < nq;
       uint32_t m = 0;
 #pragma unroll
-      for (int grp = 0; grp < 4; ++grp) {
+      for (int grp = 0; grp < 2; ++grp) {
         const int rowb = r + 16 * grp + 4 * g;
         f32x4v xa = {0.f, 0.f, 0.f, 0.f};
         if constexpr (MODE == MODE_L2) xa = *(const f32x4v*)(xaux + rowb);
@@ -174,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
       }
       if (m) {
 #pragma unroll
-        for (int grp = 0; grp < 4; ++grp)
+        for (int grp = 0; grp < 2; ++grp)
 #pragma unroll
           for (int i = 0; i < 4; ++i) spark[(grp * 4 + i) * 256 + tid] = acc[qg][grp][i];
         do {
@@ -185,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
         } while (m);
       }
     }
-    __syncthreads();  // the next tile's first stage overwrites the parking area
+    __syncthreads();  // the next tile's first slices overwrite the parking area
   }
 
   // Fold the 16 lists of each query (4 lane groups x 4 waves) in LDS, one

@@ -690,10 +690,13 @@ __device__ __forceinline__ int64_t count_less(const int64_t* a, int64_t n, int64
   return lo;
 }
 
-// One wave per source row: the kept rows of [src0, src0+n) are packed, in
-// order, into out (and their norms into out_norms).  removed holds the sorted
-// removed rows of that range only (a slice of the whole list), so a row's
-// packed position is i minus the removed rows below it in the slice.
+// The kept rows of [src0, src0+n) packed, in order, into out (and their norms
+// into out_norms).  removed holds the sorted removed rows of that range only (a
+// slice of the whole list).  One workgroup per 64 consecutive rows: two binary
+// searches bound the block's removed entries, which flag their rows in LDS; a
+// ballot over the flags gives every kept row its packed position; then each
+// wave copies 16 rows, 16 B per lane (no per-row search on the copy's path).
+constexpr int kKeptRows = 64;
 __global__ __launch_bounds__(256) void gather_kept_kernel(const char* __restrict__ X,
                                                           const float* __restrict__ norms,
                                                           int64_t rowbytes, int64_t src0,
@@ -701,24 +704,41 @@ __global__ __launch_bounds__(256) void gather_kept_kernel(const char* __restrict
                                                           const int64_t* __restrict__ removed,
                                                           int64_t nrem, char* __restrict__ out,
                                                           float* __restrict__ out_norms) {
-  const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
-  const int64_t row = src0 + i;
-  const int64_t b = count_less(removed, nrem, row);
-  if (b < nrem && removed[b] == row) return;  // removed
-  const int64_t dst = i - b;
-  const uint4* s = (const uint4*)(X + row * rowbytes);
-  uint4* dd = (uint4*)(out + dst * rowbytes);
-  for (int64_t c = lane; c < (rowbytes >> 4); c += 64) dd[c] = s[c];
-  if (lane == 0) out_norms[dst] = norms[row];
+  __shared__ int64_t bound[2];
+  __shared__ int flag[kKeptRows];
+  __shared__ int64_t dsts[kKeptRows];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * kKeptRows;
+  const int64_t r0 = src0 + i0;
+  if (tid < 2) bound[tid] = count_less(removed, nrem, r0 + (tid ? kKeptRows : 0));
+  if (tid < kKeptRows) flag[tid] = 0;
+  __syncthreads();
+  const int64_t lo = bound[0], hi = bound[1];
+  for (int64_t j = lo + tid; j < hi; j += blockDim.x) flag[(int)(removed[j] - r0)] = 1;
+  __syncthreads();
+  if (w == 0) {
+    const bool rm = flag[lane] != 0;
+    const uint64_t m = __ballot(rm);
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    dsts[lane] = rm || i0 + lane >= n ? -1 : i0 + lane - (lo + below);
+  }
+  __syncthreads();
+  const int64_t nv = rowbytes >> 4;
+  for (int r = w; r < kKeptRows; r += 4) {
+    const int64_t dst = dsts[r];
+    if (dst < 0) continue;  // uniform over the wave
+    const uint4* src = (const uint4*)(X + (r0 + r) * rowbytes);
+    uint4* dd = (uint4*)(out + dst * rowbytes);
+    for (int64_t c = lane; c < nv; c += 64) dd[c] = src[c];
+    if (lane == 0) out_norms[dst] = norms[r0 + r];
+  }
 }
 
 hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbytes, int64_t src0,
                               int64_t n, const int64_t* removed, int64_t nrem, void* out,
                               float* out_norms, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st,
+  hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + kKeptRows - 1) / kKeptRows)), dim3(256), 0, st,
                      (const char*)X, norms, rowbytes, src0, n, removed, nrem, (char*)out,
                      out_norms);
   return hipGetLastError();
