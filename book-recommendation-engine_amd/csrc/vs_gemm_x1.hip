@@ -1010,26 +1010,36 @@ static int x1_qg() {
 
 static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
 
-// Database tiles per workgroup per launch (env VS_X1_CHUNK_TILES overrides the
-// default, read at every search: A/B runs, and tests that need multi-launch
-// passes on small indexes)
-static int x1_chunk_tiles() {
+// Database tiles per workgroup per launch for a pass of per_block tiles per
+// workgroup: 64, or 32 for a pass that can dump and has 128-192 tiles per
+// workgroup, which 64-tile launches would cut into fewer than 4 (no dumps) and
+// 32-tile ones into 4-6 (one list launch, the rest dumps): a 1.25M-row shard
+// at 16 query tiles (C3 over 8 GPUs), 153 tiles: 435k vs 423k queries/s; with
+// 305 tiles (2.5M rows) and at C3, 32-tile launches lose 2 % and 1 %
+// (profiles/r04t/ab_chunk.txt).  Env VS_X1_CHUNK_TILES overrides both (read at
+// every search: A/B runs, and tests that need multi-launch passes on small
+// indexes).
+static int x1_chunk_tiles(int per_block, bool can_dump) {
   const char* e = getenv("VS_X1_CHUNK_TILES");
   const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : kX1ChunkTiles;
+  if (v > 0) return v;
+  return can_dump && per_block >= 128 && per_block <= 3 * kX1ChunkTiles ? kX1ChunkTiles / 2
+                                                                        : kX1ChunkTiles;
 }
 
 template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
   const int nqt = a.nq_pad / kT;
-  const int chunk_tiles = x1_chunk_tiles();
   const int per_block = (ntiles + a.nsplit - 1) / a.nsplit;
   // A gathered later stage holds its few queries in the first query tile(s):
   // every XCD takes every query tile there (QG = nqt), so the working
   // workgroups of tile 0 spread over all XCDs instead of the 2 of 8 that QG = 4
   // gives it (clustered C3: 202 -> 151 ms per step, profiles/r02za).
   const int qg = a.qcount ? nqt : x1_qg();
+  const bool dump = a.dump && x1_has_dump(MODE, EL) && !a.qcount && a.qcut && a.qbkey &&
+                    a.qcut_m > 0 && a.dcount && a.dslot && a.dR > 0;
+  const int chunk_tiles = x1_chunk_tiles(per_block, dump);
   // a gathered later stage (usually empty: its tiles exit at once) is one launch
   int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   // Dump launches after the first: its lists set the cuts (x1_qcut), the rest
@@ -1038,8 +1048,6 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // 4 launches (C3: 20): cutting a short pass into more launches costs more
   // than it saves (C2 forced to 3 launches: 308k vs 394k queries/s,
   // profiles/r04a/r04d_sched_c2_cl_ab.txt).
-  const bool dump = a.dump && x1_has_dump(MODE, EL) && !a.qcount && a.qcut && a.qbkey &&
-                    a.qcut_m > 0 && a.dcount && a.dslot && a.dR > 0;
   const bool dumping = dump && nchunk >= 4;  // x1_pass_dumps
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
@@ -1090,7 +1098,8 @@ int x1_dump_slots() { return kDumpMaxR; }
 bool x1_pass_dumps(int ntotal, int nsplit) {
   const int ntiles = (ntotal + kT - 1) / kT;
   const int per_block = (ntiles + nsplit - 1) / nsplit;
-  return (per_block + x1_chunk_tiles() - 1) / x1_chunk_tiles() >= 4;
+  const int ct = x1_chunk_tiles(per_block, true);
+  return (per_block + ct - 1) / ct >= 4;
 }
 
 hipError_t x1_stamps(unsigned long long* out, int reset) {
