@@ -99,9 +99,13 @@ constexpr int x1_sched(int el, bool dump) {
 // The passes with a dump form: inner product on either plane (every key
 // follows from the raw sum and, for int8, the row factor the replay reads).
 // Not the cosine: its bound is relative (B ~ 2 rho, ~0.02 at d = 1536 for
-// int8), wide beside the similarity spread of high-dimensional rows, so the
-// cut sits behind the lists' own floors and the dumps would overflow (a
-// d = 128 self-join of Gaussian rows: 31 dumps per list); the bf16 L2 /
+// int8), wide beside the similarity spread of high-dimensional rows, so only
+// the lists' own floors hold its dumps down, and its row factors (s_x / |x|)
+// spread widely, so a launch-wide factor bound passes ~70 rows per list and
+// segment (a d = 128 self-join of Gaussian rows: 3M lists past their slots).
+// A form with the list launches' per-group bounds and exact keys before the
+// dump (built, exact) made C4 slower: 439k vs 467k students/s at 4-5
+// launches per pass (profiles/r04w/ab_c4_cosine_dump.txt).  The bf16 L2 /
 // cosine keys also need the row norms in the kernel.
 constexpr bool x1_has_dump(int mode, int el) { return mode == MODE_IP; }
 
