@@ -372,6 +372,26 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       xlane = (uint32_t)((ln >> 2) ^ (f & 0x0C)) * 64u + (uint32_t)((ln & 3) ^ (ln >> 4)) * 16u;
     };
     set_xoff(t0);
+    // Segmented schedule: the load cursor's step as two running uniform
+    // pointers (X: the lower of the wave's two permuted 16-row groups; Q: the
+    // wave's query rows) and a lane offset per X group (both >= 0: the groups
+    // differ in bit 4 of the row), so a step's four pieces cost two 64-bit
+    // adds and one asm block (stage_step) instead of ~40 scalar instructions
+    // of address arithmetic and M0 saves
+    // (inner product only: the bf16 L2 / cosine list kernels have no registers
+    // to spare for the two lane offsets)
+    constexpr bool kSeg = x1_sched(EL, DUMP) == 2 && MODE == MODE_IP;
+    const char* xstep = nullptr;
+    const char* qstep = nullptr;
+    uint32_t xl0 = 0, xl2 = 0;
+    auto set_step_ptrs = [&]() {
+      const int r0 = (32 * w) ^ xhi, r2 = (32 * w + 16) ^ xhi;
+      xstep = XH + ((int64_t)lt * nksteps + lk_) * kStepB + (uint32_t)(r0 & ~16) * 64u;
+      qstep = qtile + (int64_t)lk_ * kStepB;
+      xl0 = xlane + (uint32_t)(r0 & 16) * 64u;
+      xl2 = xlane + (uint32_t)(r2 & 16) * 64u;
+    };
+    if constexpr (kSeg) set_step_ptrs();
 
     // int8 dump launches: one integer threshold per list for the whole launch
     // (its floor is fixed, and the factor bound is the launch's: the maximum
@@ -451,9 +471,44 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         if (++lk_ == nksteps) {
           lk_ = 0;
           set_xoff(++lt);
+          if constexpr (kSeg) set_step_ptrs();
+        } else {
+          if constexpr (kSeg) {
+            xstep += kStepB;
+            qstep += kStepB;
+          }
         }
       }
       lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
+    };
+    // the four pieces of the load cursor's step in stage_piece's order (X
+    // group 0, Q rows 0-15, X group 1, Q rows 16-31); M0 saved once, set per
+    // piece (one wait state before each LDS-DMA reads it).  No instruction
+    // offsets: an LDS-DMA adds its offset to the LDS address as well.
+    auto stage_step = [&]() {
+      if constexpr (!kSeg || (VS_X1_PROBE & (1 | 16 | 32)) != 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stage_piece(i);
+      } else {
+        const uint32_t lx = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)lbuf * (2 * kStepB) +
+                                                           (uint32_t)(2 * w) * 1024u);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %4\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, %5\n\t"
+            "s_add_u32 m0, %4, 0x4000\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %3, %6\n\t"
+            "s_add_u32 m0, %4, 0x400\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %2, %5\n\t"
+            "s_add_u32 m0, %4, 0x4400\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %7, %6\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(xl0), "v"(xl2), "v"(soff), "s"(lx), "s"(xstep), "s"(qstep), "v"(soff + 1024u)
+            : "memory");
+        static_assert(kStepB == 0x4000, "stage_step's M0 offsets");
+      }
     };
 #if VS_X1_STAMP
     unsigned long long ecnt[kStampCnt] = {0, 0, 0};  // only [0] (wave level) is kept
@@ -837,8 +892,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     static_assert(NBUF == 5, "segmented schedule: 3 steps in flight over 5 images");
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) stage_piece(j);
+      stage_step();
       advance_cursor();
     }
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step 0
@@ -857,8 +911,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       rd(buf, 0, fa0, fb0);
       rd(buf, 1, fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) stage_piece(i);
+      stage_step();
       advance_cursor();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(0);
