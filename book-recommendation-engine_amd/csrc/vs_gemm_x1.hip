@@ -468,15 +468,14 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     auto advance_cursor = [&]() {
       if (ls + 1 < nsteps) {
         ++ls;
+        if constexpr (kSeg) {  // a tile change rebuilds them below
+          xstep += kStepB;
+          qstep += kStepB;
+        }
         if (++lk_ == nksteps) {
           lk_ = 0;
           set_xoff(++lt);
           if constexpr (kSeg) set_step_ptrs();
-        } else {
-          if constexpr (kSeg) {
-            xstep += kStepB;
-            qstep += kStepB;
-          }
         }
       }
       lbuf = lbuf + 1 == NBUF ? 0 : lbuf + 1;
