@@ -608,7 +608,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         // memory path: a whole block's 16 sums took five stores and ~4 % of a
         // C3 step, profiles/r04f/stamp_c3_dump.txt).  A list past its dR slots
         // counts on (the replay fails its query).
-        if (__ballot(pass != 0) == 0) return;  // uniform: the usual case
+        // (a block, not an early return: one exit keeps the step loop's
+        // branch to the epilogue a single compare)
+        if (__ballot(pass != 0) != 0) {  // uniform: rare
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
 #pragma unroll
@@ -637,6 +639,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               }
             }
           }
+        }
         }
         VS_X1_EMARK(8);
       } else {
@@ -898,14 +901,18 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     __builtin_amdgcn_s_barrier();
     const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
-    int buf = 0, t = t0, ks = 0;
+    int buf = 0;
 #if VS_X1_STAMP
     tA = stamp_now();
 #define VS_X1_MARK(i) (tB = stamp_now(), sg[i] += tB - tA, tA = tB)
 #else
 #define VS_X1_MARK(i) ((void)0)
 #endif
-    for (int s = 0; s < nsteps; ++s) {
+    // One step; `first` (a tile's first step, which starts its accumulators)
+    // is a compile-time tag: the loops below peel it, so a step carries no
+    // branch on its position in the tile.
+    auto seg_step = [&](auto first_tag) {
+      constexpr bool first = decltype(first_tag)::value;
       __builtin_amdgcn_sched_barrier(0);
       rd(buf, 0, fa0, fb0);
       rd(buf, 1, fa1, fb1);
@@ -920,7 +927,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(2);
-      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
+      if constexpr (first) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, fb0);
       } else {
@@ -934,20 +941,22 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(4);
-      if (++ks == nksteps) {  // beside the partner's matrix segment
-        ks = 0;
-        if constexpr (!VS_X1_P(8)) {
-          epilogue(t);
-        } else {
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
-        }
-        ++t;
-      }
       VS_X1_MARK(5);
       buf = buf + 1 == NBUF ? 0 : buf + 1;
+    };
+    for (int t = t0; t < t1; ++t) {
+      seg_step(std::true_type{});
+      for (int k = 1; k < nksteps; ++k) seg_step(std::false_type{});
+      // the tile's epilogue, beside the partner's matrix segment
+      if constexpr (!VS_X1_P(8)) {
+        epilogue(t);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+      }
+      VS_X1_MARK(5);
     }
     if (!lag) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
 #undef VS_X1_MARK
