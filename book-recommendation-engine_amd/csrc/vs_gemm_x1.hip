@@ -785,7 +785,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     rd(0, 0, fa0, fb0);
-    int buf = 0, t = t0, ks = 0;
+    int buf = 0;
     // The instruction order inside a step is pinned with sched_barrier(0): hipcc
     // would otherwise move the MFMAs across the barrier and the fragment reads
     // next to their first use, undoing the half-step lookahead.
@@ -802,7 +802,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #else
 #define VS_X1_MARK1(i) ((void)0)
 #endif
-    for (int s = 0; s < nsteps; ++s) {
+    // one step; `first` as in the segmented schedule's seg_step (peeled)
+    auto s1_step = [&](auto first_tag) {
+      constexpr bool first = decltype(first_tag)::value;
       const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
       // this wave's pieces of step s+1: the steps s+2 .. s+D-1 stay in flight
       // (the lagging waves wait before this step's first pieces, the others
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_sched_barrier(0);
       // first half: sub-step 0 (fragments read during the previous step), with
       // the sub-step 1 reads of this step's image issued behind two MFMAs
-      if (ks == 0) {  // uniform: a tile's first step starts its accumulators
+      if constexpr (first) {  // a tile's first step starts its accumulators
         mfma_rb_first(0, fa0, fb0);
         __builtin_amdgcn_sched_barrier(0);
         rd(buf, 1, fa1, fb1);
@@ -854,20 +856,21 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
       advance_cursor();
       VS_X1_MARK1(3);
-      if (++ks == nksteps) {
-        ks = 0;
-        if constexpr (!VS_X1_P(8)) {
-          epilogue(t);
-        } else {
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
-        }
-        ++t;
-      }
       VS_X1_MARK1(5);
       buf = nbuf;
+    };
+    for (int t = t0; t < t1; ++t) {
+      s1_step(std::true_type{});
+      for (int k = 1; k < nksteps; ++k) s1_step(std::false_type{});
+      if constexpr (!VS_X1_P(8)) {
+        epilogue(t);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+      }
+      VS_X1_MARK1(5);
     }
 #undef VS_X1_MARK1
     } else {
