@@ -83,15 +83,24 @@ def x1_dominant(ctx, work_total, kms, nl):
     is the same for all of them."""
     mi, ni = ctx.lib.timer_read_kernel("gemm_topk_x1_i8")
     mil, nil = ctx.lib.timer_read_kernel("gemm_topk_x1_i8_list")
+    mip, _ = ctx.lib.timer_read_kernel("gemm_topk_x1_i8_pass")
     mb, nb = ctx.lib.timer_read_kernel("gemm_topk_x1")
     mbl, nbl = ctx.lib.timer_read_kernel("gemm_topk_x1_list")
+    mbp, _ = ctx.lib.timer_read_kernel("gemm_topk_x1_pass")
     per = work_total / max(1, ni + nil + nb + nbl)
     split = {"i8": {"dispatches": ni, "kernel_ms": round(mi, 3)},
              "i8_list_launches": {"dispatches": nil, "kernel_ms": round(mil, 3)},
+             "i8_whole_passes": {"kernel_ms": round(mip, 3)},
              "bf16": {"dispatches": nb, "kernel_ms": round(mb, 3)},
-             "bf16_list_launches": {"dispatches": nbl, "kernel_ms": round(mbl, 3)}}
+             "bf16_list_launches": {"dispatches": nbl, "kernel_ms": round(mbl, 3)},
+             "bf16_whole_passes": {"kernel_ms": round(mbp, 3)}}
+    # the whole pass of the dominant plane: its list and dump launches plus the
+    # cut and replay kernels between them (one span per pass), over the work
+    # of all its launches
     if mi + mil >= mb + mbl:
+        split["whole_pass"] = (per * (ni + nil), mip)
         return "gemm_topk_x1_i8", per * ni, mi, ni, split
+    split["whole_pass"] = (per * (nb + nbl), mbp)
     return "gemm_topk_x1", per * nb, mb, nb, split
 
 
@@ -130,9 +139,10 @@ def parse(argv=None):
                         "clustered rows like text embeddings (1024 centroids, noise 0.5; "
                         "one GPU only) to measure the filter engine's fallback rate")
     p.add_argument("--batch1-steps", type=int, default=20)
-    p.add_argument("--wide-k", type=int, default=60,
-                   help="the service's k (service.py:529-531) for the wide-k leg")
-    p.add_argument("--wide-k-batch", type=int, default=256)
+    p.add_argument("--wide-k", default="30,60",
+                   help="the service's wide k values (service.py:627 k = 30, :529-531 "
+                        "k = 60) for the wide-k leg, comma-separated")
+    p.add_argument("--wide-k-batch", type=int, default=4096)
     p.add_argument("--wide-k-steps", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
@@ -399,8 +409,9 @@ class Ctx:
 
 def dump_record(d, o):
     """The filter pass's dump launches over the timed steps (vs_gemm_x1.hip
-    header): blocks stored below the cuts and lane lists out of slots."""
-    return {"on": os.environ.get("VS_X1_DUMP", "1") != "0", "blocks_dumped": d,
+    header): rows stored below the lists' floors (one (row, raw sum) slot
+    each) and lane lists out of slots."""
+    return {"on": os.environ.get("VS_X1_DUMP", "1") != "0", "rows_dumped": d,
             "lists_out_of_slots": o}
 
 
@@ -459,12 +470,6 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
                           "per fp32 product (bf16 copies of rows and queries), against the dense "
                           "bf16 peak; candidates are then rescored exactly in fp64 and a "
                           "rigorous error bound proves the exact top-k is among them")
-    if kind in ("mfma_x1", "mfma_x1_i8"):
-        # the same algorithmic work (2*N*d per query, exact results) against the
-        # fp32 matrix peak an exact fp32 engine would be bounded by
-        r["fp32_equivalent"] = {"achieved_TFLOPs": round(achieved, 3),
-                                "fp32_matrix_peak": FP32_MFMA_PEAK_TFLOPS,
-                                "ratio": round(achieved / FP32_MFMA_PEAK_TFLOPS, 3)}
     if kind == "mfma_x1_i8":
         r["peak_note"] = ("filter pass of the filter-and-verify engine: one int8 MFMA product "
                           "per fp32 product (int8 codes of rows and queries, one fp32 scale per "
@@ -475,6 +480,20 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
     if traffic_src:
         r["traffic_source"] = traffic_src
     return r
+
+
+def add_whole_pass(rf, split, scale):
+    """`roofline` describes the dump launches alone (the kernel rocprofv3's mean
+    is checked against); `whole_pass` puts the same plane's whole filter pass
+    beside it: list + dump launches + the cut / replay kernels between them,
+    over the algorithmic work of all the pass's launches."""
+    work, ms = split.pop("whole_pass")
+    rf["scope"] = "dump launches of the filter pass only (the dominant kernel)"
+    if ms > 0:
+        ach = work / (ms / 1e3) / scale
+        rf["whole_pass"] = {"achieved": round(ach, 3), "frac": round(ach / rf["peak"], 4),
+                            "kernel_ms": round(ms, 3),
+                            "scope": "list + dump launches + x1_qcut / x1_replay kernels"}
 
 
 class ClusteredRows:
@@ -566,7 +585,8 @@ def run_knn(args, ctx):
         kname, work, kms, nl, split = x1_dominant(ctx, work, kms, nl)
     plane = {"gemm_topk_x1_i8": "i8", "gemm_topk_x1": "bf16"}.get(kname)
     # clustered data runs the bf16 plane at full size: its own PMC summary
-    pmc_key = args.workload + ("cl" if args.data == "clustered" else "")
+    pmc_key = (args.workload + ("cl" if args.data == "clustered" else "")
+               + ("l2" if args.metric == "l2" else ""))
     traffic, tsrc = (pmc_traffic(pmc_key, *rocprof_prefix(kname))
                      if ctx.world == 1 else (None, None))
     if gemv:
@@ -578,6 +598,7 @@ def run_knn(args, ctx):
                       f"2*{n_shard}*{d}*{B} FLOP per search (whole batch over the rank's shard)",
                       kname, traffic, tsrc)
         if split:
+            add_whole_pass(rf, split, scale=1e12)
             rf["first_stage_planes"] = split
 
     batch1 = None
@@ -594,26 +615,30 @@ def run_knn(args, ctx):
                   "frac_hbm_peak": round(bytes1 / kern1 / 1e9 / HBM_PEAK_GBS, 4)
                   if kern1 > 0 else None}
 
-    # The service's wide searches (service.py:529-531: k = 60 over a coalesced
-    # batch): inner-product k > 32 is the two-page exact engine (vs_api.hip
-    # run_wide_k), not the filter pass; measured apart so that engine choice
-    # has a number beside the headline.  Not part of `value`.
+    # The service's wide searches (service.py:627 k = 30, :529-531 k = 60 over
+    # a coalesced batch): inner product's rule reads the 2k - 1 best, i.e. 64
+    # and 128 candidates per query in the filter pass (the two-page exact
+    # engine only for what the filter cannot settle).  Measured apart so that
+    # each k has a number beside the headline; not part of `value`.
     wide = None
-    if (args.wide_k_steps > 0 and metric == vfaiss.METRIC_INNER_PRODUCT
-            and args.wide_k > 32 and not gemv):
+    if (args.wide_k_steps > 0 and metric == vfaiss.METRIC_INNER_PRODUCT and args.wide_k
+            and not gemv):
+        wide = []
         bw = min(args.wide_k_batch, B)
         qw = xq[:bw].contiguous()
-        tw, kw, nw, (Dw, Iw) = ctx.timed(
-            lambda i: index.search_device(qw, args.wide_k, stream=ctx.stream),
-            args.wide_k_steps, 1)
-        Iwh = Iw.cpu().numpy()
-        wide = {"k": args.wide_k, "batch": bw, "steps": args.wide_k_steps,
-                "ms_per_search": round(tw / args.wide_k_steps * 1e3, 3),
-                "queries_per_s": round(args.wide_k_steps * bw / tw, 1),
-                "kernel": ctx.lib.timer_kernel(),
-                "kernel_ms_per_dispatch": round(kw / max(1, nw), 3),
-                "result_sane": bool((Iwh >= 0).all() and (Iwh < args.ntotal).all()),
-                "note": "exact two-page engine (run_wide_k); the filter pass serves k <= 28"}
+        for kw in [int(v) for v in str(args.wide_k).split(",") if v]:
+            ctx.lib.filter_stats(reset=True)
+            tw, kmw, nw, (Dw, Iw) = ctx.timed(
+                lambda i: index.search_device(qw, kw, stream=ctx.stream), args.wide_k_steps, 1)
+            wq, wf = ctx.lib.filter_stats(reset=True)
+            Iwh = Iw.cpu().numpy()
+            wide.append({"k": kw, "batch": bw, "steps": args.wide_k_steps,
+                         "ms_per_search": round(tw / args.wide_k_steps * 1e3, 3),
+                         "queries_per_s": round(args.wide_k_steps * bw / tw, 1),
+                         "kernel": ctx.lib.timer_kernel(),
+                         "kernel_ms_per_dispatch": round(kmw / max(1, nw), 3),
+                         "filter_queries": wq, "exact_redo_queries": wf,
+                         "result_sane": bool((Iwh >= 0).all() and (Iwh < args.ntotal).all())})
 
     if ctx.rank == 0:
         cpu = None
@@ -730,6 +755,7 @@ def run_selfjoin(args, ctx):
                   f"2*{N}*{d}*{nq} FLOP per step ({nq} query rows per rank)",
                   kname, traffic, tsrc)
     if split:
+        add_whole_pass(rf, split, scale=1e12)
         rf["first_stage_planes"] = split
     if ctx.rank == 0:
         # the writer's rows: (a, b, sim) with sim >= threshold (main.py:350-354),

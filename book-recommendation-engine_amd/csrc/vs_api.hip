@@ -53,7 +53,26 @@ struct vs_index {
   // per plane: max |x|^2, max |x - plane(x)|^2, max of their ratio over the
   // rows (the bound's index maxima; grown by add, recomputed by remove_ids)
   unsigned* bstats[2] = {nullptr, nullptr};
-  int64_t planebytes(int p) const { return ld * filter_bytes(p); }
+  // L2 indexes: the int8 plane holds the augmented rows x' = [x, e_1 .. e_m]
+  // whose inner product with q' = [q, C .. C] ranks rows as the L2 key does
+  // (launch_quantize_i8_l2aug); m and C are set by the first add (aug_m = 0
+  // before), anorm[r] = |x'_r|^2 (the int8 plane's bound maxima use it)
+  int aug_m = 0;
+  L2Aug aug;
+  float* anorm = nullptr;
+  // Tombstones (indexes without filter planes, e.g. bf16 storage): removed
+  // rows stay in place, NaN-filled (no kernel admits them), until a pack; faiss
+  // labels are positions among the live rows (searches map their rows through
+  // the sorted dead list, launch_label_map).  ntotal counts the rows in place.
+  std::vector<int64_t> dead;
+  int64_t* ddead = nullptr;  // device copy of `dead`
+  int64_t ddead_cap = 0;
+  int64_t live() const { return ntotal - (int64_t)dead.size(); }
+  bool tombstones() const { return !plane_on[0] && !plane_on[1]; }
+  bool l2aug() const { return metric == VS_METRIC_L2 && esize == 4; }
+  int64_t planebytes(int p) const {
+    return (p == FILTER_I8 && l2aug() ? ld + aug_m : ld) * filter_bytes(p);
+  }
   // Adaptive plane order: the int8 stage pays off while it settles most
   // queries; on data where it hands most of them to bf16 (clustered
   // embeddings) the searches go to bf16 directly, re-probing int8 with an
@@ -359,6 +378,7 @@ struct TimedSpan {
   hipEvent_t a, b;
   int dispatches;
   const char* name;
+  bool aux;  // an extra span over other spans' kernels: not in the unnamed total
 };
 std::vector<TimedSpan> g_timer_events;
 const char* g_timer_kernel = "";
@@ -367,8 +387,8 @@ const char* g_timer_kernel = "";
 // search): [0] queries, [1] flagged by the first check (given to the wide
 // check), [2] flagged by both (redone by the exact engine), [3] handed to a
 // second filter stage, [4] wide-set entries, [5] of them rescored (the rest
-// reuse the first check's keys), [6] blocks stored by dump launches, [7] lane
-// lists out of dump slots.  One buffer per device.
+// reuse the first check's keys), [6] rows stored by dump launches (one
+// (row, raw sum) slot each), [7] lane lists out of dump slots.  One buffer per device.
 constexpr int kStatSlots = 8;
 std::mutex g_stats_mu;
 std::vector<unsigned long long*> g_dev_stats;
@@ -399,12 +419,16 @@ struct KernelTimer {
   hipStream_t st;
   const char* name = nullptr;
   int dispatches = 1;  // kernel launches between the two events
+  bool aux = false;
   // name == nullptr: untimed (the filter engine's exact redo, which is not the
   // kernel the roofline is quoted on)
-  KernelTimer(hipStream_t s, const char* nm) : st(s), name(nm) {
+  // names_kernel: this span names the search's dominant kernel (vs_timer_kernel);
+  // false for an extra span over several kernels (the whole filter pass)
+  KernelTimer(hipStream_t s, const char* nm, bool names_kernel = true) : st(s), name(nm) {
     if (!name) return;
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_kernel = name;
+    if (names_kernel) g_timer_kernel = name;
+    aux = !names_kernel;
     if (!g_timer_on) return;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
       a = b = nullptr;
@@ -416,7 +440,7 @@ struct KernelTimer {
     if (!a) return;
     (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_events.push_back({a, b, dispatches, name});
+    g_timer_events.push_back({a, b, dispatches, name, aux});
     a = b = nullptr;
   }
 };
@@ -445,7 +469,7 @@ struct X1SpanTimer : X1Timing {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
-int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : 64; }
+int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : 128; }
 
 int engine_from_env() {
   const char* e = getenv("VS_ENGINE");
@@ -456,14 +480,47 @@ int engine_from_env() {
   return VS_ENGINE_AUTO;
 }
 
-// Filter planes of a new fp32 index: inner product holds int8 + bf16 (the
-// staged engine), L2 bf16 only (the int8 filter has no L2 form).  Env
-// VS_FILTER=bf16 | i8 keeps only that plane (A/B; i8 only for inner product).
+// Filter planes of a new fp32 index: int8 + bf16 (the staged engine; an L2
+// index's int8 plane holds the augmented rows, vs_index::aug_m).  Env
+// VS_FILTER=bf16 | i8 keeps only that plane (A/B).
 void planes_for(vs_index* idx) {
   const char* e = getenv("VS_FILTER");
-  const bool ip = idx->metric == VS_METRIC_INNER_PRODUCT && idx->esize == 4;
-  idx->plane_on[FILTER_BF16] = idx->esize == 4 && !(ip && e && strcmp(e, "i8") == 0);
-  idx->plane_on[FILTER_I8] = ip && !(e && strcmp(e, "bf16") == 0);
+  const bool f32 = idx->esize == 4;
+  const bool i8able = f32 && (idx->metric == VS_METRIC_INNER_PRODUCT || idx->metric == VS_METRIC_L2);
+  idx->plane_on[FILTER_BF16] = f32 && !(i8able && e && strcmp(e, "i8") == 0);
+  idx->plane_on[FILTER_I8] = i8able && !(e && strcmp(e, "bf16") == 0);
+}
+
+// The augmentation of an L2 index's int8 plane, fixed by its first add (rows
+// [0, n) in place, their norms too): m extra columns and C (l2aug_params),
+// then the plane reallocated at ld + m bytes per row (it holds no row yet).
+int choose_l2aug(vs_index* idx, int64_t n, hipStream_t st) {
+  L2Aug g;
+  VS_HIP(l2aug_params((const float*)idx->codes, idx->ld, 0, n, idx->norms, &g, st),
+         "vs: L2 plane parameters");
+  VS_HIP(hipStreamSynchronize(st), "vs: L2 plane");
+  VS_HIP(wait_readers(idx), "vs: L2 plane");
+  if (idx->fplane[FILTER_I8]) (void)hipFree(idx->fplane[FILTER_I8]);
+  idx->fplane[FILTER_I8] = nullptr;
+  idx->aug_m = g.m;
+  idx->aug = g;
+  hipError_t e = hipMalloc(&idx->fplane[FILTER_I8], (size_t)idx->capacity * idx->planebytes(FILTER_I8));
+  if (e != hipSuccess) {  // no room for the wider plane: the index goes on without it
+    (void)hipGetLastError();
+    idx->fplane[FILTER_I8] = nullptr;
+    idx->plane_on[FILTER_I8] = false;
+    return VS_OK;
+  }
+  VS_HIP(launch_plane_zero_rows(idx->fplane[FILTER_I8], idx->planebytes(FILTER_I8), 0,
+                                idx->capacity, st),
+         "vs: L2 plane");
+  return VS_OK;
+}
+
+// The norms a plane's bound maxima take: |x'|^2 for an L2 index's augmented
+// int8 plane, the stored |x|^2 otherwise.
+const float* plane_norms(const vs_index* idx, int p) {
+  return p == FILTER_I8 && idx->l2aug() && idx->anorm ? idx->anorm : idx->norms;
 }
 
 // The filter plane and residual norms of fp32 rows [r0, r0+n) (after the rows
@@ -475,10 +532,24 @@ int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
     VS_HIP(hipMalloc(&idx->bstats[p], 4 * sizeof(unsigned)), "vs: bound maxima");
     VS_HIP(hipMemsetAsync(idx->bstats[p], 0, 4 * sizeof(unsigned), st), "vs: bound maxima");
   }
-  if (idx->plane_on[FILTER_I8])
+  if (idx->plane_on[FILTER_I8] && idx->l2aug()) {
+    if (idx->aug_m == 0) {  // the first rows fix the augmentation (and the plane's width)
+      const int64_t n0 = r0 + n;
+      int rc = choose_l2aug(idx, n0, st);
+      if (rc) return rc;
+      r0 = 0;
+      n = n0;
+    }
+    if (idx->plane_on[FILTER_I8])
+      VS_HIP(launch_quantize_i8_l2aug((const float*)idx->codes, idx->ld, r0, n, idx->aug,
+                                      idx->norms, (int8_t*)idx->fplane[FILTER_I8], idx->fscale,
+                                      idx->rn2[FILTER_I8], idx->anorm, st),
+             "vs: int8 L2 filter plane");
+  } else if (idx->plane_on[FILTER_I8]) {
     VS_HIP(launch_quantize_i8((const float*)idx->codes, idx->ld, r0, n,
                               (int8_t*)idx->fplane[FILTER_I8], idx->fscale, idx->rn2[FILTER_I8], st),
            "vs: int8 filter plane");
+  }
   if (idx->plane_on[FILTER_BF16]) {
     VS_HIP(launch_bf16_plane((const float*)idx->codes, idx->ld, r0, n,
                              (uint16_t*)idx->fplane[FILTER_BF16], st),
@@ -489,7 +560,8 @@ int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
   // the new rows' maxima fold into the index's (they only grow on add)
   for (int p = 0; p < 2; ++p)
     if (idx->plane_on[p])
-      VS_HIP(launch_bound_stats(idx->norms + r0, idx->rn2[p] + r0, n, idx->bstats[p], st, true),
+      VS_HIP(launch_bound_stats(plane_norms(idx, p) + r0, idx->rn2[p] + r0, n, idx->bstats[p], st,
+                                true),
              "vs: bound maxima");
   return VS_OK;
 }
@@ -506,6 +578,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   char* fplane[2] = {nullptr, nullptr};
   float* rn2[2] = {nullptr, nullptr};
   float* fscale = nullptr;
+  float* anorm = nullptr;
   // the planes the new storage keeps: committed to the index only once the
   // allocation succeeded (a failed growth leaves the index as it was)
   bool on[2] = {idx->plane_on[0], idx->plane_on[1]};
@@ -519,9 +592,11 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
       rn2[p] = nullptr;
     }
     if (fscale) (void)hipFree(fscale);
+    if (anorm) (void)hipFree(anorm);
     codes = nullptr;
     norms = nullptr;
     fscale = nullptr;
+    anorm = nullptr;
   };
   auto allocate = [&](int64_t c) -> hipError_t {
     hipError_t e = hipMalloc(&codes, (size_t)c * idx->rowbytes());
@@ -532,6 +607,8 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     }
     if (e == hipSuccess && on[FILTER_I8])
       e = hipMalloc(&fscale, (size_t)c * sizeof(float));
+    if (e == hipSuccess && on[FILTER_I8] && idx->l2aug())
+      e = hipMalloc(&anorm, (size_t)c * sizeof(float));
     if (e != hipSuccess) {
       (void)hipGetLastError();
       release();
@@ -573,6 +650,9 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   if (i8)
     VS_HIP(hipMemsetAsync(fscale + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
            "vs: zeroing scales");
+  if (anorm)
+    VS_HIP(hipMemsetAsync(anorm + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
+           "vs: zeroing augmented norms");
   if (idx->codes && keep > 0) {
     VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->rowbytes(),
                           hipMemcpyDeviceToDevice, st),
@@ -595,6 +675,10 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
       VS_HIP(hipMemcpyAsync(fscale, idx->fscale, (size_t)keep * sizeof(float),
                             hipMemcpyDeviceToDevice, st),
              "vs: copying scales");
+    if (anorm && idx->anorm)
+      VS_HIP(hipMemcpyAsync(anorm, idx->anorm, (size_t)keep * sizeof(float),
+                            hipMemcpyDeviceToDevice, st),
+             "vs: copying augmented norms");
   }
   // the planes' rows past the kept ones read zeros (after the prefix copy,
   // which brings whole tiles)
@@ -616,6 +700,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     idx->rn2[p] = rn2[p];
   }
   idx->fscale = fscale;
+  idx->anorm = anorm;
   idx->capacity = cap;
   return VS_OK;
 }
@@ -630,9 +715,11 @@ void free_storage(vs_index* idx) {
     idx->rn2[p] = nullptr;
   }
   if (idx->fscale) (void)hipFree(idx->fscale);
+  if (idx->anorm) (void)hipFree(idx->anorm);
   idx->codes = nullptr;
   idx->norms = nullptr;
   idx->fscale = nullptr;
+  idx->anorm = nullptr;
   idx->capacity = 0;
 }
 
@@ -689,6 +776,8 @@ int run_gemm(vs_index* idx, const SearchArgs& a, int need, hipStream_t st,
 }
 
 int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st);
+int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl = nullptr,
+               const int* gc = nullptr);
 int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
                       hipStream_t st, const int* gl, const int* gc);
 
@@ -782,6 +871,11 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const int qa_rows = gathered ? x.nq_pad : a.nq_pad;  // rows of Q / qaux
   // query plane: a conversion of the stage's queries, or the stored rows' plane
   const bool i8 = plane == FILTER_I8;
+  // L2 on the int8 plane: the pass is the inner product of the augmented rows
+  // and queries (vs_index::aug_m); its lists are mapped to L2 keys after it
+  const bool aug = i8 && mode == MODE_L2;
+  if (aug && (idx->aug_m <= 0 || self_rows)) return fail(VS_E_INVALID, "vs: int8 L2 plane");
+  const int kmode = aug ? MODE_IP : mode;  // the pass's own metric
   const int64_t pb = idx->planebytes(plane);
   const char* QH = nullptr;
   const float* qs = nullptr;    // int8: query scales
@@ -803,7 +897,13 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
       float *sc = nullptr, *r = nullptr;
       VS_HIP(scr.alloc((void**)&sc, (size_t)qa_rows * sizeof(float)), "vs: scratch");
       VS_HIP(scr.alloc((void**)&r, (size_t)qa_rows * sizeof(float)), "vs: scratch");
-      VS_HIP(launch_quantize_i8(Q, idx->ld, 0, qa_rows, (int8_t*)qh, sc, r, st), "vs: query plane");
+      if (aug)
+        VS_HIP(launch_quantize_i8_l2aug(Q, idx->ld, 0, qa_rows, idx->aug, nullptr, (int8_t*)qh, sc,
+                                        r, nullptr, st),
+               "vs: query plane");
+      else
+        VS_HIP(launch_quantize_i8(Q, idx->ld, 0, qa_rows, (int8_t*)qh, sc, r, st),
+               "vs: query plane");
       qs = sc;
       qr2 = r;
     } else {
@@ -834,21 +934,25 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   }
   if (i8) {  // the per-lane factor bounds of the fast reject (scalar loads in the kernel)
     float* gm = nullptr;
-    VS_HIP(scr.alloc((void**)&gm, (size_t)(idx->capacity / 16) * sizeof(float)), "vs: scratch");
-    VS_HIP(launch_group_max(x.xs, idx->capacity, gm, st), "vs: factor bounds");
+    const size_t ng = (size_t)(idx->capacity / 16);
+    VS_HIP(scr.alloc((void**)&gm, 2 * ng * sizeof(float)), "vs: scratch");
+    VS_HIP(launch_group_max(x.xs, idx->capacity, gm, st, ntotal, gm + ng), "vs: factor bounds");
     x.xgmax = gm;
+    x.xgmin = gm + ng;
   }
   x.xaux = a.xaux;
   x.QH = QH;
   x.qs = qs;
   x.qaux = qaux;
   x.nqa = qa_rows;
-  x.ld = idx->ld;
+  x.ld = aug ? idx->ld + idx->aug_m : idx->ld;  // the plane's K
   x.ntotal = ntotal;
   x.self0 = self_rows ? a.self0 : -1;
   x.qrow = qrow;
   x.qcount = gc;
-  if (!gathered && x1_dump_applies(mode, plane) && dump_enabled() &&
+  const BoundArgs ba = aug ? make_bound_args_l2aug(idx->ld, idx->aug)
+                           : make_bound_args(idx->ld, plane);
+  if (!gathered && x1_dump_applies(kmode, plane) && dump_enabled() &&
       x1_pass_dumps(ntotal, x.nsplit)) {
     // query cuts + dump launches (vs_gemm_x1.hip header and "Query cuts"): the
     // cuts are set after the pass's first launch and are the verification's
@@ -868,7 +972,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
         VS_HIP(hipMemsetD32Async((hipDeviceptr_t)x.qcut, 0x7f7fffff, (size_t)qa_rows, st),
                "vs: cuts");
         VS_HIP(hipMemsetAsync(dc, 0, (size_t)lists * sizeof(int), st), "vs: dumps");
-        VS_HIP(launch_qbound(mode, Q, idx->ld, qaux, plane, stats, qr2, qa_rows, bk, st),
+        VS_HIP(launch_qbound(mode, Q, idx->ld, qaux, plane, stats, qr2, qa_rows, bk, st, &ba),
                "vs: cuts");
         x.qbkey = bk;
         x.qcut_m = need;
@@ -883,24 +987,37 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     }
   }
   {
+    // the pass as a whole (list + dump launches and the cut / replay kernels
+    // between them) under "<name>_pass", beside the per-launch spans
+    KernelTimer whole(st, gathered ? nullptr : i8 ? "gemm_topk_x1_i8_pass" : "gemm_topk_x1_pass",
+                      false);
     X1SpanTimer tm(i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1",
                    i8 ? "gemm_topk_x1_i8_list" : "gemm_topk_x1_list");
     if (!gathered) x.timing = &tm;
     int nd = 0;
-    VS_HIP(launch_gemm_topk_x1(mode, x, part, st, &nd), "vs: gemm_topk_x1 launch");
+    VS_HIP(launch_gemm_topk_x1(kmode, x, part, st, &nd), "vs: gemm_topk_x1 launch");
     x.timing = nullptr;
+    whole.stop();
   }
+  if (aug)  // augmented inner-product keys A -> L2 keys |q|^2 + 2A (lists and cuts)
+    VS_HIP(launch_l2aug_map(part.key, part.id, (int64_t)part.P * part.KP, qa_rows, qaux,
+                            idx->aug.nref, x.qcut, st),
+           "vs: L2 keys");
 
   // approximate top-KF per query (plain lexicographic order: the L2 merge)
   float* Dk = nullptr;
   int64_t* Ik = nullptr;
   VS_HIP(scr.alloc((void**)&Dk, (size_t)nq * KF * sizeof(float)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&Ik, (size_t)nq * KF * sizeof(int64_t)), "vs: scratch");
-  Partials mp = part;
-  mp.KP = kp_for(KF);
-  mp.KL = L;
-  VS_HIP(launch_merge_partials(MODE_L2, mp, nq, KF, 0, 0.0f, Dk, Ik, KF, st, 0, nullptr, gc),
-         "vs: merge");
+  if (KF > 64) {  // 2k - 1 > 64 (inner product, k > 32): the select kernel
+    VS_HIP(launch_select_lists(part, L, nq, KF, Dk, Ik, st, gc), "vs: merge");
+  } else {
+    Partials mp = part;
+    mp.KP = kp_for(KF);
+    mp.KL = L;
+    VS_HIP(launch_merge_partials(MODE_L2, mp, nq, KF, 0, 0.0f, Dk, Ik, KF, st, 0, nullptr, gc),
+           "vs: merge");
+  }
   Partials vp;
   vp.KP = kp_for(KF);
   vp.P = 1;
@@ -912,7 +1029,6 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(scr.alloc((void**)&flags, (size_t)nq * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&qlist, (size_t)x.nq_pad * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&qcount, 2 * sizeof(int)), "vs: scratch");
-  const BoundArgs ba = make_bound_args(idx->ld, plane);
   const float* qinv = mode == MODE_COS ? qaux : nullptr;
   const float* xinv = mode == MODE_COS ? a.xaux : nullptr;
   VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
@@ -963,6 +1079,10 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
 // computes is not used here: this is the last stage.
 int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
                       hipStream_t st, const int* gl, const int* gc) {
+  // more than the 64 entries one exact page holds (inner product, k > 32): the
+  // two-page exact engine over the gathered queries (its keys are the fp32
+  // engine's own, as in a search that never went through the filter)
+  if (KF > 64) return run_wide_k(idx, a, st, gl, gc);
   const int ntotal = (int)idx->ntotal;
   const int KP = kp_for(KF);
   const int nslot = (int)round_up(a.nq, kBQ);
@@ -1102,8 +1222,11 @@ int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st) {
 //  3. page_finish: the pages concatenated, faiss's rule, the k outputs.
 // The small-batch GEMV serves one or two fp32 queries (the k = 60 single query);
 // everything else runs the fp32 / bf16 MFMA GEMM.
-int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st) {
+// gl / gc: a gathered batch, queries gl[0 .. *gc) of `a` (the staged engine's
+// last stage for k > 32; device-side count), whose rows alone are written.
+int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl, const int* gc) {
   const int nq = a.nq;
+  const bool gathered = gl != nullptr;
   const int ntotal = (int)idx->ntotal;
   Scratch scr(st);
   float *D1 = nullptr, *D2 = nullptr, *fkey = nullptr;
@@ -1121,7 +1244,7 @@ int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st) {
   VS_HIP(scr.alloc((void**)&qcount, sizeof(int)), "vs: scratch");
   const bool gemv_fits =
       (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
-  const bool gemv = a.self0 < 0 && nq <= 2 && idx->esize == 4 && gemv_fits;
+  const bool gemv = !gathered && a.self0 < 0 && nq <= 2 && idx->esize == 4 && gemv_fits;
   Partials gp;  // GEMV lists (both pages)
   gp.KP = 64;
   if (gemv) {
@@ -1143,10 +1266,12 @@ int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st) {
     p1.raw = 1;
     p1.D = D1;
     p1.I = I1;
-    const int rc = run_gemm(idx, p1, 64, st);
+    const int rc = run_gemm(idx, p1, 64, st, gl, gc);
     if (rc) return rc;
   }
-  VS_HIP(launch_page_check(D1, I1, nq, a.k, a.raw, idx->id_base, fkey, fid, flags, st),
+  if (gathered)  // only the gathered queries' rows of D1 exist
+    VS_HIP(hipMemsetAsync(flags, 0, (size_t)nq * sizeof(int), st), "vs: page check");
+  VS_HIP(launch_page_check(D1, I1, nq, a.k, a.raw, idx->id_base, fkey, fid, flags, st, gl, gc),
          "vs: page check");
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, nullptr, nullptr, st), "vs: flags");
   if (gemv) {  // every block exits at once when no query needs the second page
@@ -1179,24 +1304,46 @@ int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st) {
              "vs: merge launch");
     }
   }
-  VS_HIP(launch_page_finish(D1, I1, D2, I2, flags, nq, a.k, a.raw, a.D, a.I, st), "vs: pages");
+  VS_HIP(launch_page_finish(D1, I1, D2, I2, flags, nq, a.k, a.raw, a.D, a.I, st, gl, gc),
+         "vs: pages");
   return VS_OK;
 }
 
 // Shared search driver: queries already staged in `qbuf` ([nq_pad][ld] device,
 // zero-padded) with query aux values (`qaux`, L2 norms or 1/|q|).
 int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engine) {
-  if (a.mode == MODE_IP && (a.raw ? a.k > VS_MAX_K : 2 * a.k - 1 > VS_MAX_K))
-    return run_wide_k(idx, a, st);
   // faiss's inner-product tie rule (vs_support.hip, faiss_ip_tie_order) needs the
   // lowest 2k-1 (key, label) entries of every partial list to be exact; `raw`
   // output (plain lexicographic order) needs k.
   const int mode = a.mode;
   const bool tie_rule = mode == MODE_IP && !a.raw;
-  const int need = tie_rule ? std::min(2 * a.k - 1, VS_MAX_K) : a.k;
-  const int KP = kp_for(need);
+  const int need = tie_rule ? 2 * a.k - 1 : a.k;
   const int ntotal = (int)idx->ntotal;
   const int nq = a.nq;
+  int engine = force_engine != VS_ENGINE_AUTO ? force_engine
+               : idx->engine != VS_ENGINE_AUTO ? idx->engine
+                                               : engine_from_env();
+  // Large batches of fp32 indexes: the filter-and-verify engine where it applies
+  // (candidates for `need` exact entries: x1_list_len, up to 127 — inner
+  // product to k = 64), else (or VS_ENGINE=fp32) the fp32 MFMA GEMM.  bf16
+  // indexes: the bf16 MFMA GEMM.
+  // (past 64 candidates, inner product only: the last stage for what the
+  // filter cannot settle is then the two-page exact engine, inner product's;
+  // L2 / cosine with k > 56 keep the exact engine)
+  const int KF = x1_list_len(need) > 64 && mode != MODE_IP ? 0 : x1_list_len(need);
+  // the planes this search may run through: int8 first, then bf16; a forced
+  // *_VERIFY engine runs its plane alone (an L2 index's int8 plane is the
+  // augmented one: L2 searches only)
+  bool i8_ok = idx->plane_on[FILTER_I8] && idx->ld + idx->aug_m <= kI8MaxLd &&
+               (idx->l2aug() ? mode == MODE_L2 && idx->aug_m > 0 : mode != MODE_L2) &&
+               engine != VS_ENGINE_BF16_VERIFY;
+  const bool b16_ok = idx->plane_on[FILTER_BF16] && engine != VS_ENGINE_I8_VERIFY;
+  const bool staged = idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0 &&
+                      nq > kSkinnyMaxQ && (i8_ok || b16_ok);
+  // more entries than one exact page holds (inner product k > 32, raw k > 64)
+  // and no filter pass for them: the two-page exact engine
+  if (need > VS_MAX_K && !staged) return run_wide_k(idx, a, st);
+  const int KP = kp_for(need);
 
   // Small batches stream the corpus once.  fp32 L2 searches whose CALL has
   // fewer than 20 queries take faiss's sequential branch (direct sum (x-q)^2,
@@ -1261,25 +1408,14 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
            "vs: merge launch");
     return VS_OK;
   }
-  // Large batches of fp32 indexes: the filter-and-verify engine where it applies
-  // (IP k <= 28, L2 / cosine k <= 56), else (or VS_ENGINE=fp32) the fp32 MFMA
-  // GEMM.  bf16 indexes: the bf16 MFMA GEMM.
-  int engine = force_engine != VS_ENGINE_AUTO ? force_engine
-               : idx->engine != VS_ENGINE_AUTO ? idx->engine
-                                               : engine_from_env();
-  const int KF = x1_list_len(need);
   if (idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0) {
-    // the planes this search runs through: int8 first (inner product and
-    // cosine), then bf16; a forced *_VERIFY engine runs its plane alone
-    bool i8_ok = idx->plane_on[FILTER_I8] && idx->ld <= kI8MaxLd && mode != MODE_L2 &&
-                 engine != VS_ENGINE_BF16_VERIFY;
-    const bool b16_ok = idx->plane_on[FILTER_BF16] && engine != VS_ENGINE_I8_VERIFY;
     // the automatic order adapts to how much the int8 stage settles
     if (i8_ok && b16_ok && engine == VS_ENGINE_AUTO) i8_ok = adaptive_use_i8(idx);
     // stages: [int8] -> bf16 with deep lists over what is left -> exact fp32
     if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
     if (b16_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);
   }
+  if (need > VS_MAX_K) return run_wide_k(idx, a, st);
   return run_gemm(idx, a, need, st);
 }
 
@@ -1349,6 +1485,7 @@ int vs_destroy(vs_index* idx) {
     for (int p = 0; p < 2; ++p)
       if (idx->bstats[p]) (void)hipFree(idx->bstats[p]);
     if (idx->ad.dcount) (void)hipFree(idx->ad.dcount);
+    if (idx->ddead) (void)hipFree(idx->ddead);
     if (idx->ad.hmirror) (void)hipHostFree(idx->ad.hmirror);
     if (idx->ad.ev) (void)hipEventDestroy(idx->ad.ev);
   }
@@ -1471,12 +1608,13 @@ int vs_reset(vs_index* idx) {
   for (int p = 0; p < 2; ++p)
     if (idx->bstats[p]) VS_HIP(hipMemset(idx->bstats[p], 0, 4 * sizeof(unsigned)), "vs_reset");
   idx->ntotal = 0;
+  idx->dead.clear();
   return VS_OK;
 }
 
 int vs_ntotal(const vs_index* idx, int64_t* out) {
   if (!idx || !out) return fail(VS_E_INVALID, "vs_ntotal: null argument");
-  *out = idx->ntotal;
+  *out = idx->live();  // faiss ntotal: the live rows
   return VS_OK;
 }
 
@@ -1614,6 +1752,10 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
       int rc = run_topk(idx, sa, st, VS_ENGINE_AUTO);
       if (rc) return rc;
     }
+    // tombstoned rows never enter a list; the rows found become faiss labels
+    if (!idx->dead.empty())
+      VS_HIP(launch_label_map(Id, n * k, idx->ddead, (int64_t)idx->dead.size(), idx->id_base, st),
+             "vs_search: labels");
   }
   if (!out_dev) {
     VS_HIP(hipMemcpyAsync(D, Dd, (size_t)n * k * sizeof(float), hipMemcpyDeviceToHost, st),
@@ -1627,16 +1769,47 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
   return VS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+int reconstruct_rows(vs_index* idx, int64_t i0, int64_t n, float* out, int flags, hipStream_t st);
+int64_t row_of_label(const vs_index* idx, int64_t l);
+int pack_dead(vs_index* idx);
+}  // namespace
+
+extern "C" {
+
 int vs_reconstruct_n(vs_index* idx, int64_t i0, int64_t n, float* out, int flags, void* stream) {
   if (!idx) return fail(VS_E_INVALID, "vs_reconstruct_n: null index");
-  if (n < 0 || i0 < 0 || i0 + n > idx->ntotal)
+  hipStream_t st = (hipStream_t)stream;
+  std::shared_lock<std::shared_mutex> lk(idx->mu);
+  if (n < 0 || i0 < 0 || i0 + n > idx->live())
     return fail(VS_E_INVALID, "vs_reconstruct_n: key out of range");  // faiss: FAISS_THROW_IF_NOT
   if (n == 0) return VS_OK;
   if (!out) return fail(VS_E_INVALID, "vs_reconstruct_n: null output");
-  hipStream_t st = (hipStream_t)stream;
-  std::shared_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
   ReaderMark mark(idx, st);
+  // labels [i0, i0 + n) are runs of rows in place between tombstones
+  int64_t p = row_of_label(idx, i0), done = 0;
+  size_t j = std::upper_bound(idx->dead.begin(), idx->dead.end(), p) - idx->dead.begin();
+  while (done < n) {
+    const int64_t stop = j < idx->dead.size() ? idx->dead[j] : idx->ntotal;
+    const int64_t run = std::min(n - done, stop - p);
+    const int rc = reconstruct_rows(idx, p, run, out + done * idx->d, flags, st);
+    if (rc) return rc;
+    done += run;
+    p += run;
+    while (j < idx->dead.size() && idx->dead[j] == p) ++p, ++j;  // skip the tombstones
+  }
+  if (!(flags & VS_OUT_DEVICE)) VS_HIP(hipStreamSynchronize(st), "vs_reconstruct_n: synchronise");
+  return VS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// Rows in place [i0, i0 + n) -> fp32 out (the caller holds the reader lock).
+int reconstruct_rows(vs_index* idx, int64_t i0, int64_t n, float* out, int flags, hipStream_t st) {
   const hipMemcpyKind kind =
       (flags & VS_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
   if (idx->esize == 4) {
@@ -1660,35 +1833,21 @@ int vs_reconstruct_n(vs_index* idx, int64_t i0, int64_t n, float* out, int flags
     }
     VS_HIP(hipStreamSynchronize(st), "vs_reconstruct_n: synchronise");
   }
-  if (!(flags & VS_OUT_DEVICE)) VS_HIP(hipStreamSynchronize(st), "vs_reconstruct_n: synchronise");
   return VS_OK;
 }
+}  // namespace
 
-int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremoved) {
-  if (!idx) return fail(VS_E_INVALID, "vs_remove_ids: null index");
-  if (n < 0) return fail(VS_E_INVALID, "vs_remove_ids: n < 0");
-  if (nremoved) *nremoved = 0;
-  if (n == 0) return VS_OK;
-  if (!ids) return fail(VS_E_INVALID, "vs_remove_ids: null ids");
-  std::unique_lock<std::shared_mutex> lk(idx->mu);
-  // IDSelectorBatch semantics: membership test; duplicates and out-of-range ids
-  // are ignored.  Labels here are global (id_base applied), as faiss sees them.
-  std::vector<int64_t> rm;
-  rm.reserve((size_t)n);
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t r = ids[i] - idx->id_base;
-    if (r >= 0 && r < idx->ntotal) rm.push_back(r);
-  }
-  std::sort(rm.begin(), rm.end());
-  rm.erase(std::unique(rm.begin(), rm.end()), rm.end());
+extern "C" {
+
+}  // extern "C"
+
+namespace {
+// Stable compaction of the sorted physical rows `rm` out of the index (rows,
+// norms, filter planes re-derived over the moved rows), on the writer stream
+// `st`, after the index's readers have drained; synchronises.
+int compact_rows(vs_index* idx, const std::vector<int64_t>& rm, hipStream_t st) {
   const int64_t nrem = (int64_t)rm.size();
   if (nrem == 0) return VS_OK;
-  DeviceGuard g(idx->device);
-  // Searches of this index already queued on other streams read the rows we
-  // are about to move: wait for their marks (not for the device).
-  VS_HIP(wait_readers(idx), "vs_remove_ids: drain");
-  hipStream_t st = nullptr;
-  VS_HIP(writer_stream(idx, &st), "vs_remove_ids: stream");
   Scratch scr(st);
   int64_t* drm = nullptr;
   VS_HIP(scr.alloc((void**)&drm, (size_t)nrem * sizeof(int64_t)), "vs_remove_ids: scratch");
@@ -1749,7 +1908,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
   if (rc) return rc;
   for (int p = 0; p < 2; ++p)
     if (idx->plane_on[p] && idx->bstats[p])
-      VS_HIP(launch_bound_stats(idx->norms, idx->rn2[p], nt, idx->bstats[p], st),
+      VS_HIP(launch_bound_stats(plane_norms(idx, p), idx->rn2[p], nt, idx->bstats[p], st),
              "vs_remove_ids: bound maxima");
   for (int p = 0; p < 2; ++p) {
     if (!idx->plane_on[p]) continue;
@@ -1761,8 +1920,124 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
   if (idx->fscale)
     VS_HIP(hipMemsetAsync(idx->fscale + nt, 0, (size_t)nrem * sizeof(float), st),
            "vs_remove_ids: zero tail");
+  if (idx->anorm)
+    VS_HIP(hipMemsetAsync(idx->anorm + nt, 0, (size_t)nrem * sizeof(float), st),
+           "vs_remove_ids: zero tail");
   VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
   idx->ntotal = nt;
+  return VS_OK;
+}
+
+// Tombstoned rows -> packed storage (the same compaction as an immediate
+// removal); the labels do not change.
+int pack_dead(vs_index* idx) {
+  if (idx->dead.empty()) return VS_OK;
+  DeviceGuard g(idx->device);
+  VS_HIP(wait_readers(idx), "vs: pack");
+  hipStream_t st = nullptr;
+  VS_HIP(writer_stream(idx, &st), "vs: pack");
+  const int rc = compact_rows(idx, idx->dead, st);
+  if (rc) return rc;
+  idx->dead.clear();
+  return VS_OK;
+}
+
+// Dead fraction at which a removal packs the tombstones (1 / kPackDen of the
+// rows in place; env VS_PACK_DEN overrides, 1 = pack at every removal).  A
+// dead row costs every search its bytes until the pack, a pack moves every
+// row after the first dead one: at C5's 1 % per mutation round a pack comes
+// every ~6 rounds.
+int pack_den() {
+  const char* e = getenv("VS_PACK_DEN");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : 16;
+}
+
+// Live label l -> its row in place (the sorted dead list skipped).
+int64_t row_of_label(const vs_index* idx, int64_t l) {
+  int64_t p = l;
+  for (int64_t d : idx->dead) {
+    if (d <= p) ++p;
+    else break;
+  }
+  return p;
+}
+}  // namespace
+
+extern "C" {
+
+int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremoved) {
+  if (!idx) return fail(VS_E_INVALID, "vs_remove_ids: null index");
+  if (n < 0) return fail(VS_E_INVALID, "vs_remove_ids: n < 0");
+  if (nremoved) *nremoved = 0;
+  if (n == 0) return VS_OK;
+  if (!ids) return fail(VS_E_INVALID, "vs_remove_ids: null ids");
+  std::unique_lock<std::shared_mutex> lk(idx->mu);
+  // IDSelectorBatch semantics: membership test; duplicates and out-of-range ids
+  // are ignored.  Labels here are global (id_base applied), as faiss sees them.
+  std::vector<int64_t> rm;
+  rm.reserve((size_t)n);
+  const int64_t live = idx->live();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = ids[i] - idx->id_base;
+    if (r >= 0 && r < live) rm.push_back(r);
+  }
+  std::sort(rm.begin(), rm.end());
+  rm.erase(std::unique(rm.begin(), rm.end()), rm.end());
+  const int64_t nrem = (int64_t)rm.size();
+  if (nrem == 0) return VS_OK;
+  DeviceGuard g(idx->device);
+  // Searches of this index already queued on other streams read the rows we
+  // are about to move or overwrite: wait for their marks (not for the device).
+  VS_HIP(wait_readers(idx), "vs_remove_ids: drain");
+  hipStream_t st = nullptr;
+  VS_HIP(writer_stream(idx, &st), "vs_remove_ids: stream");
+  // labels -> rows in place (both ascending: one merge walk over the dead list)
+  if (!idx->dead.empty()) {
+    size_t j = 0;
+    int64_t shift = 0;
+    for (auto& r : rm) {
+      while (j < idx->dead.size() && idx->dead[j] <= r + shift) ++j, ++shift;
+      r += shift;
+    }
+  }
+  if (!idx->tombstones()) {  // filter planes to keep in step: compact now
+    const int rc = compact_rows(idx, rm, st);
+    if (rc) return rc;
+  } else {
+    Scratch scr(st);
+    int64_t* drm = nullptr;
+    VS_HIP(scr.alloc((void**)&drm, (size_t)nrem * sizeof(int64_t)), "vs_remove_ids: scratch");
+    VS_HIP(hipMemcpyAsync(drm, rm.data(), (size_t)nrem * sizeof(int64_t), hipMemcpyHostToDevice,
+                          st),
+           "vs_remove_ids: upload");
+    VS_HIP(launch_fill_nan_rows(idx->codes, idx->rowbytes(), idx->norms, idx->esize, drm, nrem, st),
+           "vs_remove_ids: tombstones");
+    std::vector<int64_t> merged;
+    merged.reserve(idx->dead.size() + rm.size());
+    std::merge(idx->dead.begin(), idx->dead.end(), rm.begin(), rm.end(),
+               std::back_inserter(merged));
+    idx->dead.swap(merged);
+    VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
+    if ((int64_t)idx->dead.size() * pack_den() >= idx->ntotal) {
+      const int rc = pack_dead(idx);
+      if (rc) return rc;
+    } else {
+      const int64_t nd = (int64_t)idx->dead.size();
+      if (nd > idx->ddead_cap) {
+        const int64_t cap = std::max<int64_t>(nd, 2 * idx->ddead_cap);
+        if (idx->ddead) (void)hipFree(idx->ddead);
+        idx->ddead = nullptr;
+        idx->ddead_cap = 0;
+        VS_HIP(hipMalloc(&idx->ddead, (size_t)cap * sizeof(int64_t)), "vs_remove_ids: dead list");
+        idx->ddead_cap = cap;
+      }
+      VS_HIP(hipMemcpyAsync(idx->ddead, idx->dead.data(), (size_t)nd * sizeof(int64_t),
+                            hipMemcpyHostToDevice, st),
+             "vs_remove_ids: dead list");
+      VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
+    }
+  }
   if (nremoved) *nremoved = nrem;
   return VS_OK;
 }
@@ -1770,6 +2045,11 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
 int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_self,
                 float min_sim, float* D, int64_t* I, int flags, void* stream) {
   if (!idx) return fail(VS_E_INVALID, "vs_selfjoin: null index");
+  {  // the self-join reads its query rows in place: pack the tombstones first
+    std::unique_lock<std::shared_mutex> wl(idx->mu);
+    const int rc = pack_dead(idx);
+    if (rc) return rc;
+  }
   if (k <= 0) return fail(VS_E_INVALID, "vs_selfjoin: k must be > 0");
   if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_selfjoin: k > VS_MAX_K (64) not supported yet");
   if (q0 < 0 || nq < 0 || q0 + nq > idx->ntotal)
@@ -1953,7 +2233,7 @@ int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches
   double tot = 0.0;
   int64_t n = 0;
   for (auto& p : g_timer_events) {
-    if (kernel && strcmp(kernel, p.name) != 0) continue;
+    if (kernel ? strcmp(kernel, p.name) != 0 : p.aux) continue;
     VS_HIP(hipEventSynchronize(p.b), "vs_timer_read: synchronise");
     float ms = 0.0f;
     VS_HIP(hipEventElapsedTime(&ms, p.a, p.b), "vs_timer_read: elapsed");

@@ -35,16 +35,19 @@
 //    block can enter the lane's list, inserts its rows one by one;
 //  * dump launches (every later launch of an int8 or bf16 inner-product
 //    pass): the lists stay in memory; the epilogue compares each block with
-//    the query's CUT (x1_qcut, set from the first launch's lists) and, for
-//    the rare block that may hold a row below it, stores the lane's 16 raw
-//    sums to a per-list dump slot; x1_replay (after the pass) admits the dumped
-//    rows into the lists exactly as a list launch would have — same keys, same
-//    order, same admission rule — so both kinds leave the same lists.
+//    its list's floor (the query's CUT, x1_qcut, set from the first launch's
+//    lists, or the list's own last entry) and, for the rare block that may
+//    hold a row below it, stores one (row, raw sum) pair per row that clears
+//    the per-row threshold to the list's next dump slot; x1_replay (between
+//    segments of launches) admits the dumped rows into the lists exactly as a
+//    list launch would have — same keys, same order, same admission rule — so
+//    both kinds leave the same lists.
 // The lists are per lane, so a list launch pays for a wave's rows whenever ANY
 // of its 64 lanes admits one (an exec-masked insertion chain per block that
 // passes somewhere): about a sixth of the int8 pass (profiles/r04a/x1_probes.txt:
 // 3.45 ms per dispatch with the candidate work, 2.86 ms with the epilogue's
-// per-block test alone).  A dump costs five stores on the lanes that pass.
+// per-block test alone).  A dump costs one 8-B store per candidate row on the
+// lanes that pass.
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -245,7 +248,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
     int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax,
-    const float* __restrict__ qcut, int* __restrict__ dcount, int* __restrict__ dslot, int dR) {
+    const float* __restrict__ xgmin, const float* __restrict__ qcut, int* __restrict__ dcount,
+    int* __restrict__ dslot, int dR) {
   static_assert(!DUMP || x1_has_dump(MODE, EL), "dump form");
   constexpr int NBUF = kNbuf;
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
@@ -397,18 +401,31 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // (its floor is fixed, and the factor bound is the launch's: the maximum
     // of its tiles' group maxima), so the per-block test is a maximum and a
     // compare with no per-tile loads or threshold arithmetic
+    // A floor above 0 (every row of the list so far scored below 0: queries
+    // pointing away from the data) needs the SMALLEST factor instead: a row
+    // with a negative sum scores highest with its smallest factor, so it can
+    // clear the limit only if fl(sum * fl(s_q * fmin)) does (rows with sums
+    // >= 0 always clear it, and the threshold is below 0).
     int Tq[2] = {0, 0};
     if constexpr (DUMP && EL == FILTER_I8) {
       const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      float fm = 0.0f;
-      for (int g = 16 * t0 + ln; g < 16 * t1; g += 64) fm = fmaxf(fm, xgmax[g]);
+      float fm = 0.0f, fn = FLT_MAX;
+      for (int g = 16 * t0 + ln; g < 16 * t1; g += 64) {
+        fm = fmaxf(fm, xgmax[g]);
+        fn = fminf(fn, xgmin[g]);
+      }
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) fm = fmaxf(fm, __shfl_xor(fm, m));
+      for (int m = 32; m >= 1; m >>= 1) {
+        fm = fmaxf(fm, __shfl_xor(fm, m));
+        fn = fminf(fn, __shfl_xor(fn, m));
+      }
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
-        const float c = qsc[qb] * fm, last = tq[qb];
-        Tq[qb] = (c > 0.0f && -last >= 0.0f) ? i8_threshold(-last, c)
-                 : (c > 0.0f || -0.0f < last) ? INT_MIN : INT_MAX;
+        const float c = qsc[qb] * fm, cn = qsc[qb] * fn, last = tq[qb];
+        Tq[qb] = (c > 0.0f && -last >= 0.0f)                    ? i8_threshold(-last, c)
+                 : (cn > 0.0f && cn <= FLT_MAX && -last < 0.0f) ? min(i8_threshold(-last, cn), -1)
+                 : (c > 0.0f || -0.0f < last)                   ? INT_MIN
+                                                                : INT_MAX;
         asm volatile("" ::"v"(Tq[qb]));
       }
     }
@@ -628,13 +645,17 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
               while (cm) {
                 const int bi = __builtin_ctz(cm);
                 cm &= cm - 1;
+                // rows past the corpus (the last tile's zero padding, whose sums
+                // of 0 clear a floor above 0) take no slot
+                const int row = rowof(rb, bi >> 2) + (bi & 3);
+                if (!plain && !(row < ntotal && row != selfrow[qb])) continue;
                 const int c = dc[qb]++;
                 if (c < dR) {
                   int sum;
                   if constexpr (EL == FILTER_I8) sum = sel16i(acc[rb][qb], bi);
                   else sum = __float_as_int(sel16(acc[rb][qb], bi));
                   const int64_t slot = ((int64_t)gq[qb] * P + pl) * dR + c;
-                  *(i32x2*)(dslot + slot * 2) = i32x2{rowof(rb, bi >> 2) + (bi & 3), sum};
+                  *(i32x2*)(dslot + slot * 2) = i32x2{row, sum};
                 }
               }
             }
@@ -1129,13 +1150,13 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
                            st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                            a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                            a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
-                           a.xgmax, a.qcut, a.dcount, a.dslot, a.dR);
+                           a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
     } else {
       hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                          st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                          a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                          a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
-                         a.xgmax, nullptr, nullptr, nullptr, 0);
+                         a.xgmax, a.xgmin, nullptr, nullptr, nullptr, 0);
     }
     if (a.timing) a.timing->end(st);
     hipError_t e = hipGetLastError();
@@ -1205,7 +1226,7 @@ hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStre
       part.P != 4 * a.nsplit || a.nsplit < 1 || a.ntotal <= 0)
     return hipErrorInvalidValue;
   if (a.filter == FILTER_I8) {
-    if (!a.xs || !a.qs || !a.xgmax || a.ld > kI8MaxLd) return hipErrorInvalidValue;
+    if (!a.xs || !a.qs || !a.xgmax || !a.xgmin || a.ld > kI8MaxLd) return hipErrorInvalidValue;
     return x1_dispatch<FILTER_I8>(mode, a, part, st, ndispatch);
   }
   return x1_dispatch<FILTER_BF16>(mode, a, part, st, ndispatch);
@@ -1235,7 +1256,11 @@ hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st) {
 // Filter-pass candidate count: the merged approximate candidates for `need`
 // exact entries, with a margin of at least 8 (0 = not served by the filter).
 int x1_list_len(int need) {
-  return need + 8 <= 24 ? 24 : need + 8 <= 32 ? 32 : need + 8 <= 64 ? 64 : 0;
+  return need + 8 <= 24   ? 24
+         : need + 8 <= 32 ? 32
+         : need + 8 <= 64 ? 64
+         : need < kVerifyMaxKF ? kVerifyMaxKF  // inner product k = 29 .. 64 (2k - 1 <= 127)
+                               : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1367,6 +1392,249 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// L2 on the int8 plane: the augmented inner product (vs_internal.h,
+// launch_quantize_i8_l2aug).  faiss ranks an L2 index's rows by
+// fl(fl(|q|^2 + n_x) - 2 fl(q.x)) (exhaustive_L2sqr_blas), i.e. by
+// q.x - n_x / 2 up to rounding; with x' = [x, e_1 .. e_m], q' = [q, C .. C] and
+// sum_j e_j = -n_x / (2 C), that is x'.q', an inner product the int8 filter
+// pass runs unchanged (list and dump launches, cuts, replays).  After the pass
+// the lane lists' keys A ~ n_x / 2 - q.x become L2 keys qn + 2A
+// (launch_l2aug_map) and the verification runs in the L2 metric with the
+// augmented bound (bound_key).  One wave per row; the codes are written four per
+// lane-store, the extra block (m a multiple of 64) after the ld row columns.
+__global__ __launch_bounds__(256) void quantize_i8_l2aug_kernel(
+    const float* __restrict__ X, int64_t ld, int64_t r0, int64_t n, int64_t pld, int m, float C,
+    float nref, const float* __restrict__ norms, int8_t* __restrict__ codes,
+    float* __restrict__ scale, float* __restrict__ rn2, float* __restrict__ anorm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* xr = X + (r0 + row) * ld;
+  float mx = 0.0f;
+  bool bad = false;
+  double sq = 0.0;
+  for (int64_t c = lane * 4; c < ld; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bad |= !isfinite(v[i]);
+      mx = fmaxf(mx, fabsf(v[i]));
+      sq += (double)v[i] * (double)v[i];
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o));
+    sq += __shfl_xor(sq, o);
+  }
+  bad = __any(bad);
+  const bool rows = norms != nullptr;
+  // the scale and the extra block's codes: rows an even split of T = rint(E / s)
+  // (base + 1 on the first |rem| columns), queries c everywhere
+  double E = 0.0;
+  float s = 0.0f;
+  int64_t T = 0;
+  int cq = 0;
+  if (rows) {
+    E = ((double)nref - (double)norms[r0 + row]) / (2.0 * (double)C);
+    bad |= !isfinite(E);
+    const double sd = fmax((double)mx, fabs(E) / m) / 127.0;
+    s = (float)sd;
+    if ((double)s < sd) s = nextafterf(s, INFINITY);
+    if (bad) s = 0.0f;
+    if (s > 0.0f) {
+      const double t = rint(E / (double)s);
+      T = (int64_t)fmin(fmax(t, -127.0 * m), 127.0 * m);
+    }
+  } else {
+    cq = mx > C ? max(1, min(127, (int)floorf(127.0f * (C / mx)))) : 127;
+    s = bad ? 0.0f : C / (float)cq;
+  }
+  const int64_t base = T / m, rem = T - base * m;  // |rem| < m, the sign of T
+  const int64_t sg = rem < 0 ? -1 : 1, nrem = rem < 0 ? -rem : rem;
+  double acc = 0.0;
+  for (int64_t c = lane * 4; c < pld; c += 256) {
+    uint32_t packed = 0;
+    if (c < ld) {
+      const f32x4 v = *(const f32x4*)(xr + c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int code = 0;
+        if (s > 0.0f) code = (int)fminf(fmaxf(rintf(v[i] / s), -127.0f), 127.0f);
+        packed |= (uint32_t)(code & 0xFF) << (8 * i);
+        const double r = (double)v[i] - (double)s * (double)code;
+        acc += r * r;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t j = c + i - ld;  // extra column j (0 .. m-1; pld = ld + m)
+        int code = 0;
+        if (j < m) {
+          if (rows) {
+            code = (int)(base + (j < nrem ? sg : 0));
+          } else if (s > 0.0f) {
+            code = cq;
+            const double r = (double)C - (double)s * (double)cq;
+            acc += r * r;
+          }
+        }
+        packed |= (uint32_t)(code & 0xFF) << (8 * i);
+      }
+    }
+    *(uint32_t*)(codes + plane_offset(r0 + row, c, pld)) = packed;  // tile-major
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) {
+    scale[r0 + row] = s;
+    auto up = [](double v) {
+      float f = (float)v;
+      if ((double)f < v) f = nextafterf(f, INFINITY);
+      return f;
+    };
+    if (rows) {
+      // the extra block: e_j = s c_j + delta, delta = (E - s T) / m (E's fp64
+      // rounding folded into the margin); |e|^2 = s^2 sum c_j^2 + 2 delta s T + m delta^2
+      const double dlt = fabs(E - (double)s * (double)T) + fabs(E) * 1e-15;
+      const double d1 = (E - (double)s * (double)T) / m;
+      const double cc = (double)(m - nrem) * (double)(base * base) +
+                        (double)nrem * (double)((base + sg) * (base + sg));
+      const double e2 = (double)s * (double)s * cc + 2.0 * d1 * (double)s * (double)T + m * d1 * d1;
+      rn2[r0 + row] = bad ? INFINITY : up((acc + dlt * dlt / m) * (1.0 + 1e-12));
+      if (anorm) anorm[r0 + row] = bad ? INFINITY : up((sq + fmax(e2, 0.0)) * (1.0 + 1e-12) + 1e-30);
+    } else {
+      rn2[r0 + row] = bad ? INFINITY : up(acc * (1.0 + 1e-12));
+    }
+  }
+}
+
+hipError_t launch_quantize_i8_l2aug(const float* X, int64_t ld, int64_t r0, int64_t n,
+                                    const L2Aug& g, const float* norms, int8_t* codes,
+                                    float* scale, float* rn2, float* anorm, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ld % 64 != 0 || g.m <= 0 || g.m % 64 != 0 || !(g.C > 0.0f) || !std::isfinite(g.nref) ||
+      !rn2)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(quantize_i8_l2aug_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X,
+                     ld, r0, n, ld + g.m, g.m, g.C, g.nref, norms, codes, scale, rn2, anorm);
+  return hipGetLastError();
+}
+
+// The augmentation's statistics, two passes over the first rows: nref < 0:
+// acc[0] += max|x| over the nonzero rows, acc[1] += their count, acc[2] = the
+// largest norm; nref >= 0: acc[3] = max |nref - n_x| / max|x| (bits of a
+// non-negative double order as its unsigned image).  One wave per row, one
+// atomic set per block.
+__global__ __launch_bounds__(256) void l2aug_stats_kernel(const float* __restrict__ X, int64_t ld,
+                                                          int64_t r0, int64_t n,
+                                                          const float* __restrict__ norms,
+                                                          float nref, double* __restrict__ acc) {
+  __shared__ double part[4][3];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wv;
+  float mx = 0.0f;
+  if (row < n) {
+    const float* xr = X + (r0 + row) * ld;
+    for (int64_t c = lane * 4; c < ld; c += 256) {
+      const f32x4 v = *(const f32x4*)(xr + c);
+      mx = fmaxf(fmaxf(fmaxf(mx, fabsf(v[0])), fmaxf(fabsf(v[1]), fabsf(v[2]))), fabsf(v[3]));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) {
+    const bool on = row < n && mx > 0.0f && isfinite(mx);
+    const double nx = on ? (double)norms[r0 + row] : 0.0;
+    part[wv][0] = on ? (double)mx : 0.0;
+    part[wv][1] = on ? 1.0 : 0.0;
+    const double r = nref < 0.0f ? nx : fabs((double)nref - nx) / (double)mx;
+    part[wv][2] = on && isfinite(r) ? r : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int i = 0; i < 4; ++i) {
+      a += part[i][0];
+      b += part[i][1];
+      c = fmax(c, part[i][2]);
+    }
+    if (b > 0.0) {
+      if (nref < 0.0f) {
+        atomicAdd(acc + 0, a);
+        atomicAdd(acc + 1, b);
+      }
+      atomicMax((unsigned long long*)(acc + (nref < 0.0f ? 2 : 3)),
+                (unsigned long long)__double_as_longlong(c));
+    }
+  }
+}
+
+hipError_t l2aug_params(const float* X, int64_t ld, int64_t r0, int64_t n, const float* norms,
+                        L2Aug* out, hipStream_t st) {
+  out->m = 64;
+  out->C = 1.0f;
+  out->nref = 0.0f;
+  if (n <= 0) return hipSuccess;
+  double* acc = nullptr;
+  hipError_t e = hipMalloc(&acc, 4 * sizeof(double));
+  if (e != hipSuccess) return e;
+  double h[4] = {0.0, 0.0, 0.0, 0.0};
+  const dim3 grid((unsigned)((n + 3) / 4));
+  e = hipMemsetAsync(acc, 0, 4 * sizeof(double), st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(l2aug_stats_kernel, grid, dim3(256), 0, st, X, ld, r0, n, norms, -1.0f, acc);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  const float nref = (float)h[2];
+  if (e == hipSuccess && h[1] > 0.0 && h[0] > 0.0 && std::isfinite(nref)) {
+    hipLaunchKernelGGL(l2aug_stats_kernel, grid, dim3(256), 0, st, X, ld, r0, n, norms, nref, acc);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) {
+      const double c = h[0] / h[1];
+      // a row's extra entries stay within its own max|x| when
+      // m >= |nref - n_x| / (2 C max|x|)
+      const double need = h[3] / (2.0 * c);
+      out->C = (float)c;
+      out->nref = nref;
+      out->m = (int)std::min<double>(4096.0, std::max(64.0, std::ceil(need / 64.0) * 64.0));
+    }
+  }
+  (void)hipFree(acc);
+  return e;
+}
+
+__global__ __launch_bounds__(256) void l2aug_map_kernel(float* __restrict__ key,
+                                                        const int* __restrict__ id,
+                                                        int64_t per_query, int nq,
+                                                        const float* __restrict__ qn, float nref,
+                                                        float* __restrict__ qcut) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (int64_t)nq * per_query && id[i] >= 0) {
+    const float v = (qn[i / per_query] + nref) + 2.0f * key[i];
+    key[i] = v < 0.0f ? 0.0f : v;
+  }
+  if (qcut && i < nq) {
+    const float c = qcut[i];
+    if (c < FLT_MAX && c > -FLT_MAX) {
+      const float v = (qn[i] + nref) + 2.0f * c;
+      qcut[i] = v < 0.0f ? 0.0f : v;
+    }
+  }
+}
+
+hipError_t launch_l2aug_map(float* key, const int* id, int64_t per_query, int nq, const float* qn,
+                            float nref, float* qcut, hipStream_t st) {
+  const int64_t tot = std::max<int64_t>((int64_t)nq * per_query, nq);
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(l2aug_map_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, key, id,
+                     per_query, nq, qn, nref, qcut);
+  return hipGetLastError();
+}
+
 // Gathered batch of a later filter stage: slot s < *count takes query gl[s]
 // (its fp32 row of `src`, stride ld, and its aux value; self row self0 + gl[s]
 // when self0 >= 0); slots past the count are zero rows (aux 0, no self row).
@@ -1436,27 +1704,36 @@ __global__ __launch_bounds__(256) void mul_arrays_kernel(const float* __restrict
 }
 
 // out[2 g + b] = max of f[r] over the rows r of 32-row group g with bit 2 of r
-// equal to b (f >= 0); n a multiple of 32.
+// equal to b (f >= 0); n a multiple of 32.  outmin (optional): the minimum
+// over the rows below nvalid (FLT_MAX for a part with none: padding rows,
+// whose zero factors would otherwise make every dump launch's minimum 0).
 __global__ __launch_bounds__(256) void group_max_kernel(const float* __restrict__ f, int64_t ngrp,
-                                                        float* __restrict__ out) {
+                                                        int64_t nvalid, float* __restrict__ out,
+                                                        float* __restrict__ outmin) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (group, bit)
   if (i >= 2 * ngrp) return;
-  const float* p = f + (i >> 1) * 32 + (i & 1) * 4;
-  float m = 0.0f;
+  const int64_t r0 = (i >> 1) * 32 + (i & 1) * 4;
+  const float* p = f + r0;
+  float m = 0.0f, mn = FLT_MAX;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const f32x4 v = *(const f32x4*)(p + 8 * j);
     m = fmaxf(fmaxf(fmaxf(m, v[0]), fmaxf(v[1], v[2])), v[3]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (r0 + 8 * j + e < nvalid) mn = fminf(mn, v[e]);
   }
   out[i] = m;
+  if (outmin) outmin[i] = mn;
 }
 
-hipError_t launch_group_max(const float* f, int64_t n, float* out, hipStream_t st) {
+hipError_t launch_group_max(const float* f, int64_t n, float* out, hipStream_t st, int64_t nvalid,
+                            float* outmin) {
   if (n <= 0) return hipSuccess;
   if (n % 32 != 0) return hipErrorInvalidValue;
   const int64_t m = 2 * (n / 32);
   hipLaunchKernelGGL(group_max_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, f,
-                     n / 32, out);
+                     n / 32, nvalid, out, outmin);
   return hipGetLastError();
 }
 
@@ -1501,6 +1778,26 @@ hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n,
 
 __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, double qh2, double qr2,
                                             double qn2, const unsigned* stats) {
+  if (ba.l2aug) {
+    // L2 through the augmented int8 plane: stats are the maxima of |x'|^2 and
+    // |x' - plane(x')|^2, qh2 / qr2 the query's |plane(q')|^2 bound and
+    // |q' - plane(q')|^2, qn2 = |q|^2 as staged.  The pass's key A differs from
+    // n_x / 2 - q.x by at most the inner-product bound b of the augmented
+    // vectors (no fp32 key rounding inside: A is not rounded again); the list
+    // key is max(0, fl(fl(qn + nref) + 2A)) (two more roundings, at most
+    // 2u (qn + nref + 2 |A|)) and
+    // the exact key fl(fl(qn + n_x) - fl(2 fl(q.x))) is within 8u (qn + n_x) of
+    // qn + n_x - 2 q.x (as for the other L2 passes); max(0, .) is 1-Lipschitz.
+    const double ax2 = (double)__uint_as_float(stats[0]);  // >= max |x|^2 too
+    const double hx = sqrt(ax2) + sqrt((double)__uint_as_float(stats[1]));
+    const double rx = sqrt((double)__uint_as_float(stats[1]));
+    const double hq = sqrt(qh2), rq = sqrt(qr2);
+    const double u = ldexp(1.0, -24);
+    double b = ba.gam * hx * hq + hx * rq + rx * hq + rx * rq;
+    b *= 1.0 + 1e-6;
+    return (2.0 * b + 8.0 * u * (qn2 + ax2) + 2.0 * u * (qn2 + ba.aug_nref + 2.01 * hx * hq)) *
+           (1.0 + 1e-6);
+  }
   const double xm = sqrt((double)__uint_as_float(stats[0]) * (1.0 + ba.norm_inf));
   const double rx = sqrt((double)__uint_as_float(stats[1]));
   const double hx = xm + rx;
@@ -1528,7 +1825,8 @@ __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, doubl
 // |hi(q)| <= |q| + |r(q)|
 __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow, int64_t ld,
                                                   int lane, const float* __restrict__ qr2i8,
-                                                  double& qh2, double& qr2, double& qn2) {
+                                                  double& qh2, double& qr2, double& qn2,
+                                                  double aug = 0.0) {
   double a = 0.0, r = 0.0, n = 0.0;
   for (int64_t c = lane * 4; c < ld; c += 256) {
     const f32x4 v = *(const f32x4*)(qrow + c);
@@ -1550,9 +1848,9 @@ __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow
   qh2 = a;
   qr2 = r;
   qn2 = n;
-  if (qr2i8) {
+  if (qr2i8) {  // aug: |q'|^2 = |q|^2 + m C^2 (the augmented L2 plane)
     qr2 = (double)*qr2i8;
-    const double hq = sqrt(n) + sqrt(qr2);
+    const double hq = sqrt(n + aug) + sqrt(qr2);
     qh2 = hq * hq;
   }
 }
@@ -1630,8 +1928,8 @@ __device__ __forceinline__ float exact_key(float ip, int q, int r, const float* 
 // One wave per query.  Dk/Ik: the KF best approximate keys (ascending) and
 // local rows; X/xn: fp32 rows (stride ld) and squared norms; Q: query rows
 // (stride ld); qn: |q|^2 as staged for L2.  Writes KF exact (key, row) entries
-// sorted, padded to KP, and fail[q].
-template <int MODE>
+// sorted, padded to KP, and fail[q].  NE = candidates per lane (KF <= 64 NE).
+template <int MODE, int NE>
 __global__ __launch_bounds__(64) void verify_rescore_kernel(
     int KF, int M, const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
     const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
@@ -1640,17 +1938,25 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
     const float* __restrict__ qinv, const float* __restrict__ xinv, const float* __restrict__ qr2i8,
     const int* __restrict__ qcount, const float* __restrict__ qcut) {
-  __shared__ float ek[64];
+  __shared__ float ek[64 * NE];
+  __shared__ int sid[64 * NE];
+  __shared__ float eMs;
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
   if (qcount && q >= *qcount) {  // gathered batch: slots past the count are not flagged
     if (lane == 0) fail[q] = 0;
     return;
   }
-  const float a = lane < KF ? Dk[(int64_t)q * KF + lane] : FLT_MAX;
-  const int id = lane < KF ? (int)Ik[(int64_t)q * KF + lane] : -1;
-  const float aK = __shfl(a, KF - 1);
-  const int idK = __shfl(id, KF - 1);
+  int id[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int j = lane + 64 * e;
+    id[e] = j < KF ? (int)Ik[(int64_t)q * KF + j] : -1;
+    sid[j] = id[e];
+  }
+  if (lane == 0) eMs = FLT_MAX;
+  const float aK = Dk[(int64_t)q * KF + KF - 1];
+  const int idK = (int)Ik[(int64_t)q * KF + KF - 1];
   // T: the KF-th merged key (if the merge found KF) and the last key of every
   // full lane list; `bounded` = false when neither exists (the candidates are
   // every admissible row)
@@ -1672,12 +1978,13 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
 
   const float* qrow = Q + (int64_t)q * ld;
   double qh2, qr2, qn2;
-  query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2);
+  query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2, ba.aug_q2);
+  __syncthreads();  // sid
   if (ld <= 256 * kQV) {  // two candidates per step, the query in registers
     QSlice qsl;
     load_qslice(qrow, ld, lane, qsl);
     for (int j = 0; j < KF; j += 2) {
-      const int ra = __shfl(id, j), rb = j + 1 < KF ? __shfl(id, j + 1) : -1;
+      const int ra = sid[j], rb = j + 1 < KF ? sid[j + 1] : -1;
       double da, db;
       wave_dot2(X + (int64_t)max(ra, 0) * ld, X + (int64_t)max(rb, 0) * ld, qsl, ld, lane, da, db);
       if (lane == 0) {
@@ -1687,7 +1994,7 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     }
   } else {
     for (int j = 0; j < KF; ++j) {
-      const int r = __shfl(id, j);
+      const int r = sid[j];
       if (r < 0) {
         if (lane == 0) ek[j] = FLT_MAX;
         continue;
@@ -1697,28 +2004,31 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     }
   }
   __syncthreads();
-  // rank sort of (key, row); empty slots last, in lane order among themselves
-  const float k0 = lane < KF ? ek[lane] : FLT_MAX;
-  const int i0 = id < 0 ? INT_MAX : id;
-  int rank = 0;
-  for (int j = 0; j < KF; ++j) {
-    const float kj = __shfl(k0, j);
-    const int ij = __shfl(i0, j);
-    rank += (lex_less(kj, ij, k0, i0) || (kj == k0 && ij == i0 && j < lane)) ? 1 : 0;
-  }
+  // rank sort of (key, row); empty slots last, in slot order among themselves
   float* ok = okey + (int64_t)q * KP;
   int* oi = oid + (int64_t)q * KP;
-  if (lane < KF) {
-    ok[rank] = k0;
-    oi[rank] = id;  // -1 for empty slots
-  } else if (lane < KP) {
-    ok[lane] = FLT_MAX;
-    oi[lane] = -1;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int s = lane + 64 * e;
+    if (s < KF) {
+      const float k0 = ek[s];
+      const int i0 = id[e] < 0 ? INT_MAX : id[e];
+      int rank = 0;
+      for (int j = 0; j < KF; ++j) {
+        const float kj = ek[j];
+        const int ij = sid[j] < 0 ? INT_MAX : sid[j];
+        rank += (lex_less(kj, ij, k0, i0) || (kj == k0 && ij == i0 && j < s)) ? 1 : 0;
+      }
+      ok[rank] = k0;
+      oi[rank] = id[e];  // -1 for empty slots
+      if (rank == M - 1) eMs = k0;  // the M-th exact key
+    } else if (s < KP) {
+      ok[s] = FLT_MAX;
+      oi[s] = -1;
+    }
   }
-  // the M-th exact key (the lane whose rank is M-1 publishes it)
-  if (lane < KF && rank == M - 1) ek[63] = k0;
   __syncthreads();
-  const float eM = ek[63];
+  const float eM = eMs;
   const double bkey = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
   const bool pass = !bounded || ((double)T - bkey > (double)eM && isfinite(T) && isfinite(eM) &&
                                   isfinite(bkey));
@@ -1732,22 +2042,28 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
                                  int* oid, int KP, int* fail, hipStream_t st, const float* qinv,
                                  const float* xinv, const float* qr2i8, const int* qcount,
                                  const float* qcut) {
-  if (KF > 64 || KP > 64 || KF > KP || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
-      L > lists.KP)
+  if (KF > kVerifyMaxKF || KP > kVerifyMaxKF || KF > KP || M < 1 || M > KF || ld % 4 != 0 ||
+      L < 1 || L > lists.KP)
     return hipErrorInvalidValue;
   if (nq <= 0) return hipSuccess;
-#define VS_VERIFY(MD)                                                                             \
-  hipLaunchKernelGGL(verify_rescore_kernel<MD>, dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, X, xn, \
-                     Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey, oid,  \
-                     KP, fail, qinv, xinv, qr2i8, qcount, qcut)
+#define VS_VERIFY(MD, NE)                                                                     \
+  hipLaunchKernelGGL((verify_rescore_kernel<MD, NE>), dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, \
+                     X, xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L,    \
+                     okey, oid, KP, fail, qinv, xinv, qr2i8, qcount, qcut)
+#define VS_VERIFY_NE(MD) \
+  if (KF <= 64)          \
+    VS_VERIFY(MD, 1);    \
+  else                   \
+    VS_VERIFY(MD, 2)
   if (mode == MODE_IP)
-    VS_VERIFY(MODE_IP);
+    VS_VERIFY_NE(MODE_IP);
   else if (mode == MODE_L2)
-    VS_VERIFY(MODE_L2);
+    VS_VERIFY_NE(MODE_L2);
   else if (mode == MODE_COS && qinv && xinv)
-    VS_VERIFY(MODE_COS);
+    VS_VERIFY_NE(MODE_COS);
   else
     return hipErrorInvalidValue;
+#undef VS_VERIFY_NE
 #undef VS_VERIFY
   return hipGetLastError();
 }
@@ -1836,8 +2152,9 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     unsigned long long* __restrict__ sizes, const float* __restrict__ qcut) {
   __shared__ float ck[kWideCap];
   __shared__ int cid[kWideCap];
-  __shared__ float rk[64], kk[64];  // the first check's exact keys / the reused ones
-  __shared__ int ri[64], ki[64];
+  // the first check's exact keys (KP <= kVerifyMaxKF) / the reused ones
+  __shared__ float rk[kVerifyMaxKF], kk[kVerifyMaxKF];
+  __shared__ int ri[kVerifyMaxKF], ki[kVerifyMaxKF];
   __shared__ int cntk;
   __shared__ float wT[4];
   __shared__ int wB[4];
@@ -1870,14 +2187,14 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
       bad = 0;
       eMs = FLT_MAX;
     }
-    if (tid < 64) {  // the first check's output for this query (KP <= 64 entries)
+    if (tid < kVerifyMaxKF) {  // the first check's output for this query (KP entries)
       rk[tid] = tid < KP ? okey[(int64_t)q * KP + tid] : FLT_MAX;
       ri[tid] = tid < KP ? oid[(int64_t)q * KP + tid] : -1;
     }
     const float* qrow = Q + (int64_t)q * ld;
     if (wv == 0) {
       double a, b, c;
-      query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, a, b, c);
+      query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, a, b, c, ba.aug_q2);
       if (lane == 0) {
         qs[0] = a;
         qs[1] = b;
@@ -1926,10 +2243,10 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
       if (r >= 0 && (!bounded || lk < T)) {
         int hit = -1;
         if (Dk && (kfi < 0 || !lex_less(kfk, kfi, lk, r)))
-          for (int t = 0; t < KP && t < 64; ++t) hit = ri[t] == r ? t : hit;
+          for (int t = 0; t < KP; ++t) hit = ri[t] == r ? t : hit;
         if (hit >= 0) {
           const int s = atomicAdd(&cntk, 1);
-          if (s < 64) {
+          if (s < kVerifyMaxKF) {
             kk[s] = rk[hit];
             ki[s] = r;
           }
@@ -1941,7 +2258,7 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
     }
     __syncthreads();
     const int nu = cnt;  // rows to rescore
-    const int nk = min(cntk, 64);
+    const int nk = min(cntk, kVerifyMaxKF);
     const int n = nu + cntk;
     if (sizes && tid == 0) {
       atomicAdd(sizes, (unsigned long long)n);
@@ -2015,7 +2332,9 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
                               const float* xinv, const float* qr2i8, const float* Dk,
                               const int64_t* Ik, unsigned long long* sizes,
                               const float* qcut) {
-  if (KF > KP || KP > 64 || (Dk && !Ik) || M < 1 || M > KF || ld % 4 != 0 || L < 1 || L > lists.KP) return hipErrorInvalidValue;
+  if (KF > KP || KP > kVerifyMaxKF || (Dk && !Ik) || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
+      L > lists.KP)
+    return hipErrorInvalidValue;
   if (nq_max <= 0) return hipSuccess;
   const int grid = std::min(nq_max, 2048);
 #define VS_WIDE(MD)                                                                               \
@@ -2072,8 +2391,12 @@ __global__ __launch_bounds__(64) void qbound_kernel(const float* __restrict__ Q,
   const int lane = threadIdx.x;
   if (q >= nq) return;
   double qh2, qr2, qn2;
-  query_split_norms(Q + (int64_t)q * ld, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2);
-  const double b = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
+  query_split_norms(Q + (int64_t)q * ld, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2,
+                    ba.aug_q2);
+  double b = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
+  // the augmented L2 pass cuts its lists in the inner-product keys A, whose
+  // map qn + 2A doubles distances: half the L2 bound there
+  if (ba.l2aug) b *= 0.5;
   if (lane == 0) bkey[q] = b;
 }
 
@@ -2083,6 +2406,112 @@ __device__ __forceinline__ uint32_t key_order(float f) {  // float order as unsi
 }
 __device__ __forceinline__ float key_unorder(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// The KF = 128 best approximate candidates of each query (KF <= 64 goes through
+// merge_lists_kernel, whose register lists would not hold 128): one
+// 256-thread workgroup per query finds the KF-th smallest 64-bit image
+// (key order << 32 | row; a query's lists hold distinct rows) of its P lists of
+// L entries by a bitwise search, keeps the entries at or below it and ranks
+// them.  Writes Dk/Ik [nq][KF] ascending (FLT_MAX / -1 padding).
+__global__ __launch_bounds__(256) void select_lists_kernel(const float* __restrict__ lkey,
+                                                           const int* __restrict__ lid, int P,
+                                                           int LKP, int L, int KF,
+                                                           float* __restrict__ Dk,
+                                                           int64_t* __restrict__ Ik,
+                                                           const int* __restrict__ qcount) {
+  __shared__ int wsum[4];
+  __shared__ unsigned long long sel[kVerifyMaxKF];
+  __shared__ int nsel;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (qcount && q >= *qcount) return;  // gathered batch: slots past the count
+  const int64_t base = (int64_t)q * P * LKP;
+  const int n = P * L;
+  constexpr int kR = 16;
+  constexpr unsigned long long kNone = ~0ull;
+  unsigned long long v[kR];
+  const bool regs = n <= 256 * kR;  // uniform
+  auto image = [&](int j) -> unsigned long long {
+    const int64_t o = base + (int64_t)(j / L) * LKP + j % L;
+    const int r = lid[o];
+    return r >= 0 ? ((unsigned long long)key_order(lkey[o]) << 32) | (uint32_t)r : kNone;
+  };
+#pragma unroll
+  for (int i = 0; i < kR; ++i) {
+    const int j = tid + 256 * i;
+    v[i] = regs && j < n ? image(j) : kNone;
+  }
+  auto count_le = [&](unsigned long long y) {  // entries with image <= y (workgroup-wide)
+    int c = 0;
+    if (regs) {
+#pragma unroll
+      for (int i = 0; i < kR; ++i) c += v[i] <= y && v[i] != kNone ? 1 : 0;
+    } else {
+      for (int j = tid; j < n; j += 256) {
+        const unsigned long long x = image(j);
+        c += x <= y && x != kNone ? 1 : 0;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    __syncthreads();
+    if (lane == 0) wsum[wv] = c;
+    __syncthreads();
+    return wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  };
+  const int total = count_le(kNone - 1);
+  const int M = total < KF ? total : KF;
+  // the smallest y with M entries at or below it (bit by bit from the top)
+  unsigned long long y = kNone - 1;
+  if (M > 0 && M < total) {
+    unsigned long long x = 0;  // invariant: count_le(x - 1) < M
+    for (int b = 63; b >= 0; --b) {
+      const unsigned long long t = x + (1ull << b);
+      if (t - 1 < x) continue;  // overflow
+      if (count_le(t - 1) < M) x = t;
+    }
+    y = x;  // count_le(y - 1) < M <= count_le(y): y is the M-th smallest image
+  }
+  if (tid == 0) nsel = 0;
+  __syncthreads();
+  auto take = [&](unsigned long long x) {
+    if (x != kNone && x <= y) {
+      const int s = atomicAdd(&nsel, 1);
+      if (s < kVerifyMaxKF) sel[s] = x;
+    }
+  };
+  if (M > 0) {
+    if (regs) {
+#pragma unroll
+      for (int i = 0; i < kR; ++i) take(v[i]);
+    } else {
+      for (int j = tid; j < n; j += 256) take(image(j));
+    }
+  }
+  __syncthreads();
+  float* dk = Dk + (int64_t)q * KF;
+  int64_t* ik = Ik + (int64_t)q * KF;
+  if (tid < KF) {
+    if (tid < M) {
+      const unsigned long long x = sel[tid];
+      int rank = 0;
+      for (int j = 0; j < M; ++j) rank += sel[j] < x ? 1 : 0;
+      dk[rank] = key_unorder((uint32_t)(x >> 32));
+      ik[rank] = (int64_t)(uint32_t)(x & 0xFFFFFFFFull);
+    } else {
+      dk[tid] = FLT_MAX;
+      ik[tid] = -1;
+    }
+  }
+}
+
+hipError_t launch_select_lists(Partials part, int L, int nq, int KF, float* Dk, int64_t* Ik,
+                               hipStream_t st, const int* qcount) {
+  if (KF < 1 || KF > kVerifyMaxKF || L < 1 || L > part.KP || part.P < 1) return hipErrorInvalidValue;
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(select_lists_kernel, dim3(nq), dim3(256), 0, st, part.key, part.id, part.P,
+                     part.KP, L, KF, Dk, Ik, qcount);
+  return hipGetLastError();
 }
 
 // One wave per query: a_M = the M-th smallest key over the query's P lists of
@@ -2138,10 +2567,10 @@ __global__ __launch_bounds__(64) void qcut_kernel(const float* __restrict__ lkey
 
 hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, int filter,
                          const unsigned* stats, const float* qr2i8, int nq, double* bkey,
-                         hipStream_t st) {
+                         hipStream_t st, const BoundArgs* bap) {
   if (nq <= 0) return hipSuccess;
   if (ld % 4 != 0) return hipErrorInvalidValue;
-  const BoundArgs ba = make_bound_args(ld, filter);
+  const BoundArgs ba = bap ? *bap : make_bound_args(ld, filter);
 #define VS_QB(MD) \
   hipLaunchKernelGGL(qbound_kernel<MD>, dim3(nq), dim3(64), 0, st, Q, ld, qn, ba, stats, qr2i8, nq, bkey)
   if (mode == MODE_IP)
@@ -2173,6 +2602,14 @@ BoundArgs make_bound_args(int64_t ld, int filter) {
   // the stored norms are fp32 sums of ld squares: they undercount by at most
   // ~gam(ld), whatever the plane
   ba.norm_inf = 2.0 * (n * u / (1.0 - n * u));
+  return ba;
+}
+
+BoundArgs make_bound_args_l2aug(int64_t ld, const L2Aug& g) {
+  BoundArgs ba = make_bound_args(ld + g.m, FILTER_I8);
+  ba.l2aug = 1;
+  ba.aug_q2 = (double)g.m * (double)g.C * (double)g.C;
+  ba.aug_nref = (double)g.nref;
   return ba;
 }
 

@@ -110,6 +110,7 @@ struct X1Args {
   const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)
   const float* xgmax = nullptr;  // int8: launch_group_max of xs (capacity rows)
+  const float* xgmin = nullptr;  // int8: the group minima of xs over rows < ntotal
   // Dump launches (vs_gemm_x1.hip header): after the pass's first launch the
   // cuts are set and the later launches store the blocks below them
   bool dump = false;
@@ -137,8 +138,8 @@ struct X1Args {
 constexpr int kX1Q = 256;  // queries (and database rows) per x1 tile
 // int8 sums stay exact in int32 up to this many elements per row.
 constexpr int64_t kI8MaxLd = 131072;
-// Candidates merged from the lane lists for `need` exact entries (24, 32 or 64;
-// 0 = not served by the filter engine).
+// Candidates merged from the lane lists for `need` exact entries (24, 32, 64 or
+// 128; 0 = not served by the filter engine).
 int x1_list_len(int need);
 // Entries per lane list of the filter pass (8).
 int x1_lane_len();
@@ -157,8 +158,22 @@ struct BoundArgs {
                           // accumulation of ld + 1 terms, n u / (1 - n u), u = 2^-23;
                           // int8: exact int32 sum, three fp32 roundings of the scaling)
   double norm_inf = 0.0;  // relative undercount of the stored fp32 norms
+  // L2 on the int8 plane (the augmented inner product, launch_quantize_i8_l2aug):
+  // the bound is the inner-product bound of the augmented vectors, mapped to
+  // the L2 key; aug_q2 = m C^2, what the augmentation adds to every |q|^2
+  int l2aug = 0;
+  double aug_q2 = 0.0;
+  double aug_nref = 0.0;  // the augmentation's reference norm (launch_l2aug_map)
 };
 BoundArgs make_bound_args(int64_t ld, int filter);
+// The augmentation of an L2 index's int8 plane (launch_quantize_i8_l2aug).
+struct L2Aug {
+  int m = 0;          // extra columns (a multiple of 64)
+  float C = 0.0f;     // the queries' extra entry
+  float nref = 0.0f;  // reference norm: the rows' extra entries sum to (nref - n_x) / (2 C)
+};
+// The bound constants for an L2 index's augmented int8 plane.
+BoundArgs make_bound_args_l2aug(int64_t ld, const L2Aug& g);
 // out[0..3) = bits of max norms, max rn2, max rn2/norms over rows [0, n).
 // accumulate: fold rows [0, n) into the maxima already in out (no reset).
 hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, unsigned* out,
@@ -171,6 +186,35 @@ hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n,
 // * code_r|^2 rounded up (+inf for a row with a non-finite element).
 hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
                               float* scale, float* rn2, hipStream_t st);
+// L2 as an inner product ("int8 L2"): ranking rows by the faiss
+// L2 key |q|^2 + |x|^2 - 2 q.x is ranking them by q.x + (nref - n_x) / 2 =
+// x'.q' with x' = [x, e_1 .. e_m], sum_j C e_j = (nref - n_x) / 2 (n_x the
+// stored norm, nref a constant of the index: the largest norm of its first
+// rows, so the scores of the best rows stay positive and the extra entries
+// small), and q' = [q, C .. C].  Rows (norms != nullptr): the codes of x'
+// (plane rows of ld + m bytes, the extra columns at [ld, ld + m)), s =
+// max(max|x|, |E| / m) / 127 with E = (nref - n_x) / (2 C), the extra codes an
+// even split of T = rint(E / s) (the conceptual e_j are those codes' values
+// plus an even share of the remainder, so the residual of the extra block is
+// |E - s T|^2 / m), rn2 = |x' - plane(x')|^2 and anorm = |x'|^2, both rounded
+// up.  Queries (norms == nullptr): extra codes c and s = C / c with c =
+// min(127, floor(127 C / max|q|)) (so s * c = C up to one rounding), rn2 =
+// |q' - plane(q')|^2 rounded up.
+hipError_t launch_quantize_i8_l2aug(const float* X, int64_t ld, int64_t r0, int64_t n,
+                                    const L2Aug& g, const float* norms, int8_t* codes,
+                                    float* scale, float* rn2, float* anorm, hipStream_t st);
+// The augmentation's parameters from fp32 rows [r0, r0+n): C = the mean of
+// max|x| over the nonzero rows, nref = the largest norm, m = the extra columns
+// that keep every row's extra entries within its own max|x|
+// (|nref - n_x| / (2 C max|x|) at most), rounded up to 64, at least 64 (no
+// nonzero row: C = 1).  Synchronises `st`.
+hipError_t l2aug_params(const float* X, int64_t ld, int64_t r0, int64_t n, const float* norms,
+                        L2Aug* out, hipStream_t st);
+// Lane lists of an augmented pass -> L2 keys: key = max(0, fl(fl(|q|^2 + nref)
+// + 2 key)) for every entry with a row (the map is monotone, so the lists stay
+// sorted and every floor stays a floor), and the cuts likewise (-FLT_MAX kept).
+hipError_t launch_l2aug_map(float* key, const int* id, int64_t per_query, int nq,
+                            const float* qn, float nref, float* qcut, hipStream_t st);
 // A later filter stage's gathered batch: dst[s] = src[gl[s]] (rows of stride
 // ld), daux[s] = aux[gl[s]], drow[s] = self0 + gl[s] (or -1) for s < *count,
 // zero rows / 0 / -1 for the other slots of [0, nslot).
@@ -187,7 +231,8 @@ hipError_t launch_compose_list(const int* outer, const int* inner, const int* co
 hipError_t launch_window_count(const int* count, int w0, int cap, int* out, hipStream_t st);
 // out[2 g + b] = max of f over the rows of 32-row group g whose bit 2 is b
 // (the int8 filter's per-lane factor bound), n a multiple of 32.
-hipError_t launch_group_max(const float* f, int64_t n, float* out, hipStream_t st);
+hipError_t launch_group_max(const float* f, int64_t n, float* out, hipStream_t st,
+                            int64_t nvalid = 0, float* outmin = nullptr);
 // out[i] = a[i] * b[i] (the int8 cosine's folded factors s / |x|).
 hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* out,
                              hipStream_t st);
@@ -218,6 +263,14 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // are reused instead of read again.  sizes (optional): += the wide-set entries
 // and the rescored ones.
 constexpr int kWideCap = 2048;
+// The most candidates (KF) the verification rescores per query, and the longest
+// exact list (KP) it writes: 128 holds inner product's 2k - 1 for k <= 64.
+constexpr int kVerifyMaxKF = 128;
+// The KF (<= kVerifyMaxKF) lexicographically best (key, row) entries of every
+// query's P lane lists of L entries (stride part.KP), ascending, into Dk/Ik
+// [nq][KF] (the approximate merge when KF > 64; launch_merge_partials below).
+hipError_t launch_select_lists(Partials part, int L, int nq, int KF, float* Dk, int64_t* Ik,
+                               hipStream_t st, const int* qcount = nullptr);
 
 // Scratch chunks (vs_api.hip): device memory of at least `bytes` whose previous
 // use the taker's stream `st` waits for; put records the chunk's last use on
@@ -248,7 +301,7 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
 // launch_x1_replay after it, and the verification must get the same cuts).
 hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, int filter,
                          const unsigned* stats, const float* qr2i8, int nq, double* bkey,
-                         hipStream_t st);
+                         hipStream_t st, const BoundArgs* ba = nullptr);
 bool x1_dump_applies(int mode, int filter);
 int x1_dump_slots();  // the most dump slots per lane list worth allocating
 bool x1_pass_dumps(int ntotal, int nsplit);  // a pass this long has dump launches
@@ -271,13 +324,17 @@ hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int 
 // lexicographic top-64 of each query: scores, labels with id_base); flags[q] =
 // a second page is needed (the k-th key's run of equal keys reaches entry 63, or
 // raw and the page is full), fkey/fid = its floor (key and local row of entry 63).
+// gl / gc (optional): a gathered batch, queries gl[0 .. *gc) of the nq rows
+// (the other rows' flags are left as they are).
 hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, int raw,
-                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st);
+                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st,
+                             const int* gl = nullptr, const int* gc = nullptr);
 // The two pages -> (D, I) rows of k <= 128 entries (faiss's rule unless raw);
 // D2/I2 rows are read only where flags[q].
 hipError_t launch_page_finish(const float* D1, const int64_t* I1, const float* D2,
                               const int64_t* I2, const int* flags, int nq, int k, int raw,
-                              float* D, int64_t* I, hipStream_t st);
+                              float* D, int64_t* I, hipStream_t st, const int* gl = nullptr,
+                              const int* gc = nullptr);
 // out[r] = sum_j X[r][j]^2 for rows [r0, r0+n) (fp32 or bf16 rows).
 hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, int64_t n,
                             float* out, hipStream_t st);
@@ -308,6 +365,13 @@ hipError_t launch_fill_empty(int mode, float* D, int64_t* I, int64_t n, hipStrea
 // Stable compaction helper: copy the kept rows of [src0, src0+n) into tmp,
 // given the sorted removed-row list (device).  Also moves the norms.
 // Rows are `rowbytes` long (multiple of 16).
+// Tombstones: rows[0 .. n) (device) filled with NaN elements and a NaN norm;
+// the labels I[0 .. n) of a search (kernel rows + id_base) mapped to positions
+// among the live rows (dead: the sorted tombstoned rows, ndead of them).
+hipError_t launch_fill_nan_rows(void* X, int64_t rowbytes, float* norms, int esize,
+                                const int64_t* rows, int64_t n, hipStream_t st);
+hipError_t launch_label_map(int64_t* I, int64_t n, const int64_t* dead, int64_t ndead,
+                            int64_t id_base, hipStream_t st);
 hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbytes, int64_t src0,
                               int64_t n, const int64_t* removed, int64_t nrem, void* tmp,
                               float* tmp_norms, hipStream_t st);

@@ -223,6 +223,30 @@ static hipError_t merge_levels(int mode, Partials part, int nq, int k, int64_t i
   return e;
 }
 
+// One sorted list of up to 128 entries per query (the verification's exact
+// lists when inner product's rule reads 2k - 1 > 64 of them) -> (D, I) rows:
+// faiss's rule on lane 0 over LDS, then the k outputs (k <= 128).
+__global__ __launch_bounds__(64) void emit_list_kernel(
+    const float* __restrict__ pkey, const int* __restrict__ pid, int KP, int k, int mode, int raw,
+    int64_t id_base, float min_score, float* __restrict__ D, int64_t* __restrict__ I,
+    int64_t ldo, const int* __restrict__ qlist, const int* __restrict__ qcount) {
+  __shared__ float sk[128];
+  __shared__ int si[128];
+  const int lane = threadIdx.x;
+  const int q = blockIdx.x;
+  if (qcount && q >= *qcount) return;  // gathered batch: slots past the count
+  for (int j = lane; j < 128; j += 64) {
+    sk[j] = j < KP ? pkey[(int64_t)q * KP + j] : FLT_MAX;
+    si[j] = j < KP ? pid[(int64_t)q * KP + j] : -1;
+  }
+  __syncthreads();
+  if (lane == 0 && mode == MODE_IP && !raw) faiss_ip_tie_order<int>(sk, si, KP, k);
+  __syncthreads();
+  const int64_t qe = qlist ? qlist[q] : q;  // output row
+  for (int j = lane; j < k; j += 64)
+    emit_result(mode, sk[j], si[j], id_base, min_score, D + qe * ldo + j, I + qe * ldo + j);
+}
+
 hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t id_base,
                                  float min_score, float* D, int64_t* I, int64_t ldo,
                                  hipStream_t st, int raw, const int* qlist, const int* qcount) {
@@ -230,6 +254,13 @@ hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t
       part.KL % 4 != 0)
     return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
+  if (part.KP > 64) {  // one sorted list per query only (the verification's output)
+    if (part.KP > 128 || part.P != 1 || (part.KL != 0 && part.KL != part.KP))
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(emit_list_kernel, dim3(nq), dim3(64), 0, st, part.key, part.id, part.KP, k,
+                       mode, raw, id_base, min_score, D, I, ldo, qlist, qcount);
+    return hipGetLastError();
+  }
   switch (part.KP) {
     case 8:
       return merge_levels<8>(mode, part, nq, k, id_base, min_score, D, I, ldo, raw, st, qlist, qcount);
@@ -333,9 +364,12 @@ __global__ __launch_bounds__(256) void page_check_kernel(const float* __restrict
                                                          int k, int raw, int64_t id_base,
                                                          float* __restrict__ fkey,
                                                          int* __restrict__ fid,
-                                                         int* __restrict__ flags) {
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
+                                                         int* __restrict__ flags,
+                                                         const int* __restrict__ gl,
+                                                         const int* __restrict__ gc) {
+  const int j0 = blockIdx.x * 256 + threadIdx.x;
+  if (j0 >= nq || (gc && j0 >= *gc)) return;
+  const int q = gl ? gl[j0] : j0;  // a gathered batch: its queries' rows only
   const float* d = D1 + (int64_t)q * 64;
   const int64_t* i = I1 + (int64_t)q * 64;
   const bool full = i[63] >= 0;
@@ -345,11 +379,12 @@ __global__ __launch_bounds__(256) void page_check_kernel(const float* __restrict
 }
 
 hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, int raw,
-                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st) {
+                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st,
+                             const int* gl, const int* gc) {
   if (nq <= 0) return hipSuccess;
   if (k < 1 || k > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(page_check_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, D1, I1, nq, k,
-                     raw, id_base, fkey, fid, flags);
+                     raw, id_base, fkey, fid, flags, gl, gc);
   return hipGetLastError();
 }
 
@@ -359,10 +394,12 @@ hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, 
 __global__ __launch_bounds__(64) void page_finish_kernel(
     const float* __restrict__ D1, const int64_t* __restrict__ I1, const float* __restrict__ D2,
     const int64_t* __restrict__ I2, const int* __restrict__ flags, int k, int raw,
-    float* __restrict__ D, int64_t* __restrict__ I) {
+    float* __restrict__ D, int64_t* __restrict__ I, const int* __restrict__ gl,
+    const int* __restrict__ gc) {
   __shared__ float sk[128];
   __shared__ int64_t si[128];
-  const int q = blockIdx.x;
+  if (gc && (int)blockIdx.x >= *gc) return;
+  const int q = gl ? gl[blockIdx.x] : (int)blockIdx.x;  // a gathered batch: its rows only
   const int lane = threadIdx.x;
   const bool two = flags[q] != 0;
   const int64_t o = (int64_t)q * 64 + lane;
@@ -384,11 +421,11 @@ __global__ __launch_bounds__(64) void page_finish_kernel(
 
 hipError_t launch_page_finish(const float* D1, const int64_t* I1, const float* D2,
                               const int64_t* I2, const int* flags, int nq, int k, int raw,
-                              float* D, int64_t* I, hipStream_t st) {
+                              float* D, int64_t* I, hipStream_t st, const int* gl, const int* gc) {
   if (nq <= 0) return hipSuccess;
   if (k < 1 || k > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(page_finish_kernel, dim3(nq), dim3(64), 0, st, D1, I1, D2, I2, flags, k, raw,
-                     D, I);
+                     D, I, gl, gc);
   return hipGetLastError();
 }
 
@@ -741,6 +778,58 @@ hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbyte
   hipLaunchKernelGGL(gather_kept_kernel, dim3((unsigned)((n + kKeptRows - 1) / kKeptRows)), dim3(256), 0, st,
                      (const char*)X, norms, rowbytes, src0, n, removed, nrem, (char*)out,
                      out_norms);
+  return hipGetLastError();
+}
+
+// Tombstones (vs_api.hip, vs_remove_ids on an index without filter planes):
+// the removed rows keep their place until a pack, filled with NaN (fp32
+// 0x7FC00000, bf16 0x7FC0) and a NaN norm, so every kernel's strict admission
+// (key < last, lex_less) leaves them out, whatever the metric.  One workgroup
+// per row.
+__global__ __launch_bounds__(256) void fill_nan_rows_kernel(char* __restrict__ X, int64_t rowbytes,
+                                                            float* __restrict__ norms, int esize,
+                                                            const int64_t* __restrict__ rows) {
+  const int64_t r = rows[blockIdx.x];
+  uint32_t* p = (uint32_t*)(X + r * rowbytes);
+  const uint32_t v = esize == 2 ? 0x7FC07FC0u : 0x7FC00000u;
+  for (int64_t i = threadIdx.x; i < rowbytes / 4; i += 256) p[i] = v;
+  if (threadIdx.x == 0) norms[r] = __uint_as_float(0x7FC00000u);
+}
+
+hipError_t launch_fill_nan_rows(void* X, int64_t rowbytes, float* norms, int esize,
+                                const int64_t* rows, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (rowbytes % 4 != 0 || n > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fill_nan_rows_kernel, dim3((unsigned)n), dim3(256), 0, st, (char*)X, rowbytes,
+                     norms, esize, rows);
+  return hipGetLastError();
+}
+
+// Search output labels of a tombstoned index: a kernel row p (plus id_base)
+// becomes faiss's label, its position among the live rows: p minus the dead
+// rows below it (binary search in the sorted dead list; p itself is live).
+__global__ __launch_bounds__(256) void label_map_kernel(int64_t* __restrict__ I, int64_t n,
+                                                        const int64_t* __restrict__ dead,
+                                                        int64_t ndead, int64_t id_base) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t v = I[i];
+  if (v < 0) return;
+  const int64_t p = v - id_base;
+  int64_t lo = 0, hi = ndead;  // first dead row >= p
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (dead[mid] < p) lo = mid + 1;
+    else hi = mid;
+  }
+  I[i] = p - lo + id_base;
+}
+
+hipError_t launch_label_map(int64_t* I, int64_t n, const int64_t* dead, int64_t ndead,
+                            int64_t id_base, hipStream_t st) {
+  if (n <= 0 || ndead <= 0) return hipSuccess;
+  hipLaunchKernelGGL(label_map_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, I, n,
+                     dead, ndead, id_base);
   return hipGetLastError();
 }
 

@@ -182,7 +182,24 @@ class ShardedIndexFlat:
 
     def search_device(self, xq, k: int, stream: int = 0):
         """Device tensors end to end: xq (nq, d) float32 cuda tensor on this rank's
-        GPU (replicated on every rank) -> merged (D, I) cuda tensors."""
+        GPU (replicated on every rank) -> merged (D, I) cuda tensors.
+
+        Every step runs in the order of `stream`: the shard search writes its
+        lists there, and the output allocations, the collective (RCCL runs it on
+        its own stream after waiting for the current one, and makes the current
+        one wait for it) and the merge all see `stream` as torch's current stream,
+        so a caller's stream other than torch's current one orders the gather
+        after the search and the merge after the gather (no race either way)."""
+        import torch
+
+        cur = torch.cuda.current_stream(xq.device)
+        if stream and stream != cur.cuda_stream:
+            ext = torch.cuda.ExternalStream(stream, device=xq.device)
+            with torch.cuda.stream(ext):
+                return self._search_device(xq, k, stream)
+        return self._search_device(xq, k, stream)
+
+    def _search_device(self, xq, k: int, stream: int):
         import torch
 
         nq = xq.shape[0]
@@ -198,4 +215,3 @@ class ShardedIndexFlat:
                                  raw=True)
         Dall, Iall = self._gather(Dl, Il)
         return self.merge_device(Dall, Iall, nq, kin, k, stream)
-

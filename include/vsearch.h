@@ -222,8 +222,9 @@ int vs_filter_second_stats(int64_t* second);
  * were read from HBM and rescored (the rest reuse the first check's exact keys),
  * since the last vs_filter_stats reset.  Diagnostic only: no reference interface. */
 int vs_filter_wide_sets(int64_t* entries, int64_t* rescored);
-/* Blocks the filter pass's dump launches stored (a lane's 16 sums that may
- * hold a row below its query's cut) and lane lists that ran out of dump slots
+/* Rows the filter pass's dump launches stored (one (row, raw sum) slot per
+ * row that may lie below its lane list's floor) and lane lists that ran out of
+ * dump slots
  * (their queries went to the next stage), since the last vs_filter_stats
  * reset.  Diagnostic only: no reference interface. */
 int vs_filter_dump_stats(int64_t* dumps, int64_t* overflows);
@@ -237,7 +238,10 @@ int vs_timer_reset(void);
 int vs_x1_stamps(unsigned long long* out, int reset);
 int vs_timer_read(double* total_ms, int64_t* launches);
 /* The same for the spans of one kernel name only (the filter engine's first
- * stage is "gemm_topk_x1_i8" or "gemm_topk_x1" (bf16) per search). */
+ * stage is "gemm_topk_x1_i8" or "gemm_topk_x1" (bf16) per search; its first
+ * launch, when the later ones dump, "<name>_list"; the whole pass including
+ * the cut and replay kernels "<name>_pass", a span that vs_timer_read's total
+ * leaves out because its kernels are in the other spans). */
 int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches);
 /* Name of the fused search kernel the last search launched ("gemm_topk_x1",
  * "gemm_topk", "skinny_topk" or "gemv_topk"). */

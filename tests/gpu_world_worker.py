@@ -92,6 +92,17 @@ def main():
             torch.cuda.synchronize()
             check(f"{mn}_float_device_k{k}", Dd.cpu().numpy(), Id.cpu().numpy(), xf, qf, k,
                   metric, False)
+        # a caller's stream other than torch's current one (sharded.py runs the
+        # search, the gather and the merge in that stream's order): the queries
+        # are written on the current stream, the lists read back after a sync of
+        # the side stream alone
+        side = torch.cuda.Stream()
+        qd = torch.from_numpy(qf).cuda()
+        side.wait_stream(torch.cuda.current_stream())
+        Dd, Id = idf.search_device(qd, 10, stream=side.cuda_stream)
+        side.synchronize()
+        check(f"{mn}_float_side_stream_k10", Dd.cpu().numpy(), Id.cpu().numpy(), xf, qf, 10,
+              metric, False)
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.barrier()

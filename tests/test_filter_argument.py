@@ -178,6 +178,119 @@ def test_int8_filter_bound_holds_for_cosine():
     assert (np.abs(key_a - key_e) <= b).all(), float(np.abs(key_a - key_e).max() - b)
 
 
+def _l2aug_params(x, xn):
+    """vs_gemm_x1.hip l2aug_params: C = mean max|x| over the nonzero rows, nref
+    = the largest norm, m = max |nref - n_x| / (2 C max|x|) rounded up to 64
+    (at least 64)."""
+    mx = np.abs(x).max(axis=1).astype(np.float64)
+    on = mx > 0
+    C = float(np.float32(mx[on].mean()))
+    nref = float(np.float32(xn[on].max()))
+    need = (np.abs(nref - xn[on].astype(np.float64)) / mx[on]).max() / (2.0 * C)
+    return max(64, int(np.ceil(need / 64.0) * 64)), C, nref
+
+
+def _quantize_i8_l2aug_rows(x, xn, m, C, nref):
+    """quantize_i8_l2aug_kernel, rows: x' = [x, e], sum_j C e_j = (nref - n_x) / 2;
+    the extra codes split T = rint(E / s) evenly; returns codes, s,
+    |x'-p(x')|^2 and |x'|^2 (rounded up)."""
+    x = np.asarray(x, np.float32)
+    mx = np.abs(x).max(axis=1)
+    E = (np.float64(nref) - xn.astype(np.float64)) / (2.0 * np.float64(C))
+    sd = np.maximum(mx.astype(np.float64), np.abs(E) / m) / 127.0
+    s = sd.astype(np.float32)
+    s = np.where(s.astype(np.float64) < sd, np.nextafter(s, np.float32(np.inf)), s)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        c = np.where(s[:, None] > 0, np.rint(x / s[:, None]), 0.0)
+        T = np.where(s > 0, np.rint(E / s.astype(np.float64)), 0.0)
+    c = np.clip(c, -127, 127).astype(np.int64)
+    T = np.clip(T, -127.0 * m, 127.0 * m).astype(np.int64)
+    base = np.trunc(T / m).astype(np.int64)
+    rem = T - base * m
+    j = np.arange(m)[None, :]
+    ce = base[:, None] + np.where(j < np.abs(rem)[:, None], np.sign(rem)[:, None], 0)
+    assert np.abs(ce).max() <= 127
+    r = x.astype(np.float64) - s[:, None].astype(np.float64) * c
+    dlt = np.abs(E - s.astype(np.float64) * T) + np.abs(E) * 1e-15
+    rn2 = ((r * r).sum(axis=1) + dlt * dlt / m) * (1 + 1e-12)
+    d1 = (E - s.astype(np.float64) * T) / m
+    e = s[:, None].astype(np.float64) * ce + d1[:, None]        # the conceptual extra entries
+    an2 = ((x.astype(np.float64) ** 2).sum(axis=1) + (e * e).sum(axis=1)) * (1 + 1e-12)
+    return np.concatenate([c, ce], axis=1), s, rn2, an2
+
+
+def _quantize_i8_l2aug_queries(q, m, C):
+    q = np.asarray(q, np.float32)
+    mx = np.abs(q).max(axis=1)
+    C32 = np.float32(C)
+    with np.errstate(divide="ignore"):
+        cq = np.where(mx > C32, np.clip(np.floor(np.float32(127.0) * (C32 / mx)), 1, 127), 127)
+    cq = cq.astype(np.int64)
+    s = (C32 / cq.astype(np.float32)).astype(np.float32)
+    c = np.clip(np.rint(q / s[:, None]), -127, 127).astype(np.int64)
+    r = q.astype(np.float64) - s[:, None].astype(np.float64) * c
+    re = np.float64(C32) - s.astype(np.float64) * cq
+    rn2 = ((r * r).sum(axis=1) + m * re * re) * (1 + 1e-12)
+    ce = np.repeat(cq[:, None], m, axis=1)
+    return np.concatenate([c, ce], axis=1), s, rn2
+
+
+def test_int8_l2_augmented_bound_holds():
+    """L2 on the int8 plane (vs_gemm_x1.hip quantize_i8_l2aug_kernel, bound_key's
+    l2aug branch, l2aug_map_kernel): the pass scores the augmented vectors
+    x' = [x, e] (sum_j C e_j = (nref - n_x) / 2) and q' = [q, C ..] with the
+    inner product's int8 arithmetic, A = -fl(fl(sum) fl(s_q s_x)) ~ n_x / 2 -
+    q.x - nref / 2; the list keys become max(0, fl(fl(qn + nref) + 2A)) (the
+    rows' extra entries stay small: their norms sit near nref); faiss's L2 key is
+    max(0, fl(fl(qn + n_x) - fl(2 fl(q.x)))).  Every pair is within the bound,
+    zero, tiny, outlier, embedding-like and one-hot rows included, and the bound
+    is not vacuous on uniform rows."""
+    rng = np.random.default_rng(21)
+    d = 1536
+    x = _rows(rng, 64, d)
+    q = _rows(rng, 16, d)
+    q[5] = -x[9]                                   # a query far from everything
+    q[6] = x[10]                                   # a query equal to a row
+    xn = (x.astype(np.float32) ** 2).sum(axis=1, dtype=np.float32)
+    qn = (q.astype(np.float32) ** 2).sum(axis=1, dtype=np.float32)
+    m, C, nref = _l2aug_params(x[6:], xn[6:])      # the uniform bulk sets them
+    assert m == 64  # uniform rows' norms lie within a few per cent of each other
+    cx, sx, rx2, ax2 = _quantize_i8_l2aug_rows(x, xn, m, C, nref)
+    cq, sq, rq2 = _quantize_i8_l2aug_queries(q, m, C)
+    dot = (cq @ cx.T).astype(np.int64)
+    assert np.abs(dot).max() < 2 ** 31
+    f = (sq[:, None] * sx[None, :]).astype(np.float32)
+    A = -(dot.astype(np.float32) * f).astype(np.float32)
+    qr = (qn + np.float32(nref)).astype(np.float32)
+    Ahat = np.maximum(np.float32(0), (qr[:, None] + np.float32(2) * A).astype(np.float32))
+    ip = (q.astype(np.float64) @ x.astype(np.float64).T).astype(np.float32)
+    K = np.maximum(np.float32(0), ((qn[:, None] + xn[None, :]).astype(np.float32)
+                                   - np.float32(2) * ip).astype(np.float32))
+    # bound_key, l2aug: index maxima of |x'|^2 and |r(x')|^2, the query's own
+    axm2, rxm2 = ax2.max(), rx2.max()
+    hx = np.sqrt(axm2) + np.sqrt(rxm2)
+    rx = np.sqrt(rxm2)
+    qn64 = (q.astype(np.float64) ** 2).sum(axis=1)
+    rq = np.sqrt(rq2)
+    hq = np.sqrt(qn64 + m * np.float64(np.float32(C)) ** 2) + rq
+    b = (_GAM_I8 * hx * hq + hx * rq + rx * hq + rx * rq) * (1 + 1e-6)
+    B = (2 * b + 8 * _U * (qn.astype(np.float64) + axm2)
+         + 2 * _U * (qn.astype(np.float64) + nref + 2.01 * hx * hq)) * (1 + 1e-6)
+    err = np.abs(Ahat.astype(np.float64) - K.astype(np.float64))
+    assert (err <= B[:, None]).all(), float((err - B[:, None]).max())
+    # not vacuous: over an index of the uniform rows alone (the outlier row's
+    # scale sets the maxima above), a small part of the L2 key spread
+    axm2, rxm2 = ax2[6:].max(), rx2[6:].max()
+    hx = np.sqrt(axm2) + np.sqrt(rxm2)
+    rx = np.sqrt(rxm2)
+    b = (_GAM_I8 * hx * hq + hx * rq + rx * hq + rx * rq) * (1 + 1e-6)
+    B = (2 * b + 8 * _U * (qn.astype(np.float64) + axm2)
+         + 2 * _U * (qn.astype(np.float64) + nref + 2.01 * hx * hq)) * (1 + 1e-6)
+    assert (err[6:, 6:] <= B[6:, None]).all()
+    spread = K[6:, 6:].astype(np.float64).std()
+    assert np.median(B[6:]) < 0.25 * spread, (np.median(B[6:]), spread)
+
+
 def test_wide_threshold_below_the_floor_is_exact():
     """The wide check may use any T' <= T (vs_gemm_x1.hip verify_wide_kernel):
     with a_M the M-th smallest approximate key, T' = min(T, a_M + 2.000001 B)
@@ -364,19 +477,22 @@ def test_query_cut_selection_is_the_mth_smallest_key():
 
 def test_dump_and_replay_leave_the_lists_of_in_kernel_admission():
     """The dump launches (vs_gemm_x1.hip header) restated: after the first
-    launch sets the cut, a lane stores a whole 16-row block whenever its block
-    test says a row may be below the cut (a superset: here the block's
-    smallest key), in the order it meets them, and x1_replay admits the
-    stored rows in that order against min(list last, cut).  The lists equal
-    those of admitting every row in-kernel against min(list last, cut), and a
-    list whose dumps exceed its slots is reported (its query is then failed)."""
+    launch sets the cut, a lane stores one (row, raw sum) slot for every row
+    of a block whose per-row test says it may be below the floor (a superset:
+    the kernel's integer threshold comes from the launch's largest row factor,
+    modelled here as a lower bound a_lo <= a of the row's key), in the order it
+    meets them, and x1_replay admits the stored rows in that order against
+    min(list last, cut).  The lists equal those of admitting every row
+    in-kernel against min(list last, cut), and a list whose dumped rows exceed
+    its R = 64 slots (x1_dump_slots) is reported (its query is then failed)."""
     rng = np.random.default_rng(11)
-    B, M, P, L, R = 1e-3, 19, 64, 8, 32
+    B, M, P, L, R = 1e-3, 19, 64, 8, 64
     for trial in range(30):
         n = 16 * 2048
         a = (rng.standard_normal(n) * 0.01).astype(np.float64)
         if trial % 4 == 0:  # near-duplicates: many rows just above the top
             a[rng.choice(n, 400, replace=False)] = -0.04 + rng.uniform(0, B, 400)
+        a_lo = a - np.abs(rng.standard_normal(n)) * 2e-3  # the per-row test's bound
         owner = np.repeat(rng.integers(0, P, size=n // 16), 16)  # blocks of 16 rows
         order = np.arange(n)
         cut_at = n // 8
@@ -388,20 +504,21 @@ def test_dump_and_replay_leave_the_lists_of_in_kernel_admission():
         dumps = [[] for _ in range(P)]
         for b0 in range(cut_at, n, 16):
             blk = np.arange(b0, b0 + 16)
-            if a[blk].min() < cut:  # the block test (a superset of rows below the cut)
-                dumps[owner[b0]].append(blk)
+            if a_lo[blk].min() < cut:  # the block test: one maximum and a compare
+                # one slot per row that clears the per-row threshold
+                dumps[owner[b0]].extend(int(r) for r in blk if a_lo[r] < cut)
         overflow = [len(d) > R for d in dumps]
+        assert any(len(d) > 0 for d in dumps)
         for p in range(P):
             if overflow[p]:
                 continue
             lst = lists[p]
-            for blk in dumps[p]:
-                for r in blk:
-                    lim = a[lst[-1]] if len(lst) == L else np.inf
-                    if a[r] < min(lim, cut):
-                        lst.append(r)
-                        lst.sort(key=lambda x: (a[x], x))
-                        del lst[L:]
+            for r in dumps[p]:
+                lim = a[lst[-1]] if len(lst) == L else np.inf
+                if a[r] < min(lim, cut):
+                    lst.append(r)
+                    lst.sort(key=lambda x: (a[x], x))
+                    del lst[L:]
         for p in range(P):
             if not overflow[p]:
                 np.testing.assert_array_equal(np.array(lists[p], dtype=np.int64), ref[p])

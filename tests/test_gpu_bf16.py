@@ -110,3 +110,66 @@ def test_bf16_selfjoin(vf):
     for q, j in zip(*np.nonzero(diff)):
         assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
     np.testing.assert_allclose(S[~diff], Sr[~diff], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_bf16_tombstoned_removals(vf, metric, monkeypatch):
+    """remove_ids on an index without filter planes (bf16 storage) tombstones
+    the rows (NaN-filled in place, vs_api.hip vs_remove_ids) until the dead
+    fraction reaches 1 / VS_PACK_DEN: faiss's labels (positions among the live
+    rows) must come out of every search path — the small-batch kernels, the
+    bf16 GEMM, the two-page k > 32 engine, raw lists — and out of reconstruct;
+    appends continue the label space; a large removal packs; the self-join
+    packs first.  Oracle: the fp64 search over the bf16-rounded live rows."""
+    monkeypatch.setenv("VS_PACK_DEN", "16")
+    d = 96
+    xb = _rand(8000, d, 11)
+    index = vf.IndexFlat(d, metric, dtype="bf16")
+    index.add(xb)
+    xr = flat.round_bf16(xb)
+    rng = np.random.default_rng(12)
+
+    def check(nq, k, seed, raw=False):
+        xq = _rand(nq, d, seed)
+        rq = flat.round_bf16(xq)
+        D, I = index.search(xq, k, raw=raw)
+        if raw:
+            Dr, Ir = flat.knn_lex(xr, rq, k, metric)
+        else:
+            Dr, Ir = flat.knn_exact(xr, rq, k, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xr, rq)
+        assert not bad, (nq, k, raw, bad[:3])
+
+    for r in range(4):
+        rm = rng.choice(xr.shape[0], 60, replace=False)  # well under 1/16: tombstones
+        assert index.remove_ids(np.concatenate([rm, rm[:3], [10 ** 9]])) == 60
+        xr, _ = flat.remove_ids(xr, rm)
+        add = _rand(50, d, 20 + r)
+        index.add(add)
+        xr = np.concatenate([xr, flat.round_bf16(add)])
+        assert index.ntotal == xr.shape[0]
+        for nq in (1, 8, 40):
+            check(nq, 10, 30 + r)
+        for lab in rng.choice(xr.shape[0], 5, replace=False):
+            np.testing.assert_array_equal(index.reconstruct(int(lab)), xr[lab])
+        np.testing.assert_array_equal(index.reconstruct_n(0, index.ntotal), xr)
+    if metric == IP:
+        check(40, 50, 40)              # faiss's rule past k = 32 (two pages)
+        check(40, 100, 41, raw=True)   # a shard's raw half of a sharded k = 50
+    # a removal past 1/16 of the rows packs the tombstones (labels unchanged)
+    rm = np.arange(0, xr.shape[0], 5, dtype=np.int64)
+    assert index.remove_ids(rm) == rm.size
+    xr, _ = flat.remove_ids(xr, rm)
+    assert index.ntotal == xr.shape[0]
+    check(40, 10, 50)
+    np.testing.assert_array_equal(index.reconstruct_n(0, index.ntotal), xr)
+    # tombstones again, then the self-join (which packs them first)
+    rm = rng.choice(xr.shape[0], 40, replace=False)
+    index.remove_ids(rm)
+    xr, _ = flat.remove_ids(xr, rm)
+    S, I = index.selfjoin(10)
+    Sr, Ir = flat.pgvector_cosine_topk(xr, 10)
+    diff = I != Ir
+    for q, j in zip(*np.nonzero(diff)):
+        assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
+    assert index.ntotal == xr.shape[0]

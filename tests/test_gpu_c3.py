@@ -36,6 +36,7 @@ N, D_, K = 10_000_000, 1536, 10
 SAMPLE = sorted({q for t in range(16) for q in (256 * t, 256 * t + 37, 256 * t + 160,
                                                  256 * t + 255)})
 CL_SAMPLE = SAMPLE[::2] + [4095]  # clustered: 33 queries (m = 256 candidates each)
+KW = (30, 60)  # inner product's wide k (checked on the IP candidate sets, m = 256)
 
 
 @pytest.fixture(scope="module")
@@ -53,8 +54,16 @@ def c3():
         index.add_synthetic(N, seed=1234)
         Db, Ib = index.search(xq, K)  # batch 4096 (default engine)
         D1, I1 = index.search(xq[SAMPLE[-1]:SAMPLE[-1] + 1], K)  # batch 1
-        cand = proven_candidates(index, xq[SAMPLE], metric, N, K)
-        out[metric] = (Db, Ib, D1, I1, cand)
+        wide = {}
+        if metric == flat.METRIC_INNER_PRODUCT:
+            # the service's wide searches (service.py:627 k = 30, :529 k = 60) at
+            # batch 4096: the filter pass with 64 / 128 candidates per query
+            for kw in KW:
+                wide[kw] = index.search(xq, kw)
+            cand = proven_candidates(index, xq[SAMPLE], metric, N, max(KW), m=256)
+        else:
+            cand = proven_candidates(index, xq[SAMPLE], metric, N, K)
+        out[metric] = (Db, Ib, D1, I1, cand, wide)
         del index
     return xq, out
 
@@ -62,7 +71,7 @@ def c3():
 @pytest.mark.parametrize("metric", [flat.METRIC_INNER_PRODUCT, flat.METRIC_L2])
 def test_c3_batch4096_sampled_against_oracle(c3, metric):
     xq, out = c3
-    Db, Ib, _, _, cand = out[metric]
+    Db, Ib, _, _, cand, _ = out[metric]
     assert Ib.shape == (4096, K)
     assert (Ib >= 0).all() and (Ib < N).all()
     diffs = np.diff(Db, axis=1)
@@ -112,7 +121,22 @@ def test_c3_clustered_sampled_against_oracle(c3_clustered):
 @pytest.mark.parametrize("metric", [flat.METRIC_INNER_PRODUCT, flat.METRIC_L2])
 def test_c3_batch1_against_oracle(c3, metric):
     xq, out = c3
-    _, Ib, D1, I1, cand = out[metric]
+    _, Ib, D1, I1, cand, _ = out[metric]
     assert_against_candidates(D1[0], I1[0], cand[len(SAMPLE) - 1], metric, K, D_, strict=False)
     # batch 1 (HBM-bound kernel) and batch 4096 agree on the same query
     assert (I1[0] == Ib[SAMPLE[-1]]).all() or metric == flat.METRIC_L2
+
+
+@pytest.mark.parametrize("kw", KW)
+def test_c3_wide_k_inner_product_against_oracle(c3, kw):
+    """k = 30 and k = 60 at batch 4096 (the filter pass with 64 and 128
+    candidates per query, faiss's tie rule over the 2k - 1 best): strict on the
+    64 sampled queries against their proven 256-row candidate sets."""
+    xq, out = c3
+    _, _, _, _, cand, wide = out[flat.METRIC_INNER_PRODUCT]
+    D, I = wide[kw]
+    assert I.shape == (4096, kw) and (I >= 0).all() and (I < N).all()
+    assert (np.diff(D, axis=1) <= 0).all()
+    for row, q in enumerate(SAMPLE):
+        assert_against_candidates(D[q], I[q], cand[row], flat.METRIC_INNER_PRODUCT, kw, D_,
+                                  strict=True)

@@ -46,20 +46,42 @@ def lib():
         os.environ["VS_X1_CHUNK_TILES"] = old
 
 
-def _search_checked(lib, xb, xq, k, engine="auto"):
+def _search_checked(lib, xb, xq, k, engine="auto", metric=IP):
     from vsearch import faiss as vfaiss
 
-    index = vfaiss.IndexFlat(xb.shape[1], IP)
+    index = vfaiss.IndexFlat(xb.shape[1], metric)
     index.add(xb)
     index.set_engine(engine)
     lib.filter_stats(reset=True)
     D, I = index.search(xq, k)
     dumps, over = lib.filter_dump_stats()
     fq, ff = lib.filter_stats(reset=True)
-    Dr, Ir = flat.knn_exact(xb, xq[SAMPLE], k, IP)
-    bad = flat.mismatches(D[SAMPLE], I[SAMPLE], Dr, Ir, IP, xb, xq[SAMPLE], strict=True)
+    Dr, Ir = flat.knn_exact(xb, xq[SAMPLE], k, metric)
+    bad = flat.mismatches(D[SAMPLE], I[SAMPLE], Dr, Ir, metric, xb, xq[SAMPLE], strict=True)
     assert not bad, bad[:5]
     return dumps, over, fq, ff
+
+
+@pytest.mark.parametrize("kind", ["uniform", "normal"])
+def test_dump_launches_l2_augmented(lib, kind):
+    """L2 through the int8 plane's augmented rows (L2 as an inner product): the
+    same list / dump launches, cuts and replays as an inner-product pass, the
+    lane lists mapped to L2 keys after it; exact on the sample, dump launches
+    ran, no list out of slots and no query left to the exact engine."""
+    rng = np.random.default_rng(41)
+    if kind == "uniform":
+        xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+        xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
+    else:
+        xb = rng.standard_normal((N, D_)).astype(np.float32)
+        xq = rng.standard_normal((B, D_)).astype(np.float32)
+    dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v", metric=flat.METRIC_L2)
+    assert fq == B and dumps > 0, (dumps, over)
+    if kind == "uniform":  # rows of one scale: the launch's factor bound is tight
+        assert over == 0 and ff == 0, (dumps, over, ff)
+    # Gaussian rows at d = 128: max|x| (the int8 scale) varies ~2x between rows, so
+    # the launch's largest factor passes many more rows than reach a list and
+    # some lists run out of slots; their queries go to the next stage (exactly)
 
 
 @pytest.mark.parametrize("k", [1, 10, 28])
@@ -99,6 +121,22 @@ def test_dump_slot_overflow_hands_queries_on(lib):
     xq = (dup[None, :] + 0.3 * rng.uniform(-1, 1, (B, D_))).astype(np.float32)
     dumps, over, fq, _ = _search_checked(lib, xb, xq, 10)
     assert over > 0, (dumps, over)
+
+
+def test_dump_launches_queries_pointing_away(lib):
+    """Every inner product below 0 (rows in [0, 1), queries in [-1, 0)): the
+    lists' floors are above 0, where the largest row factor bounds nothing (a
+    row with a negative sum scores highest with its SMALLEST factor).  The dump
+    launches take their threshold from the launch's smallest factor there, so
+    the lists stay within their slots and the int8 stage settles the queries
+    instead of handing the whole batch on; the answer is exact either way."""
+    rng = np.random.default_rng(23)
+    xb = rng.uniform(0, 1, (N, D_)).astype(np.float32)
+    xq = -rng.uniform(0, 1, (B, D_)).astype(np.float32)
+    dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v")
+    assert fq == B and dumps > 0
+    assert over <= B * 128 * 0.01, (dumps, over)  # < 1 % of the 128 lane lists per query
+    assert ff <= B // 20, ff
 
 
 def test_dump_launches_bf16_plane(lib):

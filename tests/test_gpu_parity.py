@@ -32,9 +32,10 @@ def vf():
     return vfaiss
 
 
-# Filter-and-verify planes: int8 (the default of inner-product indexes) and
-# bf16; the int8 filter has no L2 form (L2 indexes hold the bf16 plane).
-FILTER_CASES = [(L2, "bf16v"), (IP, "bf16v"), (IP, "i8v")]
+# Filter-and-verify planes: int8 (the first stage by default) and bf16; an L2
+# index's int8 plane holds the augmented rows (L2 as an inner product,
+# vs_gemm_x1.hip quantize_i8_l2aug_kernel).
+FILTER_CASES = [(L2, "bf16v"), (L2, "i8v"), (IP, "bf16v"), (IP, "i8v")]
 
 
 def _rand(n, d, seed, kind="normal"):
@@ -519,33 +520,38 @@ def test_filter_step_shapes(vf, metric, engine, d):
         assert not bad, (d, k, bad[:5])
 
 
-@pytest.mark.parametrize("engine", ["i8v", "bf16v"])
-def test_filter_plane_follows_mutations(vf, engine):
+@pytest.mark.parametrize("metric,engine", [(IP, "i8v"), (IP, "bf16v"), (L2, "i8v")])
+def test_filter_plane_follows_mutations(vf, metric, engine):
     """The filter plane (codes, scales) and residual norms follow add /
     remove_ids / reset / storage growth (kept in step with the rows, never
-    rebuilt lazily)."""
+    rebuilt lazily); for L2 the augmented plane's norms |x'|^2 too, with the
+    augmentation fixed by the first add (later rows of larger norm than the
+    first ones included)."""
     xb = _rand(3000, 96, 42)
+    xb[2500:] *= 3.0  # larger rows after the augmentation is fixed
     xq = _rand(150, 96, 43)
-    index = vf.IndexFlatIP(96)
+    index = vf.IndexFlat(96, metric)
     index.set_engine(engine)
     index.add(xb[:2000])
     D, I = index.search(xq, 10)
+    Dr, Ir = flat.knn_exact(xb[:2000], xq, 10, metric)
+    assert not flat.mismatches(D, I, Dr, Ir, metric, xb[:2000], xq, strict=True)
     for i0 in range(2000, 3000, 250):  # several growths
         index.add(xb[i0:i0 + 250])
     D, I = index.search(xq, 10)
-    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
-    assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
+    assert not flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
     rm = np.arange(100, 3000, 3, dtype=np.int64)
     index.remove_ids(rm)
     xr, _ = flat.remove_ids(xb, rm)
     D, I = index.search(xq, 10)
-    Dr, Ir = flat.knn_exact(xr, xq, 10, IP)
-    assert not flat.mismatches(D, I, Dr, Ir, IP, xr, xq, strict=True)
+    Dr, Ir = flat.knn_exact(xr, xq, 10, metric)
+    assert not flat.mismatches(D, I, Dr, Ir, metric, xr, xq, strict=True)
     index.reset()
     index.add(xb[:50])
     D, I = index.search(xq, 10)
-    Dr, Ir = flat.knn_exact(xb[:50], xq, 10, IP)
-    assert not flat.mismatches(D, I, Dr, Ir, IP, xb[:50], xq, strict=True)
+    Dr, Ir = flat.knn_exact(xb[:50], xq, 10, metric)
+    assert not flat.mismatches(D, I, Dr, Ir, metric, xb[:50], xq, strict=True)
 
 
 @pytest.mark.parametrize("engine", ["fp32", "bf16v", "i8v"])
@@ -633,6 +639,33 @@ def test_filter_matches_exact_engine(vf, metric, engine):
         assert not bad, (k, bad[:5])
         assert (I == Ie).all(axis=1).mean() > 0.99
         np.testing.assert_allclose(D, De, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("engine", ["auto", "i8v", "bf16v"])
+def test_filter_wide_k_inner_product(vf, engine):
+    """Inner product past k = 28 (faiss's rule reads the 2k - 1 best: 64 and,
+    past k = 32, 128 candidates per query — the select kernel, the 128-entry
+    verification and emission): the filter engine answers (the statistics
+    count the batch), exactly; raw lexicographic lists past 64 entries (a
+    shard's half of a sharded k > 32 search) too."""
+    from vsearch import _lib
+
+    xb = _rand(200000, 256, 160)
+    xq = _rand(600, 256, 161)
+    index = vf.IndexFlatIP(256)
+    index.set_engine(engine)
+    index.add(xb)
+    for k in (29, 32, 33, 50, 60, 64):
+        _lib.filter_stats(reset=True)
+        D, I = index.search(xq, k)
+        nq, nfb = _lib.filter_stats(reset=True)
+        assert nq == 600 and nfb <= 6, (k, nq, nfb)
+        Dr, Ir = flat.knn_exact(xb, xq, k, IP)
+        bad = flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True)
+        assert not bad, (k, bad[:5])
+    D, I = index.search(xq, 100, raw=True)
+    Dr, Ir = flat.knn_lex(xb, xq, 100, IP)
+    assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True)
 
 
 @pytest.mark.parametrize("metric,engine", FILTER_CASES)
@@ -726,24 +759,33 @@ def test_filter_wide_check_settles_scattered_near_duplicates(vf, metric, engine)
     assert not bad, bad[:5]
 
 
-def test_filter_engines_agree_and_l2_has_no_int8(vf):
-    """Every filter engine of an inner-product index (the staged default, int8
-    alone, bf16 alone) returns the exact lists; an L2 index holds no int8 plane
-    (the int8 filter has no L2 form) and refuses the int8 engine."""
+@pytest.mark.parametrize("metric", [IP, L2])
+def test_filter_engines_agree(vf, metric):
+    """Every filter engine of an fp32 index (the staged default, int8 alone,
+    bf16 alone) returns the exact lists, for inner product and for L2 (whose
+    int8 plane holds the augmented rows: L2 as an inner product)."""
     xb = _rand(20000, 192, 86)
     xq = _rand(300, 192, 87)
-    index = vf.IndexFlatIP(192)
+    index = vf.IndexFlat(192, metric)
     assert index.filter_planes == ("i8", "bf16")
     index.add(xb)
-    Dr, Ir = flat.knn_exact(xb, xq, 10, IP)
+    Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
     for engine in ("auto", "bf16v", "i8v", "bf16v", "auto"):
         index.set_engine(engine)
         D, I = index.search(xq, 10)
-        assert not flat.mismatches(D, I, Dr, Ir, IP, xb, xq, strict=True), engine
-    l2 = vf.IndexFlatL2(192)
-    assert l2.filter_planes == ("bf16",)
-    with pytest.raises(RuntimeError):
-        l2.set_engine("i8v")
+        assert not flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True), engine
+
+
+def test_l2_int8_plane_stays_out_of_other_metrics(vf):
+    """The augmented int8 plane of an L2 index scores L2 only: the cosine
+    self-join of the same index runs on its bf16 plane, exactly."""
+    x = _rand(2000, 128, 90)
+    index = vf.IndexFlatL2(128)
+    index.add(x)
+    S, I = index.selfjoin(12)
+    Sr, Ir = flat.pgvector_cosine_topk(x, 12)
+    bad = flat.selfjoin_mismatches(S, I, Sr, Ir, x, np.arange(2000), strict=True)
+    assert not bad, bad[:5]
 
 
 def _clustered(n, d, ncent, seed, cseed=5):
