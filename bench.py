@@ -820,12 +820,16 @@ def run_c5(args, ctx):
     def step(i):
         nonlocal mut_time
         if i >= 0 and i % 10 == 9:  # 1 % removes + 1 % appends every 10 batches
+            # the searches already queued finish first (the removal waits for the
+            # index's readers anyway): the time below is the mutation's own
+            torch.cuda.synchronize()
             t0 = time.perf_counter()
             rm = muts[len(done)]
             index.remove_ids(rm)
             g0 = N + len(done) * nmut
             index.append_synthetic_ids(np.arange(g0, g0 + nmut, dtype=np.int64), seed=1234)
             done.append(rm)
+            torch.cuda.synchronize()
             mut_time += time.perf_counter() - t0
         j = (max(i, 0) * B) % (xq.shape[0] - B + 1)
         return index.search_device(xq[j:j + B], k, stream=ctx.stream)

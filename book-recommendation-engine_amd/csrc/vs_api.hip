@@ -53,13 +53,15 @@ struct vs_index {
   // per plane: max |x|^2, max |x - plane(x)|^2, max of their ratio over the
   // rows (the bound's index maxima; grown by add, recomputed by remove_ids)
   unsigned* bstats[2] = {nullptr, nullptr};
-  // L2 indexes: the int8 plane holds the augmented rows x' = [x, e_1 .. e_m]
-  // whose inner product with q' = [q, C .. C] ranks rows as the L2 key does
-  // (launch_quantize_i8_l2aug); m and C are set by the first add (aug_m = 0
-  // before), anorm[r] = |x'_r|^2 (the int8 plane's bound maxima use it)
+  // L2 indexes: both planes hold augmented rows x' = [x, e_1 .. e_m] whose
+  // inner product with q' = [q, C .. C] ranks rows as the L2 key does
+  // (launch_quantize_i8_l2aug, launch_bf16_plane_l2aug); the parameters are
+  // set by the first add (aug_m = 0 before), anorm / anorm_b = |x'|^2 per row
+  // (the planes' bound maxima use them)
   int aug_m = 0;
   L2Aug aug;
   float* anorm = nullptr;
+  float* anorm_b = nullptr;
   // Tombstones (indexes without filter planes, e.g. bf16 storage): removed
   // rows stay in place, NaN-filled (no kernel admits them), until a pack; faiss
   // labels are positions among the live rows (searches map their rows through
@@ -71,7 +73,8 @@ struct vs_index {
   bool tombstones() const { return !plane_on[0] && !plane_on[1]; }
   bool l2aug() const { return metric == VS_METRIC_L2 && esize == 4; }
   int64_t planebytes(int p) const {
-    return (p == FILTER_I8 && l2aug() ? ld + aug_m : ld) * filter_bytes(p);
+    if (!l2aug()) return ld * filter_bytes(p);
+    return (p == FILTER_I8 ? ld + aug_m : ld + kAugBf16) * filter_bytes(p);
   }
   // Adaptive plane order: the int8 stage pays off while it settles most
   // queries; on data where it hands most of them to bf16 (clustered
@@ -499,6 +502,11 @@ int choose_l2aug(vs_index* idx, int64_t n, hipStream_t st) {
   VS_HIP(l2aug_params((const float*)idx->codes, idx->ld, 0, n, idx->norms, &g, st),
          "vs: L2 plane parameters");
   VS_HIP(hipStreamSynchronize(st), "vs: L2 plane");
+  if (!idx->plane_on[FILTER_I8]) {  // the bf16 plane's width does not depend on them
+    idx->aug_m = g.m;
+    idx->aug = g;
+    return VS_OK;
+  }
   VS_HIP(wait_readers(idx), "vs: L2 plane");
   if (idx->fplane[FILTER_I8]) (void)hipFree(idx->fplane[FILTER_I8]);
   idx->fplane[FILTER_I8] = nullptr;
@@ -520,7 +528,8 @@ int choose_l2aug(vs_index* idx, int64_t n, hipStream_t st) {
 // The norms a plane's bound maxima take: |x'|^2 for an L2 index's augmented
 // int8 plane, the stored |x|^2 otherwise.
 const float* plane_norms(const vs_index* idx, int p) {
-  return p == FILTER_I8 && idx->l2aug() && idx->anorm ? idx->anorm : idx->norms;
+  if (!idx->l2aug()) return idx->norms;
+  return p == FILTER_I8 ? idx->anorm : idx->anorm_b;
 }
 
 // The filter plane and residual norms of fp32 rows [r0, r0+n) (after the rows
@@ -532,14 +541,15 @@ int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
     VS_HIP(hipMalloc(&idx->bstats[p], 4 * sizeof(unsigned)), "vs: bound maxima");
     VS_HIP(hipMemsetAsync(idx->bstats[p], 0, 4 * sizeof(unsigned), st), "vs: bound maxima");
   }
+  if (idx->l2aug() && idx->aug_m == 0 && (idx->plane_on[FILTER_I8] || idx->plane_on[FILTER_BF16])) {
+    // the first rows fix the augmentation (and the int8 plane's width)
+    const int64_t n0 = r0 + n;
+    int rc = choose_l2aug(idx, n0, st);
+    if (rc) return rc;
+    r0 = 0;
+    n = n0;
+  }
   if (idx->plane_on[FILTER_I8] && idx->l2aug()) {
-    if (idx->aug_m == 0) {  // the first rows fix the augmentation (and the plane's width)
-      const int64_t n0 = r0 + n;
-      int rc = choose_l2aug(idx, n0, st);
-      if (rc) return rc;
-      r0 = 0;
-      n = n0;
-    }
     if (idx->plane_on[FILTER_I8])
       VS_HIP(launch_quantize_i8_l2aug((const float*)idx->codes, idx->ld, r0, n, idx->aug,
                                       idx->norms, (int8_t*)idx->fplane[FILTER_I8], idx->fscale,
@@ -550,7 +560,12 @@ int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
                               (int8_t*)idx->fplane[FILTER_I8], idx->fscale, idx->rn2[FILTER_I8], st),
            "vs: int8 filter plane");
   }
-  if (idx->plane_on[FILTER_BF16]) {
+  if (idx->plane_on[FILTER_BF16] && idx->l2aug()) {
+    VS_HIP(launch_bf16_plane_l2aug((const float*)idx->codes, idx->ld, r0, n, idx->aug, idx->norms,
+                                   (uint16_t*)idx->fplane[FILTER_BF16], idx->rn2[FILTER_BF16],
+                                   idx->anorm_b, st),
+           "vs: bf16 L2 filter plane");
+  } else if (idx->plane_on[FILTER_BF16]) {
     VS_HIP(launch_bf16_plane((const float*)idx->codes, idx->ld, r0, n,
                              (uint16_t*)idx->fplane[FILTER_BF16], st),
            "vs: bf16 filter plane");
@@ -579,6 +594,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   float* rn2[2] = {nullptr, nullptr};
   float* fscale = nullptr;
   float* anorm = nullptr;
+  float* anorm_b = nullptr;
   // the planes the new storage keeps: committed to the index only once the
   // allocation succeeded (a failed growth leaves the index as it was)
   bool on[2] = {idx->plane_on[0], idx->plane_on[1]};
@@ -593,10 +609,12 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     }
     if (fscale) (void)hipFree(fscale);
     if (anorm) (void)hipFree(anorm);
+    if (anorm_b) (void)hipFree(anorm_b);
     codes = nullptr;
     norms = nullptr;
     fscale = nullptr;
     anorm = nullptr;
+    anorm_b = nullptr;
   };
   auto allocate = [&](int64_t c) -> hipError_t {
     hipError_t e = hipMalloc(&codes, (size_t)c * idx->rowbytes());
@@ -609,6 +627,8 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
       e = hipMalloc(&fscale, (size_t)c * sizeof(float));
     if (e == hipSuccess && on[FILTER_I8] && idx->l2aug())
       e = hipMalloc(&anorm, (size_t)c * sizeof(float));
+    if (e == hipSuccess && on[FILTER_BF16] && idx->l2aug())
+      e = hipMalloc(&anorm_b, (size_t)c * sizeof(float));
     if (e != hipSuccess) {
       (void)hipGetLastError();
       release();
@@ -653,6 +673,9 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   if (anorm)
     VS_HIP(hipMemsetAsync(anorm + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
            "vs: zeroing augmented norms");
+  if (anorm_b)
+    VS_HIP(hipMemsetAsync(anorm_b + keep, 0, (size_t)(cap - keep) * sizeof(float), st),
+           "vs: zeroing augmented norms");
   if (idx->codes && keep > 0) {
     VS_HIP(hipMemcpyAsync(codes, idx->codes, (size_t)keep * idx->rowbytes(),
                           hipMemcpyDeviceToDevice, st),
@@ -679,6 +702,10 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
       VS_HIP(hipMemcpyAsync(anorm, idx->anorm, (size_t)keep * sizeof(float),
                             hipMemcpyDeviceToDevice, st),
              "vs: copying augmented norms");
+    if (anorm_b && idx->anorm_b)
+      VS_HIP(hipMemcpyAsync(anorm_b, idx->anorm_b, (size_t)keep * sizeof(float),
+                            hipMemcpyDeviceToDevice, st),
+             "vs: copying augmented norms");
   }
   // the planes' rows past the kept ones read zeros (after the prefix copy,
   // which brings whole tiles)
@@ -701,6 +728,7 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   }
   idx->fscale = fscale;
   idx->anorm = anorm;
+  idx->anorm_b = anorm_b;
   idx->capacity = cap;
   return VS_OK;
 }
@@ -716,6 +744,8 @@ void free_storage(vs_index* idx) {
   }
   if (idx->fscale) (void)hipFree(idx->fscale);
   if (idx->anorm) (void)hipFree(idx->anorm);
+  if (idx->anorm_b) (void)hipFree(idx->anorm_b);
+  idx->anorm_b = nullptr;
   idx->codes = nullptr;
   idx->norms = nullptr;
   idx->fscale = nullptr;
@@ -871,9 +901,9 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const int qa_rows = gathered ? x.nq_pad : a.nq_pad;  // rows of Q / qaux
   // query plane: a conversion of the stage's queries, or the stored rows' plane
   const bool i8 = plane == FILTER_I8;
-  // L2 on the int8 plane: the pass is the inner product of the augmented rows
-  // and queries (vs_index::aug_m); its lists are mapped to L2 keys after it
-  const bool aug = i8 && mode == MODE_L2;
+  // L2: the pass is the inner product of the augmented rows and queries
+  // (vs_index::aug_m, either plane); its lists are mapped to L2 keys after it
+  const bool aug = mode == MODE_L2 && idx->l2aug();
   if (aug && (idx->aug_m <= 0 || self_rows)) return fail(VS_E_INVALID, "vs: int8 L2 plane");
   const int kmode = aug ? MODE_IP : mode;  // the pass's own metric
   const int64_t pb = idx->planebytes(plane);
@@ -906,6 +936,10 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
                "vs: query plane");
       qs = sc;
       qr2 = r;
+    } else if (aug) {
+      VS_HIP(launch_bf16_plane_l2aug(Q, idx->ld, 0, qa_rows, idx->aug, nullptr, (uint16_t*)qh,
+                                     nullptr, nullptr, st),
+             "vs: query plane");
     } else {
       VS_HIP(launch_bf16_plane(Q, idx->ld, 0, qa_rows, (uint16_t*)qh, st), "vs: query plane");
     }
@@ -945,12 +979,12 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   x.qs = qs;
   x.qaux = qaux;
   x.nqa = qa_rows;
-  x.ld = aug ? idx->ld + idx->aug_m : idx->ld;  // the plane's K
+  x.ld = !aug ? idx->ld : i8 ? idx->ld + idx->aug_m : idx->ld + kAugBf16;  // the plane's K
   x.ntotal = ntotal;
   x.self0 = self_rows ? a.self0 : -1;
   x.qrow = qrow;
   x.qcount = gc;
-  const BoundArgs ba = aug ? make_bound_args_l2aug(idx->ld, idx->aug)
+  const BoundArgs ba = aug ? make_bound_args_l2aug(idx->ld, idx->aug, plane)
                            : make_bound_args(idx->ld, plane);
   if (!gathered && x1_dump_applies(kmode, plane) && dump_enabled() &&
       x1_pass_dumps(ntotal, x.nsplit)) {
@@ -1337,7 +1371,8 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
   bool i8_ok = idx->plane_on[FILTER_I8] && idx->ld + idx->aug_m <= kI8MaxLd &&
                (idx->l2aug() ? mode == MODE_L2 && idx->aug_m > 0 : mode != MODE_L2) &&
                engine != VS_ENGINE_BF16_VERIFY;
-  const bool b16_ok = idx->plane_on[FILTER_BF16] && engine != VS_ENGINE_I8_VERIFY;
+  const bool b16_ok = idx->plane_on[FILTER_BF16] && engine != VS_ENGINE_I8_VERIFY &&
+                      (idx->l2aug() ? mode == MODE_L2 && idx->aug_m > 0 : true);
   const bool staged = idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0 &&
                       nq > kSkinnyMaxQ && (i8_ok || b16_ok);
   // more entries than one exact page holds (inner product k > 32, raw k > 64)
@@ -1416,9 +1451,38 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
     if (b16_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);
   }
   if (need > VS_MAX_K) return run_wide_k(idx, a, st);
+  // No plane serves this metric (the cosine self-join of an L2 index, whose
+  // planes hold the rows augmented for L2): the staged engine's last stage over
+  // every query — the exact fp32 GEMM, its candidates rescored in fp64 — so the
+  // keys are the same exact roundings the planes' searches return.
+  const int bp = idx->bstats[FILTER_BF16] ? FILTER_BF16 : idx->bstats[FILTER_I8] ? FILTER_I8 : -1;
+  if (idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0 &&
+      nq > kSkinnyMaxQ && bp >= 0) {
+    int* gl = nullptr;
+    int* gc = nullptr;
+    VS_HIP(scr.alloc((void**)&gl, (size_t)a.nq_pad * sizeof(int)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&gc, sizeof(int)), "vs: scratch");
+    VS_HIP(launch_iota(gl, nq, gc, st), "vs: every query");
+    return run_gemm_rescored(idx, a, need, KF, bp, st, gl, gc);
+  }
   return run_gemm(idx, a, need, st);
 }
 
+}  // namespace
+
+namespace {
+int pack_dead(vs_index* idx);
+int pack_den();
+
+// Room for n more rows: tombstones are packed first when the rows in place
+// would otherwise outgrow the storage, then the storage grows if it must.
+int make_room(vs_index* idx, int64_t n, hipStream_t st) {
+  if (!idx->dead.empty() && idx->ntotal + n + 256 > idx->capacity) {
+    const int rc = pack_dead(idx);
+    if (rc) return rc;
+  }
+  return ensure_capacity(idx, idx->ntotal + n, st);
+}
 }  // namespace
 
 extern "C" {
@@ -1498,7 +1562,11 @@ int vs_reserve(vs_index* idx, int64_t n) {
   if (n < 0) return fail(VS_E_INVALID, "vs_reserve: n < 0");
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
-  return ensure_capacity(idx, std::max(n, idx->ntotal), nullptr);
+  // an index that tombstones its removals keeps room for the appends that
+  // come before the next pack (1 / pack_den of the rows): at C5's size a
+  // storage growth (a copy beside the old rows) does not fit in HBM
+  const int64_t want = std::max(n, idx->ntotal);
+  return ensure_capacity(idx, idx->tombstones() ? want + want / pack_den() : want, nullptr);
 }
 
 int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
@@ -1511,7 +1579,7 @@ int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
-  int rc = ensure_capacity(idx, idx->ntotal + n, st);
+  int rc = make_room(idx, n, st);
   if (rc) return rc;
   const hipMemcpyKind kind = (flags & VS_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (idx->esize == 4) {
@@ -1555,7 +1623,7 @@ int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void
   hipStream_t st = (hipStream_t)stream;
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
-  int rc = ensure_capacity(idx, idx->ntotal + n, st);
+  int rc = make_room(idx, n, st);
   if (rc) return rc;
   VS_HIP(launch_fill_synthetic(idx->row(idx->ntotal), idx->esize, n, idx->d, idx->ld, seed, row0,
                                st),
@@ -1580,7 +1648,7 @@ int vs_add_synthetic_ids(vs_index* idx, const int64_t* ids, int64_t n, uint64_t 
   hipStream_t st = (hipStream_t)stream;
   std::unique_lock<std::shared_mutex> lk(idx->mu);
   DeviceGuard g(idx->device);
-  int rc = ensure_capacity(idx, idx->ntotal + n, st);
+  int rc = make_room(idx, n, st);
   if (rc) return rc;
   Scratch scr(st);
   int64_t* dids = nullptr;
@@ -1774,7 +1842,6 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
 namespace {
 int reconstruct_rows(vs_index* idx, int64_t i0, int64_t n, float* out, int flags, hipStream_t st);
 int64_t row_of_label(const vs_index* idx, int64_t l);
-int pack_dead(vs_index* idx);
 }  // namespace
 
 extern "C" {
@@ -1922,6 +1989,9 @@ int compact_rows(vs_index* idx, const std::vector<int64_t>& rm, hipStream_t st) 
            "vs_remove_ids: zero tail");
   if (idx->anorm)
     VS_HIP(hipMemsetAsync(idx->anorm + nt, 0, (size_t)nrem * sizeof(float), st),
+           "vs_remove_ids: zero tail");
+  if (idx->anorm_b)
+    VS_HIP(hipMemsetAsync(idx->anorm_b + nt, 0, (size_t)nrem * sizeof(float), st),
            "vs_remove_ids: zero tail");
   VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
   idx->ntotal = nt;

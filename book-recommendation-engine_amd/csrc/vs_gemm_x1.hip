@@ -1520,6 +1520,76 @@ hipError_t launch_quantize_i8_l2aug(const float* X, int64_t ld, int64_t r0, int6
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void bf16_plane_l2aug_kernel(
+    const float* __restrict__ X, int64_t ld, int64_t r0, int64_t n, float Cb, float nref,
+    const float* __restrict__ norms, uint16_t* __restrict__ plane, float* __restrict__ rn2,
+    float* __restrict__ anorm) {
+  constexpr int m = kAugBf16;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* xr = X + (r0 + row) * ld;
+  const int64_t pld = ld + m;
+  char* base = (char*)plane;
+  const bool rows = norms != nullptr;
+  const double E = rows ? ((double)nref - (double)norms[r0 + row]) / (2.0 * (double)Cb) : 0.0;
+  const uint16_t eb = rows ? f32_to_bf16_rne((float)(E / m)) : f32_to_bf16_rne(Cb);
+  const double es = (double)__uint_as_float((uint32_t)eb << 16);  // a stored extra entry
+  double acc = 0.0, sq = 0.0;
+  bool bad = !isfinite(E);
+  for (int64_t c = lane * 4; c < pld; c += 256) {
+    uint32_t lo, hi;
+    if (c < ld) {
+      const f32x4 v = *(const f32x4*)(xr + c);
+      uint16_t b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        b[i] = f32_to_bf16_rne(v[i]);
+        bad |= !isfinite(v[i]);
+        const double h = (double)__uint_as_float((uint32_t)b[i] << 16);
+        const double r = (double)v[i] - h;
+        acc += r * r;
+        sq += (double)v[i] * (double)v[i];
+      }
+      lo = (uint32_t)b[0] | ((uint32_t)b[1] << 16);
+      hi = (uint32_t)b[2] | ((uint32_t)b[3] << 16);
+    } else {  // the extra block (pld = ld + m)
+      lo = (uint32_t)eb | ((uint32_t)eb << 16);
+      hi = lo;
+    }
+    *(uint2*)(base + plane_offset(r0 + row, 2 * c, 2 * pld)) = make_uint2(lo, hi);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    acc += __shfl_xor(acc, o);
+    sq += __shfl_xor(sq, o);
+  }
+  bad = __any(bad);
+  if (lane == 0 && rows) {
+    auto up = [](double v) {
+      float f = (float)v;
+      if ((double)f < v) f = nextafterf(f, INFINITY);
+      return f;
+    };
+    // e_j = es + delta, delta = (E - m es) / m: the extra block's residual is
+    // m delta^2 (E's fp64 rounding in the margin)
+    const double d1 = (E - m * es) / m;
+    const double dlt = fabs(d1) + fabs(E) * 1e-15 / m;
+    rn2[r0 + row] = bad ? INFINITY : up((acc + m * dlt * dlt) * (1.0 + 1e-12));
+    anorm[r0 + row] = bad ? INFINITY : up((sq + m * (es + d1) * (es + d1)) * (1.0 + 1e-12) + 1e-30);
+  }
+}
+
+hipError_t launch_bf16_plane_l2aug(const float* X, int64_t ld, int64_t r0, int64_t n,
+                                   const L2Aug& g, const float* norms, uint16_t* plane, float* rn2,
+                                   float* anorm, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ld % 64 != 0 || !(g.Cb > 0.0f) || !std::isfinite(g.nref) || (norms && (!rn2 || !anorm)))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bf16_plane_l2aug_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X,
+                     ld, r0, n, g.Cb, g.nref, norms, plane, rn2, anorm);
+  return hipGetLastError();
+}
+
 // The augmentation's statistics, two passes over the first rows: nref < 0:
 // acc[0] += max|x| over the nonzero rows, acc[1] += their count, acc[2] = the
 // largest norm; nref >= 0: acc[3] = max |nref - n_x| / max|x| (bits of a
@@ -1573,6 +1643,7 @@ hipError_t l2aug_params(const float* X, int64_t ld, int64_t r0, int64_t n, const
   out->m = 64;
   out->C = 1.0f;
   out->nref = 0.0f;
+  out->Cb = 1.0f;
   if (n <= 0) return hipSuccess;
   double* acc = nullptr;
   hipError_t e = hipMalloc(&acc, 4 * sizeof(double));
@@ -1599,6 +1670,7 @@ hipError_t l2aug_params(const float* X, int64_t ld, int64_t r0, int64_t n, const
       const double need = h[3] / (2.0 * c);
       out->C = (float)c;
       out->nref = nref;
+      out->Cb = std::ldexp(1.0f, (int)std::lround(std::log2(c)));
       out->m = (int)std::min<double>(4096.0, std::max(64.0, std::ceil(need / 64.0) * 64.0));
     }
   }
@@ -1845,10 +1917,10 @@ __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow
     r += __shfl_xor(r, o);
     n += __shfl_xor(n, o);
   }
-  qh2 = a;
-  qr2 = r;
+  qh2 = a + aug;  // aug: |q'|^2 = |q|^2 + m C^2 (the augmented L2 planes; exact
+  qr2 = r;        // in bf16, whose extra entries are a power of two)
   qn2 = n;
-  if (qr2i8) {  // aug: |q'|^2 = |q|^2 + m C^2 (the augmented L2 plane)
+  if (qr2i8) {
     qr2 = (double)*qr2i8;
     const double hq = sqrt(n + aug) + sqrt(qr2);
     qh2 = hq * hq;
@@ -2605,10 +2677,12 @@ BoundArgs make_bound_args(int64_t ld, int filter) {
   return ba;
 }
 
-BoundArgs make_bound_args_l2aug(int64_t ld, const L2Aug& g) {
-  BoundArgs ba = make_bound_args(ld + g.m, FILTER_I8);
+BoundArgs make_bound_args_l2aug(int64_t ld, const L2Aug& g, int filter) {
+  const bool i8 = filter == FILTER_I8;
+  BoundArgs ba = make_bound_args(ld + (i8 ? g.m : kAugBf16), filter);
   ba.l2aug = 1;
-  ba.aug_q2 = (double)g.m * (double)g.C * (double)g.C;
+  const double c = i8 ? (double)g.C : (double)g.Cb;
+  ba.aug_q2 = (i8 ? (double)g.m : (double)kAugBf16) * c * c;
   ba.aug_nref = (double)g.nref;
   return ba;
 }

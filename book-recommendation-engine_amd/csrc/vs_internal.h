@@ -168,12 +168,16 @@ struct BoundArgs {
 BoundArgs make_bound_args(int64_t ld, int filter);
 // The augmentation of an L2 index's int8 plane (launch_quantize_i8_l2aug).
 struct L2Aug {
-  int m = 0;          // extra columns (a multiple of 64)
-  float C = 0.0f;     // the queries' extra entry
+  int m = 0;          // int8 extra columns (a multiple of 64)
+  float C = 0.0f;     // the queries' extra entry (int8 plane)
   float nref = 0.0f;  // reference norm: the rows' extra entries sum to (nref - n_x) / (2 C)
+  float Cb = 0.0f;    // bf16 plane: the queries' extra entry (C's power of two, exact in bf16)
 };
-// The bound constants for an L2 index's augmented int8 plane.
-BoundArgs make_bound_args_l2aug(int64_t ld, const L2Aug& g);
+// Extra columns of an L2 index's augmented bf16 plane (bf16 has no per-row
+// scale to keep the extra entries within: one 64-element block).
+constexpr int kAugBf16 = 64;
+// The bound constants for an L2 index's augmented int8 / bf16 plane.
+BoundArgs make_bound_args_l2aug(int64_t ld, const L2Aug& g, int filter = FILTER_I8);
 // out[0..3) = bits of max norms, max rn2, max rn2/norms over rows [0, n).
 // accumulate: fold rows [0, n) into the maxima already in out (no reset).
 hipError_t launch_bound_stats(const float* norms, const float* rn2, int64_t n, unsigned* out,
@@ -203,6 +207,15 @@ hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n,
 hipError_t launch_quantize_i8_l2aug(const float* X, int64_t ld, int64_t r0, int64_t n,
                                     const L2Aug& g, const float* norms, int8_t* codes,
                                     float* scale, float* rn2, float* anorm, hipStream_t st);
+// The same augmentation on the bf16 plane (plane rows of ld + kAugBf16
+// elements): rows (norms != nullptr) get kAugBf16 equal extra entries
+// bf16(E / kAugBf16), E = (nref - n_x) / (2 Cb) (the conceptual entries add an
+// even share of E minus their sum: residual |E - sum|^2 / kAugBf16), rn2 =
+// |x' - plane(x')|^2 and anorm = |x'|^2 rounded up; queries (norms == nullptr)
+// get Cb (exact: a power of two).
+hipError_t launch_bf16_plane_l2aug(const float* X, int64_t ld, int64_t r0, int64_t n,
+                                   const L2Aug& g, const float* norms, uint16_t* plane, float* rn2,
+                                   float* anorm, hipStream_t st);
 // The augmentation's parameters from fp32 rows [r0, r0+n): C = the mean of
 // max|x| over the nonzero rows, nref = the largest norm, m = the extra columns
 // that keep every row's extra entries within its own max|x|
@@ -365,6 +378,8 @@ hipError_t launch_fill_empty(int mode, float* D, int64_t* I, int64_t n, hipStrea
 // Stable compaction helper: copy the kept rows of [src0, src0+n) into tmp,
 // given the sorted removed-row list (device).  Also moves the norms.
 // Rows are `rowbytes` long (multiple of 16).
+// out[0 .. n) = 0 .. n-1 and *count = n (device): a gathered batch of every query.
+hipError_t launch_iota(int* out, int n, int* count, hipStream_t st);
 // Tombstones: rows[0 .. n) (device) filled with NaN elements and a NaN norm;
 // the labels I[0 .. n) of a search (kernel rows + id_base) mapped to positions
 // among the live rows (dead: the sorted tombstoned rows, ndead of them).

@@ -781,6 +781,20 @@ hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbyte
   return hipGetLastError();
 }
 
+// out[i] = i for i < n, *count = n: a gathered batch that is every query.
+__global__ __launch_bounds__(256) void iota_kernel(int* __restrict__ out, int n,
+                                                   int* __restrict__ count) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = i;
+  if (i == 0) *count = n;
+}
+
+hipError_t launch_iota(int* out, int n, int* count, hipStream_t st) {
+  if (n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, n, count);
+  return hipGetLastError();
+}
+
 // Tombstones (vs_api.hip, vs_remove_ids on an index without filter planes):
 // the removed rows keep their place until a pack, filled with NaN (fp32
 // 0x7FC00000, bf16 0x7FC0) and a NaN norm, so every kernel's strict admission

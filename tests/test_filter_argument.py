@@ -291,6 +291,62 @@ def test_int8_l2_augmented_bound_holds():
     assert np.median(B[6:]) < 0.25 * spread, (np.median(B[6:]), spread)
 
 
+def _bf16(x):
+    """Round-to-nearest-even bf16 (as float32 values)."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16 << 16
+    return u.astype(np.uint32).view(np.float32)
+
+
+def test_bf16_l2_augmented_bound_holds():
+    """The bf16 plane's form of L2 as an inner product (vs_gemm_x1.hip
+    bf16_plane_l2aug_kernel): x' = [bf16(x), 64 x bf16(E / 64)], E = (nref -
+    n_x) / (2 Cb), q' = [bf16(q), Cb ..] with Cb a power of two (exact); the
+    MFMA accumulates the products in fp32 (any order: gamma(ld + 1)); the list
+    key max(0, fl(fl(qn + nref) - 2 fl(sum))) is within the bound of faiss's
+    L2 key for every pair."""
+    rng = np.random.default_rng(22)
+    d, m = 1536, 64
+    x = _rows(rng, 48, d)
+    q = _rows(rng, 12, d)
+    q[6] = x[10]
+    xn = (x.astype(np.float32) ** 2).sum(axis=1, dtype=np.float32)
+    qn = (q.astype(np.float32) ** 2).sum(axis=1, dtype=np.float32)
+    _, C, nref = _l2aug_params(x[6:], xn[6:])
+    Cb = float(2.0 ** np.round(np.log2(C)))
+    E = (np.float64(nref) - xn.astype(np.float64)) / (2 * Cb)
+    es = _bf16((E / m).astype(np.float32)).astype(np.float64)
+    d1 = (E - m * es) / m
+    hx_rows = np.concatenate([_bf16(x), np.repeat(es[:, None], m, axis=1).astype(np.float32)], 1)
+    hq_rows = np.concatenate([_bf16(q), np.full((q.shape[0], m), Cb, np.float32)], 1)
+    r = x.astype(np.float64) - _bf16(x).astype(np.float64)
+    rx2 = (r * r).sum(axis=1) + m * (np.abs(d1) + np.abs(E) * 1e-15 / m) ** 2
+    ax2 = (x.astype(np.float64) ** 2).sum(axis=1) + m * (es + d1) ** 2
+    # fp32 accumulation in row order (one of the orders the bound covers)
+    prod = hq_rows.astype(np.float32)[:, None, :] * hx_rows.astype(np.float32)[None, :, :]
+    s32 = np.zeros(prod.shape[:2], np.float32)
+    for j in range(prod.shape[2]):
+        s32 = (s32 + prod[:, :, j]).astype(np.float32)
+    A = -s32
+    qr = (qn + np.float32(nref)).astype(np.float32)
+    Ahat = np.maximum(np.float32(0), (qr[:, None] + np.float32(2) * A).astype(np.float32))
+    ip = (q.astype(np.float64) @ x.astype(np.float64).T).astype(np.float32)
+    K = np.maximum(np.float32(0), ((qn[:, None] + xn[None, :]).astype(np.float32)
+                                   - np.float32(2) * ip).astype(np.float32))
+    n_ = d + m + 1
+    gam = n_ * 2.0 ** -23 / (1 - n_ * 2.0 ** -23)
+    qr_ = q.astype(np.float64) - _bf16(q).astype(np.float64)
+    rq = np.sqrt((qr_ * qr_).sum(axis=1))
+    hq = np.sqrt((_bf16(q).astype(np.float64) ** 2).sum(axis=1) + m * Cb * Cb)
+    hx = np.sqrt(ax2.max()) + np.sqrt(rx2.max())
+    rx = np.sqrt(rx2.max())
+    b = (gam * hx * hq + hx * rq + rx * hq + rx * rq) * (1 + 1e-6)
+    B = (2 * b + 8 * _U * (qn.astype(np.float64) + ax2.max())
+         + 2 * _U * (qn.astype(np.float64) + nref + 2.01 * hx * hq)) * (1 + 1e-6)
+    err = np.abs(Ahat.astype(np.float64) - K.astype(np.float64))
+    assert (err <= B[:, None]).all(), float((err - B[:, None]).max())
+
+
 def test_wide_threshold_below_the_floor_is_exact():
     """The wide check may use any T' <= T (vs_gemm_x1.hip verify_wide_kernel):
     with a_M the M-th smallest approximate key, T' = min(T, a_M + 2.000001 B)
