@@ -85,7 +85,13 @@ namespace {
 constexpr int kT = 256;               // rows (and queries) per tile
 constexpr int kNbuf = 5;              // LDS images in the ring (4: -1 %, profiles/r02y)
 constexpr int kX1ChunkTiles = 64;     // database tiles per workgroup per launch
-constexpr int kDumpMaxR = 64;         // dump slots (candidate rows) per lane list and segment
+// dump slots (candidate rows) per lane list and segment: a segment of
+// doubling data meets ~8 rows below a list's floor, a hybrid launch's dump part
+// (three times its list part) ~24, with a tail: the dump part beats the list
+// part's 8th row at least n times when at most 7 of the best 8 + n rows lie in
+// the list part, Binomial(8 + n, 1/4) <= 7: ~2e-4 per list at n = 64 (a fifth of
+// C2's queries, with 512 lists each, handed on), ~1e-8 at n = 128
+constexpr int kDumpMaxR = 128;
 // The step schedule of a launch: 1 = fragment reads half a step ahead, DMA
 // pieces between the MFMAs; 2 = separate load and matrix segments.  Measured
 // per plane and launch kind (A/B builds: VS_X1_SCHED_I8 forces one for every
@@ -96,8 +102,9 @@ constexpr int kDumpMaxR = 64;         // dump slots (candidate rows) per lane li
 #ifndef VS_X1_SCHED_I8
 #define VS_X1_SCHED_I8 0
 #endif
-constexpr int x1_sched(int el, bool dump) {
-  return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump ? 2 : 1;
+// A hybrid launch (mostly dump tiles) takes the dump launches' schedule.
+constexpr int x1_sched(int el, bool dump, bool hyb = false) {
+  return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump || hyb ? 2 : 1;
 }
 // The passes with a dump form: inner product on either plane (every key
 // follows from the raw sum and, for int8, the row factor the replay reads).
@@ -241,7 +248,7 @@ __device__ __forceinline__ float x1_key(int sum_bits, float qsc, float fx) {
 // slices (QG x 16 KB per step) and serves a database tile to QG workgroups;
 // slot / QG orders the splits, so with two rounds of workgroups per CU each
 // round covers its own DG / 2 splits.  Other grids: a plain dealing.
-template <int KR, int MODE, bool DUMP, int EL>
+template <int KR, int MODE, bool DUMP, int EL, bool HYB = false>
 __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ XH, const float* __restrict__ xs, const float* __restrict__ xaux,
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
@@ -251,6 +258,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const float* __restrict__ xgmin, const float* __restrict__ qcut, int* __restrict__ dcount,
     int* __restrict__ dslot, int dR) {
   static_assert(!DUMP || x1_has_dump(MODE, EL), "dump form");
+  static_assert(!HYB || (!DUMP && x1_has_dump(MODE, EL)), "hybrid launch");
   constexpr int NBUF = kNbuf;
   constexpr int kStepB = kT * 64;  // one operand tile of one 32-element step: 16 KB
   constexpr int D = NBUF - 1;      // steps in flight
@@ -290,6 +298,11 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
   const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
   const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
+  // Hybrid launch: the first quarter of the workgroup's tiles as a list
+  // launch, the rest as a dump launch whose floor is each list's own last
+  // entry after that quarter (a top-8 list over n rows is beaten by ~8 of every
+  // next n: ~24 dumps per list, within the slots)
+  const int tsw = HYB ? t0 + (t1 - t0 + 3) / 4 : t1;
 
   int gq[2], selfrow[2];
   float qa[2], qsc[2];
@@ -308,11 +321,14 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   // List launches: the lane's sorted lists (admission limit: the last entry).
   // Dump launches: the query's cut (padding queries: nothing passes) and the
   // lane list's running dump count over the search's launches.
-  constexpr int KL = DUMP ? 1 : KR;  // dump launches keep no list (1: a dummy)
+  // dump launches keep no list (the arrays are never touched there: no
+  // registers); the epilogue's list branch is a template of its dump tag, so
+  // it must type-check in every kernel
+  constexpr int KL = KR;
   float lk[2][KL];
   int li[2][KL];
-  float tq[2];
-  int dc[2];
+  float tq[2] = {0.0f, 0.0f};
+  int dc[2] = {0, 0};
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     if constexpr (DUMP) {
@@ -342,11 +358,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     asm volatile("" ::"v"(qa[qb]));
     if constexpr (EL == FILTER_I8) asm volatile("" ::"v"(qsc[qb]));
   }
-  // a block's admission limit: the list's last entry, or the cut
-  auto lim = [&](int qb) -> float {
-    if constexpr (DUMP) return tq[qb];
-    else return lk[qb][KL - 1];
-  };
 
   if (t1 > t0) {  // uniform over the workgroup
     // Planes are tile-major (vs_internal.h plane_offset): the 64-B step s of
@@ -384,7 +395,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // of address arithmetic and M0 saves
     // (inner product only: the bf16 L2 / cosine list kernels have no registers
     // to spare for the two lane offsets)
-    constexpr bool kSeg = x1_sched(EL, DUMP) == 2 && MODE == MODE_IP;
+    constexpr bool kSeg = x1_sched(EL, DUMP, HYB) == 2 && MODE == MODE_IP;
     const char* xstep = nullptr;
     const char* qstep = nullptr;
     uint32_t xl0 = 0, xl2 = 0;
@@ -407,18 +418,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // clear the limit only if fl(sum * fl(s_q * fmin)) does (rows with sums
     // >= 0 always clear it, and the threshold is below 0).
     int Tq[2] = {0, 0};
-    if constexpr (DUMP && EL == FILTER_I8) {
-      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      float fm = 0.0f, fn = FLT_MAX;
-      for (int g = 16 * t0 + ln; g < 16 * t1; g += 64) {
-        fm = fmaxf(fm, xgmax[g]);
-        fn = fminf(fn, xgmin[g]);
-      }
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        fm = fmaxf(fm, __shfl_xor(fm, m));
-        fn = fminf(fn, __shfl_xor(fn, m));
-      }
+    float fm = 0.0f, fn = FLT_MAX;  // the dump tiles' largest and smallest row factors
+    auto set_Tq = [&]() {
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         const float c = qsc[qb] * fm, cn = qsc[qb] * fn, last = tq[qb];
@@ -428,7 +429,56 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                                                                 : INT_MAX;
         asm volatile("" ::"v"(Tq[qb]));
       }
+    };
+    // the launch's (a hybrid launch: its dump part's) largest and smallest
+    // row factor
+    auto set_factor_bounds = [&](int ta) {
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      for (int g = 16 * ta + ln; g < 16 * t1; g += 64) {
+        fm = fmaxf(fm, xgmax[g]);
+        fn = fminf(fn, xgmin[g]);
+      }
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        fm = fmaxf(fm, __shfl_xor(fm, m));
+        fn = fminf(fn, __shfl_xor(fn, m));
+      }
+    };
+    if constexpr (DUMP && EL == FILTER_I8) {
+      set_factor_bounds(t0);
+      set_Tq();
     }
+    // Hybrid launch, at the end of its list part: the lists go to memory (the
+    // replay after the launch admits the dumps into them), each list's floor
+    // for the dump part is min(cut, its last entry)
+    auto to_dump_mode = [&]() {
+      if constexpr (HYB) {
+        const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const int pl1 = sp * 4 + wr * 2 + (ln >> 5);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          const int64_t g = (int64_t)(qt * kT + 64 * wq + 32 * qb + (ln & 31)) * P + pl1;
+          const int64_t o = g * KP;
+#pragma unroll
+          for (int e = 0; e < KR; ++e) {
+            pkey[o + e] = lk[qb][e];
+            pid[o + e] = li[qb][e];
+          }
+          for (int e = KR; e < KP; ++e) {
+            pkey[o + e] = FLT_MAX;
+            pid[o + e] = -1;
+          }
+          const float tl = fminf(qcut[gq[qb]], li[qb][KR - 1] >= 0 ? lk[qb][KR - 1] : FLT_MAX);
+          tq[qb] = gq[qb] < nqa ? tl : -FLT_MAX;
+          dc[qb] = dcount[g];
+          asm volatile("" ::"v"(tq[qb]), "v"(dc[qb]));
+        }
+        if constexpr (EL == FILTER_I8) {
+          set_factor_bounds(tsw);
+          set_Tq();
+        }
+      }
+    };
 
     AccT<EL> acc[4][2];
     // fragments of one sub-step: A (database rows) x4, B (queries) x2
@@ -536,7 +586,14 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #define VS_X1_COUNT(i, v) ((void)0)
 #define VS_X1_EMARK(i) ((void)0)
 #endif
-    auto epilogue = [&](int t) {
+    auto epilogue = [&](int t, auto dm_tag) {
+      // dm_tag: a dump launch's epilogue (also the dump part of a hybrid one)
+      constexpr bool DM = decltype(dm_tag)::value;
+      // a block's admission limit: the list's last entry, or the floor
+      auto lim = [&](int qb) -> float {
+        if constexpr (DM) return tq[qb];
+        else return lk[qb][KL - 1];
+      };
       // uniform: every row of the tile exists and none is excluded
       const bool plain = self0 < 0 && !qrow && (t + 1) * kT <= ntotal;
       const int f = tile_perm(t);
@@ -566,7 +623,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         fmx[rb] = 0.0f;
-        if constexpr (EL == FILTER_I8 && !DUMP) {
+        if constexpr (EL == FILTER_I8 && !DM) {
           const int grp = (t * kT + ((128 * wr + 32 * rb) ^ (f & 0xE0))) >> 5;  // uniform
           const float g0 = xgmax[2 * grp], g1 = xgmax[2 * grp + 1];
           fmx[rb] = (fh & 4) ? g1 : g0;
@@ -585,7 +642,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         for (int qb = 0; qb < 2; ++qb) {
           const float last = lim(qb);
           bool p;
-          if constexpr (EL == FILTER_I8 && DUMP) {
+          if constexpr (EL == FILTER_I8 && DM) {
             int amax = acc[rb][qb][0];
 #pragma unroll
             for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
@@ -616,7 +673,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
         asm volatile("" ::"v"(pass));
         pass = 0;
       }
-      if constexpr (DUMP) {
+      if constexpr (DM) {
         // Dump launch: every row of a block that passed whose sum clears the
         // limit (int8: above the launch's integer threshold; bf16: -sum below
         // the limit) goes to the lane list's
@@ -654,7 +711,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
                   int sum;
                   if constexpr (EL == FILTER_I8) sum = sel16i(acc[rb][qb], bi);
                   else sum = __float_as_int(sel16(acc[rb][qb], bi));
-                  const int64_t slot = ((int64_t)gq[qb] * P + pl) * dR + c;
+                  // slot-major (slot c of every list together): the replay's
+                  // threads, one per list, read their c-th slots coalesced
+                  const int64_t slot = (int64_t)c * ((int64_t)nqt * kT * P) + (int64_t)gq[qb] * P + pl;
                   *(i32x2*)(dslot + slot * 2) = i32x2{row, sum};
                 }
               }
@@ -681,7 +740,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       // row blocks per load group: 2 under the segmented schedule; 1 under the
       // round-2 schedule, whose next-step fragments stay live across the
       // epilogue (registers)
-      constexpr int G = x1_sched(EL, DUMP) != 1 ? 2 : 1;
+      constexpr int G = x1_sched(EL, DUMP, HYB) != 1 ? 2 : 1;
 #pragma unroll
       for (int hp = 0; hp < 4 / G; ++hp) {
         f32x4 rv[G][4];
@@ -792,7 +851,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
     };
 
-    constexpr int kSched = x1_sched(EL, DUMP);
+    constexpr int kSched = x1_sched(EL, DUMP, HYB);
     if constexpr (kSched == 1) {
 
     // prologue: steps 0 .. D-1 in flight, retire step 0, read its first fragments
@@ -880,18 +939,30 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       VS_X1_MARK1(5);
       buf = nbuf;
     };
-    for (int t = t0; t < t1; ++t) {
-      s1_step(std::true_type{});
-      for (int k = 1; k < nksteps; ++k) s1_step(std::false_type{});
-      if constexpr (!VS_X1_P(8)) {
-        epilogue(t);
-      } else {
+    // tiles [ta, tb) with the epilogue of kind DM (a hybrid launch: its list
+    // part, then its dump part — two loops, so the lists are dead in the
+    // second)
+    auto s1_tiles = [&](int ta, int tb, auto dm_tag) {
+      for (int t = ta; t < tb; ++t) {
+        s1_step(std::true_type{});
+        for (int k = 1; k < nksteps; ++k) s1_step(std::false_type{});
+        if constexpr (!VS_X1_P(8)) {
+          epilogue(t, dm_tag);
+        } else {
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+          for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+            for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+        }
+        VS_X1_MARK1(5);
       }
-      VS_X1_MARK1(5);
+    };
+    if constexpr (HYB) {
+      s1_tiles(t0, tsw, std::false_type{});
+      to_dump_mode();
+      s1_tiles(tsw, t1, std::true_type{});
+    } else {
+      s1_tiles(t0, t1, std::integral_constant<bool, DUMP>{});
     }
 #undef VS_X1_MARK1
     } else {
@@ -968,19 +1039,28 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       VS_X1_MARK(5);
       buf = buf + 1 == NBUF ? 0 : buf + 1;
     };
-    for (int t = t0; t < t1; ++t) {
-      seg_step(std::true_type{});
-      for (int k = 1; k < nksteps; ++k) seg_step(std::false_type{});
-      // the tile's epilogue, beside the partner's matrix segment
-      if constexpr (!VS_X1_P(8)) {
-        epilogue(t);
-      } else {
+    auto seg_tiles = [&](int ta, int tb, auto dm_tag) {
+      for (int t = ta; t < tb; ++t) {
+        seg_step(std::true_type{});
+        for (int k = 1; k < nksteps; ++k) seg_step(std::false_type{});
+        // the tile's epilogue, beside the partner's matrix segment
+        if constexpr (!VS_X1_P(8)) {
+          epilogue(t, dm_tag);
+        } else {
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+          for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+            for (int qb = 0; qb < 2; ++qb) asm volatile("" ::"v"(acc[rb][qb]));
+        }
+        VS_X1_MARK(5);
       }
-      VS_X1_MARK(5);
+    };
+    if constexpr (HYB) {
+      seg_tiles(t0, tsw, std::false_type{});
+      to_dump_mode();
+      seg_tiles(tsw, t1, std::true_type{});
+    } else {
+      seg_tiles(t0, t1, std::integral_constant<bool, DUMP>{});
     }
     if (!lag) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
 #undef VS_X1_MARK
@@ -1005,11 +1085,19 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   // across the main loop: registers)
   const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const int pl0 = sp * 4 + wr * 2 + (ln >> 5);
+  // (a hybrid launch stored its lists at the switch, which every workgroup
+  // with a tile reaches: its lists are dead past it, registers)
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int64_t g = (int64_t)(qt * kT + 64 * wq + 32 * qb + (ln & 31)) * P + pl0;
-    if constexpr (DUMP) {
+    if (DUMP || (HYB && t1 > t0)) {
       dcount[g] = dc[qb];
+    } else if (HYB) {  // no tile: empty lists
+      const int64_t o = g * KP;
+      for (int e = 0; e < KP; ++e) {
+        pkey[o + e] = FLT_MAX;
+        pid[o + e] = -1;
+      }
     } else {
       const int64_t o = g * KP;
 #pragma unroll
@@ -1039,8 +1127,8 @@ template <int KR, int EL>
 __global__ __launch_bounds__(256) void x1_replay_kernel(
     int* __restrict__ dcount, const int* __restrict__ dslot, float* __restrict__ pkey,
     int* __restrict__ pid, int P, int KP, int nqa, const float* __restrict__ qs,
-    const float* __restrict__ xs, int64_t self0, int ntotal, int dR, float* __restrict__ qcut,
-    unsigned long long* __restrict__ stats) {
+    const float* __restrict__ xs, int64_t self0, int ntotal, int dR, int64_t nl,
+    float* __restrict__ qcut, unsigned long long* __restrict__ stats) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int cnt = i < (int64_t)nqa * P ? dcount[i] : 0;
   {  // statistics: one atomic per wave
@@ -1072,13 +1160,26 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
     lk[e] = pkey[o + e];
     li[e] = pid[o + e];
   }
-  const i32x2* sl = (const i32x2*)(dslot + i * dR * 2);
-  for (int c = 0; c < cnt; ++c) {
-    const i32x2 e = sl[c];
-    const int row = e[0];
-    if (!(row < ntotal && row != selfrow)) continue;
-    const float key = x1_key<EL>(e[1], qsc, EL == FILTER_I8 ? xs[row] : 0.0f);
-    if (key < fminf(lk[KR - 1], cut)) list_insert<KR, int>(lk, li, key, row);
+  // the list's slots c = 0 .. cnt-1 at dslot[c * nl + i] (slot-major), eight
+  // at a time: their loads, then their rows' factors, then the admissions in
+  // dump order (independent loads in flight together instead of a chain)
+  const i32x2* sl = (const i32x2*)dslot + i;
+  constexpr int kB = 8;
+  for (int c0 = 0; c0 < cnt; c0 += kB) {
+    i32x2 e[kB];
+    float fx[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) e[j] = c0 + j < cnt ? sl[(int64_t)(c0 + j) * nl] : i32x2{-1, 0};
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      fx[j] = EL == FILTER_I8 && e[j][0] >= 0 && e[j][0] < ntotal ? xs[e[j][0]] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int row = e[j][0];
+      if (!(row >= 0 && row < ntotal && row != selfrow)) continue;
+      const float key = x1_key<EL>(e[j][1], qsc, fx[j]);
+      if (key < fminf(lk[KR - 1], cut)) list_insert<KR, int>(lk, li, key, row);
+    }
   }
 #pragma unroll
   for (int e = 0; e < KR; ++e) {
@@ -1098,6 +1199,18 @@ static int x1_qg() {
 }
 
 static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
+
+// Hybrid first launches (env VS_X1_HYB=0 turns them off, for A/B): for a
+// workgroup with at least kHybMinTiles tiles in the launch (its list part, a
+// quarter of them, then sees >= 4 tiles: 256 rows per lane list).
+constexpr int kHybMinTiles = 16;
+static bool x1_hybrid_on() {
+  static const bool v = [] {
+    const char* e = getenv("VS_X1_HYB");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
 
 // Database tiles per workgroup per launch for a pass of per_block tiles per
 // workgroup: 64, or 32 for a pass that can dump and has 128-192 tiles per
@@ -1137,20 +1250,35 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // 4 launches (C3: 20): cutting a short pass into more launches costs more
   // than it saves (C2 forced to 3 launches: 308k vs 394k queries/s,
   // profiles/r04a/r04d_sched_c2_cl_ab.txt).
-  const bool dumping = dump && nchunk >= 4;  // x1_pass_dumps
+  const bool cutting = dump && nchunk >= 4;  // x1_pass_dumps
+  // Hybrid first launch (gemm_topk_x1<..., HYB>): a quarter of its tiles as a
+  // list launch, the rest dumping below each list's own last entry; x1_replay
+  // right after it.  It needs no cut, so a pass of fewer launches (C2: one)
+  // dumps too, its later launches as dump launches below the lists' floors.
+  const int tiles0 = (per_block + nchunk - 1) / nchunk;
+  const bool hyb = dump && x1_hybrid_on() && tiles0 >= kHybMinTiles;
+  const bool later_dump = cutting || hyb;  // launches c > 0 are dump launches
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nchunk; ++c) {
     // the timed span of this launch alone (the cut and replay kernels between
-    // launches stay outside the spans)
-    if (a.timing) a.timing->begin(st, !dumping || c > 0);
-    if (dumping && c > 0) {
+    // launches stay outside the spans); the first launch of a pass whose later
+    // launches dump is timed apart ("<name>_list")
+    if (a.timing) a.timing->begin(st, !(later_dump && nchunk > 1) || c > 0);
+    if (later_dump && c > 0) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, true, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                            st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                            a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                            a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
                            a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
+    } else if (hyb) {
+      if constexpr (x1_has_dump(MODE, EL))
+        hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL, true>), dim3(nqt * a.nsplit),
+                           dim3(512), 0, st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH,
+                           a.qs, a.qaux, a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt,
+                           a.qtile0, a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key,
+                           part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
     } else {
       hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                          st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
@@ -1161,7 +1289,11 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     if (a.timing) a.timing->end(st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (dumping && c == 0) {
+    if (hyb && c == 0) {  // the hybrid launch's dumps, before the cuts read the lists
+      e = launch_x1_replay(a, part, st);
+      if (e != hipSuccess) return e;
+    }
+    if (cutting && c == 0) {
       e = launch_qcut(a, part, st);
       if (e != hipSuccess) return e;
     }
@@ -1173,7 +1305,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     // by ~8 of the next n) — the cut alone is too wide when 2B spans
     // thousands of rows (C3: ~5k, 63 % of the lists out of 32 slots in one
     // segment, profiles/r04b).
-    if (dumping && c > 0 && (((c + 1) & c) == 0 || c + 1 == nchunk)) {
+    if (later_dump && c > 0 && (((c + 1) & c) == 0 || c + 1 == nchunk)) {
       e = launch_x1_replay(a, part, st);
       if (e != hipSuccess) return e;
     }
@@ -1188,7 +1320,8 @@ bool x1_pass_dumps(int ntotal, int nsplit) {
   const int ntiles = (ntotal + kT - 1) / kT;
   const int per_block = (ntiles + nsplit - 1) / nsplit;
   const int ct = x1_chunk_tiles(per_block, true);
-  return (per_block + ct - 1) / ct >= 4;
+  const int nchunk = (per_block + ct - 1) / ct;
+  return nchunk >= 4 || (x1_hybrid_on() && (per_block + nchunk - 1) / nchunk >= kHybMinTiles);
 }
 
 hipError_t x1_stamps(unsigned long long* out, int reset) {
@@ -1242,14 +1375,15 @@ hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st) {
   if (part.KP < x1_lane_len()) return hipErrorInvalidValue;
   const int64_t n = (int64_t)a.nqa * part.P;
   const dim3 grid((unsigned)((n + 255) / 256));
+  const int64_t nl = (int64_t)a.nq_pad * part.P;  // lists of the pass (the slots' stride)
   if (a.filter == FILTER_I8)
     hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_I8>), grid, dim3(256), 0, st, a.dcount, a.dslot,
                        part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs, a.self0, a.ntotal,
-                       a.dR, a.qcut, stats);
+                       a.dR, nl, a.qcut, stats);
   else
     hipLaunchKernelGGL((x1_replay_kernel<8, FILTER_BF16>), grid, dim3(256), 0, st, a.dcount,
                        a.dslot, part.key, part.id, part.P, part.KP, a.nqa, a.qs, a.xs, a.self0,
-                       a.ntotal, a.dR, a.qcut, stats);
+                       a.ntotal, a.dR, nl, a.qcut, stats);
   return hipGetLastError();
 }
 

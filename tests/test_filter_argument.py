@@ -540,9 +540,9 @@ def test_dump_and_replay_leave_the_lists_of_in_kernel_admission():
     meets them, and x1_replay admits the stored rows in that order against
     min(list last, cut).  The lists equal those of admitting every row
     in-kernel against min(list last, cut), and a list whose dumped rows exceed
-    its R = 64 slots (x1_dump_slots) is reported (its query is then failed)."""
+    its R = 128 slots (x1_dump_slots) is reported (its query is then failed)."""
     rng = np.random.default_rng(11)
-    B, M, P, L, R = 1e-3, 19, 64, 8, 64
+    B, M, P, L, R = 1e-3, 19, 64, 8, 128
     for trial in range(30):
         n = 16 * 2048
         a = (rng.standard_normal(n) * 0.01).astype(np.float64)

@@ -10,8 +10,8 @@ split, launches of 8 tiles: one list launch + four dump launches in three
 segments), checked STRICTLY against the
 fp64 oracle on 512 sampled queries (every query tile), with the dump counters
 showing that dump launches ran.  Also: lane lists that run out of dump slots
-(90,000 ever-better copies of a row next to the queries: ~140 candidate rows
-per list and segment > 64 slots) hand their queries to the next stage and the answer stays exact;
+(150,000 ever-better copies of a row next to the queries: ~230 candidate rows
+per list and segment > 128 slots) hand their queries to the next stage and the answer stays exact;
 the bf16 plane's dump form; and the cosine self-join (C4's path), which keeps
 list launches."""
 
@@ -108,15 +108,15 @@ def test_dump_launches_clustered_unit_rows(lib):
 
 
 def test_dump_slot_overflow_hands_queries_on(lib):
-    """90,000 scaled copies of one row beside every query, each a little better
+    """150,000 scaled copies of one row beside every query, each a little better
     than every copy at a lower row: in a segment of dump launches a lane list
-    meets ~140 of them below its cut and its own last entry — more candidate
-    rows than its 64 dump slots.  The query is failed by the verification (cut =
+    meets ~230 of them below its cut and its own last entry — more candidate
+    rows than its 128 dump slots.  The query is failed by the verification (cut =
     -FLT_MAX) and answered by the next stage: exactly."""
     rng = np.random.default_rng(77)
     xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
     dup = rng.uniform(-1, 1, D_).astype(np.float32)
-    pos = np.sort(rng.choice(N, 90_000, replace=False))
+    pos = np.sort(rng.choice(N, 150_000, replace=False))
     xb[pos] = dup[None, :] * (1.0 + 1e-3 * pos[:, None] / N).astype(np.float32)
     xq = (dup[None, :] + 0.3 * rng.uniform(-1, 1, (B, D_))).astype(np.float32)
     dumps, over, fq, _ = _search_checked(lib, xb, xq, 10)
@@ -169,3 +169,18 @@ def test_cosine_selfjoin_keeps_list_launches(lib):
     Sr, Ir = flat.pgvector_cosine_topk(x, 15, q_rows=rows)
     bad = flat.selfjoin_mismatches(S[rows], I[rows], Sr, Ir, x, rows, strict=True)
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("metric", [IP, flat.METRIC_L2])
+def test_hybrid_single_launch(lib, metric, monkeypatch):
+    """A pass of one launch (C2's shape: 37 tiles per workgroup here) runs as a
+    hybrid launch (vs_gemm_x1.hip, HYB): its first quarter of tiles keeps lists
+    in registers, the rest dumps below each list's own last entry, and the
+    replay after it admits the dumps: exact on the sample, dumps made, no list
+    out of its slots, nothing left to a later stage."""
+    monkeypatch.setenv("VS_X1_CHUNK_TILES", "64")
+    rng = np.random.default_rng(57)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
+    dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v", metric=metric)
+    assert fq == B and dumps > 0 and over == 0 and ff == 0, (dumps, over, ff)
