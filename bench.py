@@ -809,6 +809,7 @@ def run_c5(args, ctx):
     xq = ctx.queries(max(B, args.recall_queries), d)
     nmut = max(1, N // 100)
     mut_time = 0.0
+    mut_rounds = []  # (remove ms, append ms) per mutation round
     # The workload's mutations are inputs: every removal list (labels of the
     # N-row index; each round removes and appends nmut, so the size stays N)
     # is drawn before the timed region, and the harness's record of which
@@ -826,11 +827,15 @@ def run_c5(args, ctx):
             t0 = time.perf_counter()
             rm = muts[len(done)]
             index.remove_ids(rm)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
             g0 = N + len(done) * nmut
             index.append_synthetic_ids(np.arange(g0, g0 + nmut, dtype=np.int64), seed=1234)
             done.append(rm)
             torch.cuda.synchronize()
-            mut_time += time.perf_counter() - t0
+            t2 = time.perf_counter()
+            mut_time += t2 - t0
+            mut_rounds.append((round((t1 - t0) * 1e3, 2), round((t2 - t1) * 1e3, 2)))
         j = (max(i, 0) * B) % (xq.shape[0] - B + 1)
         return index.search_device(xq[j:j + B], k, stream=ctx.stream)
 
@@ -894,6 +899,7 @@ def run_c5(args, ctx):
         res["recall_at_10_vs_fp32"] = recall
         res["recall_queries"] = args.recall_queries if recall is not None else 0
         res["mutation_seconds_in_timed_region"] = round(mt, 3)
+        res["mutation_rounds_remove_append_ms"] = mut_rounds
         res["cpu_baseline"] = None
         return res
     return None

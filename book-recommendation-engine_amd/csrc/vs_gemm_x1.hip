@@ -1200,16 +1200,17 @@ static int x1_qg() {
 
 static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
 
-// Hybrid first launches (env VS_X1_HYB=0 turns them off, for A/B): for a
-// workgroup with at least kHybMinTiles tiles in the launch (its list part, a
-// quarter of them, then sees >= 4 tiles: 256 rows per lane list).
+// Hybrid first launches (env VS_X1_HYB=1, read at every search; off by
+// default): for a workgroup with at least kHybMinTiles tiles in the launch (its
+// list part, a quarter of them, then sees >= 4 tiles: 256 rows per lane list).
+// Measured against list first launches on one box (profiles/r05j): C2 348.5k
+// vs 397.6k queries/s (the single launch's replay and dump stores cost more
+// than the list epilogue they replace), C3 76.4k vs 76.7k, clustered C3 equal:
+// kept as an exact, tested alternative, not the default.
 constexpr int kHybMinTiles = 16;
 static bool x1_hybrid_on() {
-  static const bool v = [] {
-    const char* e = getenv("VS_X1_HYB");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
+  const char* e = getenv("VS_X1_HYB");
+  return e && atoi(e) != 0;
 }
 
 // Database tiles per workgroup per launch for a pass of per_block tiles per

@@ -204,8 +204,9 @@ class IndexFlat(Index):
     @property
     def filter_planes(self):
         """The filter planes of this index, in the order the staged engine runs
-        them: ("i8", "bf16") for inner-product fp32 indexes, ("bf16",) for L2,
-        () for bf16 indexes (which search their stored values exactly)."""
+        them: ("i8", "bf16") for inner-product and L2 fp32 indexes (L2 as an
+        augmented inner product), ("bf16",) for cosine, () for bf16 indexes
+        (which search their stored values exactly)."""
         v = ctypes.c_int(0)
         _lib.check(self._lib.vs_filter_plane(self._h, ctypes.byref(v)), "vs_filter_plane")
         return tuple(n for bit, n in ((1, "i8"), (2, "bf16")) if v.value & bit)
