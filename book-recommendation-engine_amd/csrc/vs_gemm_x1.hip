@@ -253,10 +253,10 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const char* __restrict__ XH, const float* __restrict__ xs, const float* __restrict__ xaux,
     const char* __restrict__ QH, const float* __restrict__ qs, const float* __restrict__ qaux,
     int nqa, int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int64_t self0,
-    const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int nchunk, int KP,
-    int qg, float* __restrict__ pkey, int* __restrict__ pid, const float* __restrict__ xgmax,
-    const float* __restrict__ xgmin, const float* __restrict__ qcut, int* __restrict__ dcount,
-    int* __restrict__ dslot, int dR) {
+    const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int chunk_end,
+    int nchunk, int KP, int qg, float* __restrict__ pkey, int* __restrict__ pid,
+    const float* __restrict__ xgmax, const float* __restrict__ xgmin, const float* __restrict__ qcut,
+    int* __restrict__ dcount, int* __restrict__ dslot, int dR) {
   static_assert(!DUMP || x1_has_dump(MODE, EL), "dump form");
   static_assert(!HYB || (!DUMP && x1_has_dump(MODE, EL)), "hybrid launch");
   constexpr int NBUF = kNbuf;
@@ -297,7 +297,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   const int s0 = (int)((int64_t)sp * ntiles / nsplit);
   const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
   const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
-  const int t1 = s0 + (int)((int64_t)(s1 - s0) * (chunk + 1) / nchunk);
+  // parts [chunk, chunk_end) of the split's nchunk (a launch usually covers one)
+  const int t1 = s0 + (int)((int64_t)(s1 - s0) * chunk_end / nchunk);
   // Hybrid launch: the first quarter of the workgroup's tiles as a list
   // launch, the rest as a dump launch whose floor is each list's own last
   // entry after that quarter (a top-8 list over n rows is beaten by ~8 of every
@@ -1208,6 +1209,7 @@ static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
 // than the list epilogue they replace), C3 76.4k vs 76.7k, clustered C3 equal:
 // kept as an exact, tested alternative, not the default.
 constexpr int kHybMinTiles = 16;
+constexpr int kX1SplitDen = 0;  // split passes off by default (x1_split_den)
 static bool x1_hybrid_on() {
   const char* e = getenv("VS_X1_HYB");
   return e && atoi(e) != 0;
@@ -1230,6 +1232,19 @@ static int x1_chunk_tiles(int per_block, bool can_dump) {
                                                                         : kX1ChunkTiles;
 }
 
+// Split passes (env VS_X1_SPLIT=<den>, read at every search; 0 = off): a
+// dump-capable pass too short for 4 launches (C2: one launch of 61 tiles per
+// workgroup) runs as TWO launches, a list launch over the first 1/den of every
+// workgroup's tiles and one dump launch over the rest, with the cut between
+// them and one replay after: the dump launch's floor is min(cut, the list's
+// last entry), so it stores a few rows per list where a hybrid launch's
+// list-only floor stored ~24.
+static int x1_split_den() {
+  const char* e = getenv("VS_X1_SPLIT");
+  return e ? std::max(0, atoi(e)) : kX1SplitDen;
+}
+constexpr int kSplitMinTiles = 16;
+
 template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
   const int ntiles = (a.ntotal + kT - 1) / kT;
@@ -1247,45 +1262,53 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   int nchunk = a.qcount ? 1 : std::max(1, (per_block + chunk_tiles - 1) / chunk_tiles);
   // Dump launches after the first: its lists set the cuts (x1_qcut), the rest
   // of the pass stores only the blocks below them, and x1_replay folds the
-  // dumps into the lists between segments (below).  Only passes of at least
-  // 4 launches (C3: 20): cutting a short pass into more launches costs more
-  // than it saves (C2 forced to 3 launches: 308k vs 394k queries/s,
+  // dumps into the lists between segments (below).  Passes of at least 4
+  // launches (C3: 20) cut their launches as they are; a shorter one (C2) is
+  // a split pass when VS_X1_SPLIT allows it (above); otherwise list launches
+  // (C2 forced to 4 equal launches lost in round 4: 308k vs 394k queries/s,
   // profiles/r04a/r04d_sched_c2_cl_ab.txt).
-  const bool cutting = dump && nchunk >= 4;  // x1_pass_dumps
+  const int den = x1_split_den();
+  const bool split = dump && nchunk < 4 && den >= 2 && per_block >= kSplitMinTiles;
+  const bool cutting = dump && (nchunk >= 4 || split);  // x1_pass_dumps
   // Hybrid first launch (gemm_topk_x1<..., HYB>): a quarter of its tiles as a
   // list launch, the rest dumping below each list's own last entry; x1_replay
   // right after it.  It needs no cut, so a pass of fewer launches (C2: one)
   // dumps too, its later launches as dump launches below the lists' floors.
   const int tiles0 = (per_block + nchunk - 1) / nchunk;
-  const bool hyb = dump && x1_hybrid_on() && tiles0 >= kHybMinTiles;
+  const bool hyb = dump && !split && x1_hybrid_on() && tiles0 >= kHybMinTiles;
   const bool later_dump = cutting || hyb;  // launches c > 0 are dump launches
+  // the launches as part ranges [p0, p1) of nparts
+  const int nparts = split ? den : nchunk;
+  const int nlaunch = split ? 2 : nchunk;
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
-  for (int c = 0; c < nchunk; ++c) {
+  for (int c = 0; c < nlaunch; ++c) {
+    const int p0 = split ? (c == 0 ? 0 : 1) : c;
+    const int p1 = split ? (c == 0 ? 1 : den) : c + 1;
     // the timed span of this launch alone (the cut and replay kernels between
     // launches stay outside the spans); the first launch of a pass whose later
     // launches dump is timed apart ("<name>_list")
-    if (a.timing) a.timing->begin(st, !(later_dump && nchunk > 1) || c > 0);
+    if (a.timing) a.timing->begin(st, !(later_dump && nlaunch > 1) || c > 0);
     if (later_dump && c > 0) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, true, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                            st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                            a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
-                           a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
-                           a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
+                           a.self0, a.qrow, a.qcount, p0, p1, nparts, part.KP, qg, part.key,
+                           part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
     } else if (hyb) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL, true>), dim3(nqt * a.nsplit),
                            dim3(512), 0, st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH,
                            a.qs, a.qaux, a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt,
-                           a.qtile0, a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key,
-                           part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
+                           a.qtile0, a.self0, a.qrow, a.qcount, p0, p1, nparts, part.KP, qg,
+                           part.key, part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
     } else {
       hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                          st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                          a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
-                         a.self0, a.qrow, a.qcount, c, nchunk, part.KP, qg, part.key, part.id,
-                         a.xgmax, a.xgmin, nullptr, nullptr, nullptr, 0);
+                         a.self0, a.qrow, a.qcount, p0, p1, nparts, part.KP, qg, part.key,
+                         part.id, a.xgmax, a.xgmin, nullptr, nullptr, nullptr, 0);
     }
     if (a.timing) a.timing->end(st);
     hipError_t e = hipGetLastError();
@@ -1306,12 +1329,12 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     // by ~8 of the next n) — the cut alone is too wide when 2B spans
     // thousands of rows (C3: ~5k, 63 % of the lists out of 32 slots in one
     // segment, profiles/r04b).
-    if (later_dump && c > 0 && (((c + 1) & c) == 0 || c + 1 == nchunk)) {
+    if (later_dump && c > 0 && (((c + 1) & c) == 0 || c + 1 == nlaunch)) {
       e = launch_x1_replay(a, part, st);
       if (e != hipSuccess) return e;
     }
   }
-  if (ndispatch) *ndispatch = nchunk;
+  if (ndispatch) *ndispatch = nlaunch;
   return hipSuccess;
 }
 
@@ -1322,7 +1345,8 @@ bool x1_pass_dumps(int ntotal, int nsplit) {
   const int per_block = (ntiles + nsplit - 1) / nsplit;
   const int ct = x1_chunk_tiles(per_block, true);
   const int nchunk = (per_block + ct - 1) / ct;
-  return nchunk >= 4 || (x1_hybrid_on() && (per_block + nchunk - 1) / nchunk >= kHybMinTiles);
+  return nchunk >= 4 || (x1_split_den() >= 2 && per_block >= kSplitMinTiles) ||
+         (x1_hybrid_on() && (per_block + nchunk - 1) / nchunk >= kHybMinTiles);
 }
 
 hipError_t x1_stamps(unsigned long long* out, int reset) {

@@ -191,3 +191,19 @@ def test_hybrid_single_launch(lib, metric, monkeypatch):
     xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
     dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v", metric=metric)
     assert fq == B and dumps > 0 and over == 0 and ff == 0, (dumps, over, ff)
+
+
+@pytest.mark.parametrize("metric", [IP, flat.METRIC_L2])
+def test_split_pass(lib, metric, monkeypatch):
+    """A pass of one launch (C2's shape: 37 tiles per workgroup here) as a split
+    pass (VS_X1_SPLIT=4, vs_gemm_x1.hip x1_launch): a list launch over the first
+    quarter of every workgroup's tiles, the cuts, one dump launch over the rest
+    and one replay: exact on the sample, dumps made, no list out of its slots,
+    nothing left to a later stage."""
+    monkeypatch.setenv("VS_X1_CHUNK_TILES", "64")
+    monkeypatch.setenv("VS_X1_SPLIT", "4")
+    rng = np.random.default_rng(58)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
+    dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v", metric=metric)
+    assert fq == B and dumps > 0 and over == 0 and ff == 0, (dumps, over, ff)

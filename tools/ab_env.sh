@@ -16,6 +16,6 @@ for spec in "$@"; do
 import json,sys
 for l in sys.stdin:
     d=json.loads(l); r=d['roofline']; f=d.get('filter_verify') or {}
-    print('$name', round(d['value']), d['ms_per_step'], r['frac'], r['per_launch'][-45:], f.get('plane'), f.get('wide_checked'), f.get('fallback_queries', f.get('fallback_students')), (f.get('exact_check') or {}).get('rows_beyond_tie_tolerance'))"
+    print('$name', round(d['value']), d['ms_per_step'], r['frac'], r['per_launch'][-45:], f.get('plane'), f.get('wide_checked'), f.get('fallback_queries', f.get('fallback_students')), (f.get('exact_check') or {}).get('rows_beyond_tie_tolerance'), 'dump', (f.get('dump_launches') or {}).get('rows_dumped'), (f.get('dump_launches') or {}).get('lists_out_of_slots'), 'whole', (r.get('whole_pass') or {}).get('frac'))"
   [ $rc -eq 0 ] || { echo "$name rc=$rc: stop"; tail -5 "$OUT/$name.log"; exit $rc; }
 done
