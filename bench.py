@@ -477,9 +477,20 @@ def roofline(kind, work_total, kms, nl, unit_desc, kernel, traffic, traffic_src)
                           "dense int8 MFMA peak (2x bf16, MI355X_MICROARCH.md); candidates are "
                           "then rescored exactly in fp64 and a rigorous error bound proves the "
                           "exact top-k is among them")
+    if kind in HELD_CLOCK_CEILING:
+        c = HELD_CLOCK_CEILING[kind]
+        r["held_clock_ceiling"] = {
+            "value": c, "frac": round(achieved / c, 4),
+            "source": "tools/mfma_ceiling.hip: the same MFMAs at the filter kernel's occupancy "
+                      "with no loads (mean of 5 runs on one MI355X, profiles/r05k/mfma_ceiling.json)"}
     if traffic_src:
         r["traffic_source"] = traffic_src
     return r
+
+
+# The most the filter kernel's MFMA stream reaches on this chip at the clock it
+# holds under that load (TFLOP/s; nominal peaks above): int8 0.895, bf16 0.986.
+HELD_CLOCK_CEILING = {"mfma_x1_i8": 4473.7, "mfma_x1": 2464.2}
 
 
 def add_whole_pass(rf, split, scale):

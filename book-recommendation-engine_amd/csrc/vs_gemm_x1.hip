@@ -102,6 +102,12 @@ constexpr int kDumpMaxR = 128;
 #ifndef VS_X1_SCHED_I8
 #define VS_X1_SCHED_I8 0
 #endif
+// A/B builds only (tools/build_variant.sh -DVS_X1_SEGDMA=1): the segmented
+// schedule's four LDS-DMA pieces of step s+3 issued between the MFMAs of the
+// matrix segment (one per four MFMAs) instead of in the load segment.
+#ifndef VS_X1_SEGDMA
+#define VS_X1_SEGDMA 0
+#endif
 // A hybrid launch (mostly dump tiles) takes the dump launches' schedule.
 constexpr int x1_sched(int el, bool dump, bool hyb = false) {
   return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump || hyb ? 2 : 1;
@@ -1013,16 +1019,24 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       rd(buf, 0, fa0, fb0);
       rd(buf, 1, fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
+#if !VS_X1_SEGDMA
       stage_step();
       advance_cursor();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(0);
       // this wave's pieces of step s+1 (the younger steps stay in flight)
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#else
+      VS_X1_MARK(0);
+      // this wave's pieces of step s+1; step s+2's (issued in the previous
+      // matrix segment) stay in flight
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#endif
       VS_X1_MARK(1);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(2);
+#if !VS_X1_SEGDMA
       if constexpr (first) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) mfma_rb_first(rb, fa0, fb0);
@@ -1032,6 +1046,59 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       }
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, fb1);
+#else
+      {
+        // step s+3's pieces into the image of step s-2 (read two barriers ago
+        // by every wave, as in the load segment's placement), one per four MFMAs
+        const uint32_t lx = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)lbuf * (2 * kStepB) +
+                                                           (uint32_t)(2 * w) * 1024u);
+        auto piece = [&](int j, uint32_t m0v, uint32_t voff, const char* sbase) {
+          if constexpr (!kSeg) {  // the bf16 L2 / cosine kernels: no step pointers
+            stage_piece(j);
+            return;
+          }
+          uint32_t keep;
+          asm volatile(
+              "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+              "global_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+              : "=&s"(keep)
+              : "s"(m0v), "v"(voff), "s"(sbase)
+              : "memory");
+        };
+        static_assert(kStepB == 0x4000, "piece offsets");
+        if constexpr (first) {
+          mfma_rb_first(0, fa0, fb0);
+          mfma_rb_first(1, fa0, fb0);
+        } else {
+          mfma_rb(0, fa0, fb0);
+          mfma_rb(1, fa0, fb0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        piece(0, lx, xl0, xstep);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (first) {
+          mfma_rb_first(2, fa0, fb0);
+          mfma_rb_first(3, fa0, fb0);
+        } else {
+          mfma_rb(2, fa0, fb0);
+          mfma_rb(3, fa0, fb0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        piece(1, lx + 0x4000u, soff, qstep);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_rb(0, fa1, fb1);
+        mfma_rb(1, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        piece(2, lx + 0x400u, xl2, xstep);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_rb(2, fa1, fb1);
+        mfma_rb(3, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        piece(3, lx + 0x4400u, soff + 1024u, qstep);
+        __builtin_amdgcn_sched_barrier(0);
+        advance_cursor();
+      }
+#endif
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(3);
       __builtin_amdgcn_s_barrier();
@@ -1209,7 +1276,10 @@ static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
 // than the list epilogue they replace), C3 76.4k vs 76.7k, clustered C3 equal:
 // kept as an exact, tested alternative, not the default.
 constexpr int kHybMinTiles = 16;
-constexpr int kX1SplitDen = 0;  // split passes off by default (x1_split_den)
+// split passes: a list launch over the first 1/8 of every workgroup's tiles
+// (x1_split_den; C2 on one box, profiles/r05m: 426k queries/s at 1/8, 416k at
+// 1/4, 410k as one list launch)
+constexpr int kX1SplitDen = 8;
 static bool x1_hybrid_on() {
   const char* e = getenv("VS_X1_HYB");
   return e && atoi(e) != 0;
@@ -1232,7 +1302,8 @@ static int x1_chunk_tiles(int per_block, bool can_dump) {
                                                                         : kX1ChunkTiles;
 }
 
-// Split passes (env VS_X1_SPLIT=<den>, read at every search; 0 = off): a
+// Split passes (env VS_X1_SPLIT=<den>, read at every search; 0 = off;
+// default kX1SplitDen): a
 // dump-capable pass too short for 4 launches (C2: one launch of 61 tiles per
 // workgroup) runs as TWO launches, a list launch over the first 1/den of every
 // workgroup's tiles and one dump launch over the rest, with the cut between
@@ -2745,42 +2816,51 @@ hipError_t launch_select_lists(Partials part, int L, int nq, int KF, float* Dk, 
   return hipGetLastError();
 }
 
-// One wave per query: a_M = the M-th smallest key over the query's P lists of
-// L entries (bitwise search on the order-preserving integer image), then the
-// cut.  Fewer than M entries: no cut yet.
-__global__ __launch_bounds__(64) void qcut_kernel(const float* __restrict__ lkey,
-                                                  const int* __restrict__ lid, int P, int LKP, int L,
-                                                  int M, const double* __restrict__ bkey, int nq,
-                                                  float* __restrict__ cut) {
+// One workgroup of 256 threads per query: a_M = the M-th smallest key over
+// the query's P lists of L entries (bitwise search on the order-preserving
+// integer image), then the cut.  Fewer than M entries: no cut yet.  Up to 4,096
+// entries stay in registers (C2: 256 lists x 8; one wave re-reading 2,048
+// entries from memory per count cost ~0.8 ms per search, profiles/r05l), more
+// are read again per count.
+constexpr int kQcutThreads = 256;
+__global__ __launch_bounds__(kQcutThreads) void qcut_kernel(
+    const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L, int M,
+    const double* __restrict__ bkey, int nq, float* __restrict__ cut) {
   const int q = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (q >= nq) return;
+  const int tid = threadIdx.x;
+  if (q >= nq) return;  // uniform over the workgroup
   const int64_t base = (int64_t)q * P * LKP;
   const int n = P * L;
-  // order images (uint64; empty entries 2^32, never counted); up to 1024
-  // entries stay in registers, more are read again per count
+  // order images (uint64; empty entries 2^32, never counted)
   constexpr int kR = 16;
   uint64_t v[kR];
-  const bool regs = n <= 64 * kR;  // uniform
+  const bool regs = n <= kQcutThreads * kR;  // uniform
   auto image = [&](int j) -> uint64_t {
     const int64_t o = base + (int64_t)(j / L) * LKP + j % L;
     return lid[o] >= 0 ? (uint64_t)key_order(lkey[o]) : (1ull << 32);
   };
 #pragma unroll
   for (int i = 0; i < kR; ++i) {
-    const int j = lane + 64 * i;
+    const int j = tid + kQcutThreads * i;
     v[i] = regs && j < n ? image(j) : (1ull << 32);
   }
-  auto count_below = [&](uint64_t y) {  // entries with order image < y
+  __shared__ int part[kQcutThreads / 64];
+  auto count_below = [&](uint64_t y) {  // entries with order image < y (uniform result)
     int c = 0;
     if (regs) {
 #pragma unroll
       for (int i = 0; i < kR; ++i) c += v[i] < y ? 1 : 0;
     } else {
-      for (int j = lane; j < n; j += 64) c += image(j) < y ? 1 : 0;
+      for (int j = tid; j < n; j += kQcutThreads) c += image(j) < y ? 1 : 0;
     }
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    return c;
+    __syncthreads();  // the previous count's reads of part[] are done
+    if ((tid & 63) == 0) part[tid >> 6] = c;
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < kQcutThreads / 64; ++w) t += part[w];
+    return t;
   };
   if (count_below(1ull << 32) < M) return;  // uniform
   // the largest x with fewer than M entries below it: the M-th smallest image
@@ -2789,7 +2869,7 @@ __global__ __launch_bounds__(64) void qcut_kernel(const float* __restrict__ lkey
     if (count_below(x + (1ull << b)) < M) x += 1ull << b;
   const float aM = key_unorder((uint32_t)x);
   const double tp = (double)aM + 2.000001 * bkey[q];
-  if (lane == 0 && isfinite(tp) && tp < (double)FLT_MAX) {
+  if (tid == 0 && isfinite(tp) && tp < (double)FLT_MAX) {
     float t = (float)tp;
     if ((double)t < tp) t = nextafterf(t, INFINITY);
     if (t < cut[q]) cut[q] = t;
@@ -2818,7 +2898,7 @@ hipError_t launch_qbound(int mode, const float* Q, int64_t ld, const float* qn, 
 
 static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st) {
   const int nq = a.nqa;
-  hipLaunchKernelGGL(qcut_kernel, dim3(nq), dim3(64), 0, st, part.key, part.id, part.P, part.KP,
+  hipLaunchKernelGGL(qcut_kernel, dim3(nq), dim3(kQcutThreads), 0, st, part.key, part.id, part.P, part.KP,
                      x1_lane_len(), a.qcut_m, a.qbkey, nq, a.qcut);
   return hipGetLastError();
 }

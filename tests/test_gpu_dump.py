@@ -186,6 +186,7 @@ def test_hybrid_single_launch(lib, metric, monkeypatch):
     out of its slots, nothing left to a later stage."""
     monkeypatch.setenv("VS_X1_CHUNK_TILES", "64")
     monkeypatch.setenv("VS_X1_HYB", "1")  # off by default (vs_gemm_x1.hip, x1_hybrid_on)
+    monkeypatch.setenv("VS_X1_SPLIT", "0")  # a split pass would take the pass instead
     rng = np.random.default_rng(57)
     xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
     xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
