@@ -123,7 +123,16 @@ constexpr int x1_sched(int el, bool dump, bool hyb = false) {
 // dump (built, exact) made C4 slower: 439k vs 467k students/s at 4-5
 // launches per pass (profiles/r04w/ab_c4_cosine_dump.txt).  The bf16 L2 /
 // cosine keys also need the row norms in the kernel.
-constexpr bool x1_has_dump(int mode, int el) { return mode == MODE_IP; }
+constexpr bool x1_has_dump(int mode, int el) {
+  return mode == MODE_IP || (mode == MODE_COS && el == FILTER_I8);
+}
+// The int8 cosine's dump form (its folded factors s_x / |x| take the place of
+// s_x; key and bound as in its list launches) is used only with VS_X1_COSDUMP=1
+// (A/B; read at every search).
+static bool x1_cos_dump_on() {
+  const char* e = getenv("VS_X1_COSDUMP");
+  return e && atoi(e) != 0;
+}
 
 __device__ __forceinline__ unsigned long long stamp_now() {
   unsigned long long t;
@@ -1461,7 +1470,9 @@ hipError_t launch_gemm_topk_x1(int mode, const X1Args& a, Partials part, hipStre
   return x1_dispatch<FILTER_BF16>(mode, a, part, st, ndispatch);
 }
 
-bool x1_dump_applies(int mode, int filter) { return x1_has_dump(mode, filter); }
+bool x1_dump_applies(int mode, int filter) {
+  return x1_has_dump(mode, filter) && (mode != MODE_COS || x1_cos_dump_on());
+}
 
 // The replay of launch_gemm_topk_x1's dumps (a no-op when the pass had none to
 // make: the counts stay zero).

@@ -208,3 +208,26 @@ def test_split_pass(lib, metric, monkeypatch):
     xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
     dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v", metric=metric)
     assert fq == B and dumps > 0 and over == 0 and ff == 0, (dumps, over, ff)
+
+
+def test_cosine_selfjoin_dump_form(lib, monkeypatch):
+    """The int8 cosine's dump form (VS_X1_COSDUMP=1: the folded factors s_x / |x|
+    in the launch-wide threshold, the same keys as its list launches) on the
+    C4-shaped self-join above: exact on the sampled students, dump launches ran."""
+    from vsearch import faiss as vfaiss
+
+    monkeypatch.setenv("VS_X1_COSDUMP", "1")
+    rng = np.random.default_rng(14)
+    x = rng.standard_normal((N, D_)).astype(np.float32)
+    index = vfaiss.IndexFlatIP(D_)
+    index.add(x)
+    lib.filter_stats(reset=True)
+    S, I = index.selfjoin(15)
+    dumps, over = lib.filter_dump_stats()
+    lib.filter_stats(reset=True)
+    assert dumps > 0
+    rows = np.array(sorted({r for c in range(0, N, 65536) for r in (c, c + 1, c + 65535)
+                            if r < N} | set(range(0, N, N // 200))))
+    Sr, Ir = flat.pgvector_cosine_topk(x, 15, q_rows=rows)
+    bad = flat.selfjoin_mismatches(S[rows], I[rows], Sr, Ir, x, rows, strict=True)
+    assert not bad, bad[:5]
