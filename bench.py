@@ -641,6 +641,9 @@ def run_knn(args, ctx):
             ctx.lib.filter_stats(reset=True)
             tw, kmw, nw, (Dw, Iw) = ctx.timed(
                 lambda i: index.search_device(qw, kw, stream=ctx.stream), args.wide_k_steps, 1)
+            ww = ctx.lib.filter_wide_stats()
+            w2 = ctx.lib.filter_second_stats()
+            wwe, wwr = ctx.lib.filter_wide_sets()
             wq, wf = ctx.lib.filter_stats(reset=True)
             Iwh = Iw.cpu().numpy()
             wide.append({"k": kw, "batch": bw, "steps": args.wide_k_steps,
@@ -648,7 +651,10 @@ def run_knn(args, ctx):
                          "queries_per_s": round(args.wide_k_steps * bw / tw, 1),
                          "kernel": ctx.lib.timer_kernel(),
                          "kernel_ms_per_dispatch": round(kmw / max(1, nw), 3),
-                         "filter_queries": wq, "exact_redo_queries": wf,
+                         "filter_queries": wq, "wide_checked": ww,
+                         "wide_set_mean": round(wwe / ww, 1) if ww else 0.0,
+                         "wide_rescored_mean": round(wwr / ww, 1) if ww else 0.0,
+                         "to_bf16_stage": w2, "exact_redo_queries": wf,
                          "result_sane": bool((Iwh >= 0).all() and (Iwh < args.ntotal).all())})
 
     if ctx.rank == 0:
