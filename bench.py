@@ -110,10 +110,20 @@ def rocprof_prefix(kname: str):
     lookup takes the instantiation with the most dispatches (the dump launches
     where a pass has them)."""
     if kname == "gemm_topk_x1_i8":
-        return "void vs::gemm_topk_x1<", ", 1>("
+        return "void vs::gemm_topk_x1<", "el=1"
     if kname == "gemm_topk_x1":
-        return "void vs::gemm_topk_x1<", ", 0>("
+        return "void vs::gemm_topk_x1<", "el=0"
     return "void vs::" + kname + "<", ""
+
+
+def kernel_matches(name: str, must: str) -> bool:
+    """`must` is a substring of the rocprof name, or "el=<plane>": the x1
+    kernel's fourth template argument (gemm_topk_x1<KR, MODE, DUMP, EL[, HYB]>)."""
+    if not must.startswith("el="):
+        return must in name
+    i, j = name.find("<"), name.find(">(")
+    args = [a.strip() for a in name[i + 1:j].split(",")] if 0 <= i < j else []
+    return len(args) >= 4 and args[3] == must[3:]
 
 DEFAULTS = {
     "c3": dict(ntotal=10_000_000, batch=4096, k=10, metric="ip", dtype="f32"),
@@ -177,14 +187,19 @@ def pmc_traffic(workload: str, kernel_prefix: str, must_contain: str = ""):
             summ = json.load(f)
         best = None
         for name, rec in summ.get("kernels", {}).items():
-            if not (name.startswith(kernel_prefix) and must_contain in name):
+            if not (name.startswith(kernel_prefix) and kernel_matches(name, must_contain)):
                 continue
             groups = rec.get("by_grid") or {"?": rec}
+            dump = kernel_matches(name, "el=1") or kernel_matches(name, "el=0")
+            dump = dump and ", true, " in name.split("(")[0]  # DUMP = the third argument
             for grid, g in groups.items():
-                if best is None or g["dispatches"] > best[0]:
-                    best = (g["dispatches"], g["hbm_bytes_per_launch"], name, grid)
+                # the most dispatches; a dump launch over a list launch on a tie
+                # (a split pass: one of each per search)
+                key = (g["dispatches"], dump)
+                if best is None or key > best[0]:
+                    best = (key, g["hbm_bytes_per_launch"], name, grid)
         if best is not None:
-            n, hbm, name, grid = best
+            (n, _), hbm, name, grid = best
             return hbm, (f"{os.path.relpath(path, ROOT)}: {name.split('(')[0]} grid {grid}, "
                          f"{n} dispatches")
     return None, None

@@ -858,8 +858,15 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   // behind the top-M, which the bound needs on clustered data and on the int8
   // plane (profiles/r02l_ab_split.txt; one workgroup per CU left 0.7 % of the
   // C3 queries to the exact engine on int8)
-  x.nsplit = (int)std::max<int64_t>(std::min<int64_t>(ntiles, 4 * ((KF + L - 1) / L)),
-                                    std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
+  // Inner product past k = 32 (M = 2k - 1 of 59 .. 127, KF = 64 / 128) takes
+  // twice as many lists again: at C3 (B = 4096) k = 30 left 13 queries per
+  // search and k = 60 815 to the deep bf16 stage (a 10M-row pass of ~20-30 ms
+  // however few they are); with 8 KF / L lists 0 and 26 (60.5 vs 78.9 and 85.9
+  // vs 94.2 ms per search, profiles/r05q, VS_X1_SPLIT_MULT=2)
+  const int lists_per_cand = mode == MODE_IP && KF >= 64 ? 8 : 4;
+  x.nsplit = (int)std::max<int64_t>(
+      std::min<int64_t>(ntiles, lists_per_cand * ((KF + L - 1) / L)),
+      std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
   // the deep stage (a gathered batch of the few queries an earlier stage could
   // not settle): as many lists as two workgroups per CU give ONE query tile, so
   // the floors sit far behind the top (the a_M + 2B threshold keeps the wide

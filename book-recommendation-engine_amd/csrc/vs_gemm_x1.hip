@@ -294,7 +294,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   {
     const int nblk = gridDim.x;
     const int b = blockIdx.x;
-    const int QG = nqt < qg ? nqt : qg;
+    const int qga = qg < 0 ? -qg : qg;  // qg < 0: no rounds of groups (A/B)
+    const int QG = nqt < qga ? nqt : qga;
     const int G = nqt / QG;
     const int S = nblk >> 3;
     if ((nblk & 7) == 0 && nqt * nsplit == nblk && nqt % QG == 0 && G <= 8 && 8 % G == 0 &&
@@ -302,6 +303,16 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       const int xcd = b & 7, slot = b >> 3, DG = S / QG;
       qt = (xcd % G) * QG + slot % QG;
       sp = (xcd / G) * DG + slot / QG;
+    } else if (qg > 0 && (nblk & 7) == 0 && nqt * nsplit == nblk && nqt % QG == 0 && G % 8 == 0) {
+      // more query-tile groups than XCDs (C4's 65,536-student chunks: 256 query
+      // tiles): XCD x takes groups x, x + 8, ... one after another, each as QG
+      // query tiles x every split in slot order, so the workgroups an XCD runs
+      // together share their database tiles and their QG query tiles in its L2
+      // (a plain dealing put 32 different query tiles on an XCD at once)
+      const int xcd = b & 7, slot = b >> 3, per = QG * nsplit;
+      const int gi = slot / per, rem = slot - gi * per;
+      qt = (gi * 8 + xcd) * QG + rem % QG;
+      sp = rem / QG;
     } else {
       const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
       const int lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
@@ -1279,6 +1290,13 @@ static int x1_qg() {
 
 static hipError_t launch_qcut(const X1Args& a, Partials part, hipStream_t st);
 
+// XCD rounds of query-tile groups for grids of more than 8 groups (env
+// VS_X1_XCDG=0 turns them off, for A/B; read at every search)
+static bool x1_group_rounds() {
+  const char* e = getenv("VS_X1_XCDG");
+  return !e || atoi(e) != 0;
+}
+
 // Hybrid first launches (env VS_X1_HYB=1, read at every search; off by
 // default): for a workgroup with at least kHybMinTiles tiles in the launch (its
 // list part, a quarter of them, then sees >= 4 tiles: 256 rows per lane list).
@@ -1336,7 +1354,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // every XCD takes every query tile there (QG = nqt), so the working
   // workgroups of tile 0 spread over all XCDs instead of the 2 of 8 that QG = 4
   // gives it (clustered C3: 202 -> 151 ms per step, profiles/r02za).
-  const int qg = a.qcount ? nqt : x1_qg();
+  const int qg = a.qcount ? nqt : x1_qg() * (x1_group_rounds() ? 1 : -1);
   const bool dump = a.dump && x1_has_dump(MODE, EL) && !a.qcount && a.qcut && a.qbkey &&
                     a.qcut_m > 0 && a.dcount && a.dslot && a.dR > 0;
   const int chunk_tiles = x1_chunk_tiles(per_block, dump);
