@@ -78,16 +78,19 @@ def x1_dominant(ctx, work_total, kms, nl):
     the timed kernel time: (timer name, its share of the algorithmic work, its
     kernel ms, its dispatches, per-plane record).  A pass whose later launches
     are dump launches times its first (list) launch apart ("<name>_list"): the
-    roofline is the dump kernel's own time.  Every launch of a pass covers the
-    same share of the database tiles (even chunks), so the work per dispatch
-    is the same for all of them."""
-    mi, ni = ctx.lib.timer_read_kernel("gemm_topk_x1_i8")
-    mil, nil = ctx.lib.timer_read_kernel("gemm_topk_x1_i8_list")
+    roofline is the dump kernel's own time.  Each span's work is the share of
+    its pass's database tiles the library recorded for it (a list launch
+    covers less than a dump launch)."""
+    mi, ni, si = ctx.lib.timer_read_kernel_share("gemm_topk_x1_i8")
+    mil, nil, sil = ctx.lib.timer_read_kernel_share("gemm_topk_x1_i8_list")
     mip, _ = ctx.lib.timer_read_kernel("gemm_topk_x1_i8_pass")
-    mb, nb = ctx.lib.timer_read_kernel("gemm_topk_x1")
-    mbl, nbl = ctx.lib.timer_read_kernel("gemm_topk_x1_list")
+    mb, nb, sb = ctx.lib.timer_read_kernel_share("gemm_topk_x1")
+    mbl, nbl, sbl = ctx.lib.timer_read_kernel_share("gemm_topk_x1_list")
     mbp, _ = ctx.lib.timer_read_kernel("gemm_topk_x1_pass")
-    per = work_total / max(1, ni + nil + nb + nbl)
+    # launches of a pass cover unequal parts of it (the list launch a quarter
+    # chunk, or 1/8 of a split pass): work in proportion to the tiles each
+    # span covered (the library's per-span shares, in passes)
+    per = work_total / max(1e-12, si + sil + sb + sbl)
     split = {"i8": {"dispatches": ni, "kernel_ms": round(mi, 3)},
              "i8_list_launches": {"dispatches": nil, "kernel_ms": round(mil, 3)},
              "i8_whole_passes": {"kernel_ms": round(mip, 3)},
@@ -98,10 +101,10 @@ def x1_dominant(ctx, work_total, kms, nl):
     # cut and replay kernels between them (one span per pass), over the work
     # of all its launches
     if mi + mil >= mb + mbl:
-        split["whole_pass"] = (per * (ni + nil), mip)
-        return "gemm_topk_x1_i8", per * ni, mi, ni, split
-    split["whole_pass"] = (per * (nb + nbl), mbp)
-    return "gemm_topk_x1", per * nb, mb, nb, split
+        split["whole_pass"] = (per * (si + sil), mip)
+        return "gemm_topk_x1_i8", per * si, mi, ni, split
+    split["whole_pass"] = (per * (sb + sbl), mbp)
+    return "gemm_topk_x1", per * sb, mb, nb, split
 
 
 def rocprof_prefix(kname: str):

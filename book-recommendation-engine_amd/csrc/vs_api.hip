@@ -381,7 +381,8 @@ struct TimedSpan {
   hipEvent_t a, b;
   int dispatches;
   const char* name;
-  bool aux;  // an extra span over other spans' kernels: not in the unnamed total
+  bool aux;      // an extra span over other spans' kernels: not in the unnamed total
+  double share;  // the span's share of its pass's database tiles (filter passes)
 };
 std::vector<TimedSpan> g_timer_events;
 const char* g_timer_kernel = "";
@@ -423,6 +424,7 @@ struct KernelTimer {
   const char* name = nullptr;
   int dispatches = 1;  // kernel launches between the two events
   bool aux = false;
+  double share = 1.0;  // of a filter pass's tiles (X1SpanTimer)
   // name == nullptr: untimed (the filter engine's exact redo, which is not the
   // kernel the roofline is quoted on)
   // names_kernel: this span names the search's dominant kernel (vs_timer_kernel);
@@ -443,7 +445,7 @@ struct KernelTimer {
     if (!a) return;
     (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> g(g_timer_mu);
-    g_timer_events.push_back({a, b, dispatches, name, aux});
+    g_timer_events.push_back({a, b, dispatches, name, aux, share});
     a = b = nullptr;
   }
 };
@@ -458,8 +460,9 @@ struct X1SpanTimer : X1Timing {
   const char* list_name;
   KernelTimer* cur = nullptr;
   X1SpanTimer(const char* n, const char* ln) : name(n), list_name(ln) {}
-  void begin(hipStream_t st, bool dominant) override {
+  void begin(hipStream_t st, bool dominant, double share) override {
     cur = new KernelTimer(st, dominant ? name : list_name);
+    cur->share = share;
   }
   void end(hipStream_t) override {
     if (!cur) return;
@@ -2311,10 +2314,11 @@ int vs_timer_read(double* total_ms, int64_t* launches) {
   return vs_timer_read_kernel(nullptr, total_ms, launches);
 }
 
-int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches) {
+int vs_timer_read_kernel_share(const char* kernel, double* total_ms, int64_t* launches,
+                               double* share) {
   if (!total_ms || !launches) return fail(VS_E_INVALID, "vs_timer_read: null output");
   std::lock_guard<std::mutex> g(g_timer_mu);
-  double tot = 0.0;
+  double tot = 0.0, sh = 0.0;
   int64_t n = 0;
   for (auto& p : g_timer_events) {
     if (kernel ? strcmp(kernel, p.name) != 0 : p.aux) continue;
@@ -2323,10 +2327,16 @@ int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches
     VS_HIP(hipEventElapsedTime(&ms, p.a, p.b), "vs_timer_read: elapsed");
     tot += ms;
     n += p.dispatches;
+    sh += p.share;
   }
   *total_ms = tot;
   *launches = n;
+  if (share) *share = sh;
   return VS_OK;
+}
+
+int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches) {
+  return vs_timer_read_kernel_share(kernel, total_ms, launches, nullptr);
 }
 
 }  // extern "C"

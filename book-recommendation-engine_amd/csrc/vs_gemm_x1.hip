@@ -1344,6 +1344,10 @@ static int x1_split_den() {
   return e ? std::max(0, atoi(e)) : kX1SplitDen;
 }
 constexpr int kSplitMinTiles = 16;
+static bool x1_quarter_on() {
+  const char* e = getenv("VS_X1_QUARTER");
+  return !e || atoi(e) != 0;
+}
 
 template <int KR, int MODE, int EL>
 static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int* ndispatch) {
@@ -1378,17 +1382,26 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   const bool hyb = dump && !split && x1_hybrid_on() && tiles0 >= kHybMinTiles;
   const bool later_dump = cutting || hyb;  // launches c > 0 are dump launches
   // the launches as part ranges [p0, p1) of nparts
-  const int nparts = split ? den : nchunk;
-  const int nlaunch = split ? 2 : nchunk;
+  // A cutting pass of nchunk launches lists only its first quarter launch:
+  // the list launch over parts [0, 1) of 4 nchunk, a dump launch over [1, 4),
+  // then one launch per chunk (the list launch runs at ~2/3 of a dump launch's
+  // rate: the more of the pass it covers, the more it costs — a k = 60 pass of
+  // 5 chunks spent 15 of its 58 ms in it, profiles/r05t).  Env
+  // VS_X1_QUARTER=0: the first chunk whole (A/B).
+  const bool quarter = cutting && !split && nchunk >= 4 && x1_quarter_on() &&
+                       per_block / (4 * nchunk) >= 2;
+  const int nparts = split ? den : quarter ? 4 * nchunk : nchunk;
+  const int nlaunch = split ? 2 : quarter ? nchunk + 1 : nchunk;
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nlaunch; ++c) {
-    const int p0 = split ? (c == 0 ? 0 : 1) : c;
-    const int p1 = split ? (c == 0 ? 1 : den) : c + 1;
+    const int p0 = split ? (c == 0 ? 0 : 1) : quarter ? (c == 0 ? 0 : c == 1 ? 1 : 4 * (c - 1)) : c;
+    const int p1 = split ? (c == 0 ? 1 : den) : quarter ? (c == 0 ? 1 : 4 * c) : c + 1;
     // the timed span of this launch alone (the cut and replay kernels between
     // launches stay outside the spans); the first launch of a pass whose later
     // launches dump is timed apart ("<name>_list")
-    if (a.timing) a.timing->begin(st, !(later_dump && nlaunch > 1) || c > 0);
+    if (a.timing)
+      a.timing->begin(st, !(later_dump && nlaunch > 1) || c > 0, (double)(p1 - p0) / nparts);
     if (later_dump && c > 0) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, true, EL>), dim3(nqt * a.nsplit), dim3(512), 0,

@@ -100,7 +100,8 @@ __host__ __device__ inline int64_t plane_offset(int64_t row, int64_t byte, int64
 // every pass launch with begin/end; `dominant` is false for the list launch of
 // a pass that dumps (its spans are named apart from the dump launches').
 struct X1Timing {
-  virtual void begin(hipStream_t st, bool dominant) = 0;
+  // share: the launch's part of the pass's database tiles
+  virtual void begin(hipStream_t st, bool dominant, double share) = 0;
   virtual void end(hipStream_t st) = 0;
   virtual ~X1Timing() = default;
 };

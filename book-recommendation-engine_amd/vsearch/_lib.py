@@ -75,6 +75,8 @@ SIGNATURES = {
     "vs_timer_read": (_c_int, [ctypes.POINTER(ctypes.c_double), _i64p]),
     "vs_timer_kernel": (ctypes.c_char_p, []),
     "vs_timer_read_kernel": (_c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _i64p]),
+    "vs_timer_read_kernel_share": (_c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                            _i64p, ctypes.POINTER(ctypes.c_double)]),
     "vs_x1_stamps": (_c_int, [ctypes.POINTER(ctypes.c_ulonglong), _c_int]),
     "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
     "vs_filter_wide_stats": (_c_int, [_i64p]),
@@ -190,6 +192,17 @@ def timer_read_kernel(name: str):
     n = ctypes.c_int64(0)
     check(load().vs_timer_read_kernel(name.encode(), ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+def timer_read_kernel_share(name: str):
+    """(summed kernel ms, launches, summed share of their passes' tiles) of the
+    timed spans named `name`."""
+    ms = ctypes.c_double(0.0)
+    n = ctypes.c_int64(0)
+    sh = ctypes.c_double(0.0)
+    check(load().vs_timer_read_kernel_share(name.encode(), ctypes.byref(ms), ctypes.byref(n),
+                                            ctypes.byref(sh)))
+    return ms.value, n.value, sh.value
 
 
 def filter_stats(reset: bool = False):

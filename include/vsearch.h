@@ -243,6 +243,11 @@ int vs_timer_read(double* total_ms, int64_t* launches);
  * the cut and replay kernels "<name>_pass", a span that vs_timer_read's total
  * leaves out because its kernels are in the other spans). */
 int vs_timer_read_kernel(const char* kernel, double* total_ms, int64_t* launches);
+/* The same, plus the summed share of their passes' database tiles that those
+ * spans covered (a filter pass's launches cover unequal parts: its list
+ * launch a quarter chunk or 1/8 of a split pass; bench.py's roofline work). */
+int vs_timer_read_kernel_share(const char* kernel, double* total_ms, int64_t* launches,
+                               double* share);
 /* Name of the fused search kernel the last search launched ("gemm_topk_x1",
  * "gemm_topk", "skinny_topk" or "gemv_topk"). */
 const char* vs_timer_kernel(void);
