@@ -840,6 +840,13 @@ static bool dump_enabled() {
   return v;
 }
 
+// The deep stage's small-count kernel (env VS_SKINNY_DEEP=0 turns it off,
+// for A/B; read at every search).
+bool skinny_deep_on() {
+  const char* e = getenv("VS_SKINNY_DEEP");
+  return !e || atoi(e) != 0;
+}
+
 int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
                       int plane, bool last_plane, bool deep = false, const int* gl = nullptr,
                       const int* gc = nullptr) {
@@ -1045,6 +1052,13 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     X1SpanTimer tm(i8 ? "gemm_topk_x1_i8" : "gemm_topk_x1",
                    i8 ? "gemm_topk_x1_i8_list" : "gemm_topk_x1_list");
     if (!gathered) x.timing = &tm;
+    // the deep bf16 stage of a few queries (inner product / augmented L2, not
+    // a self-join): skinny_plane_topk streams the plane once for them and
+    // the x1 pass exits, or the reverse, by the device-side count
+    if (gathered && deep && !i8 && kmode == MODE_IP && a.self0 < 0 && skinny_deep_on()) {
+      VS_HIP(launch_skinny_plane(x.XH, x.QH, x.ld, ntotal, gc, part, st), "vs: skinny deep stage");
+      x.qskip = skinny_plane_max_queries();
+    }
     int nd = 0;
     VS_HIP(launch_gemm_topk_x1(kmode, x, part, st, &nd), "vs: gemm_topk_x1 launch");
     x.timing = nullptr;

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     const int* __restrict__ qrow, const int* __restrict__ qcount, int chunk, int chunk_end,
     int nchunk, int KP, int qg, float* __restrict__ pkey, int* __restrict__ pid,
     const float* __restrict__ xgmax, const float* __restrict__ xgmin, const float* __restrict__ qcut,
-    int* __restrict__ dcount, int* __restrict__ dslot, int dR) {
+    int* __restrict__ dcount, int* __restrict__ dslot, int dR, int qskip) {
   static_assert(!DUMP || x1_has_dump(MODE, EL), "dump form");
   static_assert(!HYB || (!DUMP && x1_has_dump(MODE, EL)), "hybrid launch");
   constexpr int NBUF = kNbuf;
@@ -321,7 +321,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     }
   }
   // a gathered batch (device-side count): query tiles past it have nothing to do
-  if (qcount && qt * kT >= *qcount) return;  // uniform
+  // (qskip: a gathered stage of at most qskip queries is skinny_plane_topk's)
+  if (qcount && (qt * kT >= *qcount || *qcount <= qskip)) return;  // uniform
   const int s0 = (int)((int64_t)sp * ntiles / nsplit);
   const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
   const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
@@ -1409,20 +1410,20 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
                            st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                            a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                            a.self0, a.qrow, a.qcount, p0, p1, nparts, part.KP, qg, part.key,
-                           part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
+                           part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR, a.qskip);
     } else if (hyb) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL, true>), dim3(nqt * a.nsplit),
                            dim3(512), 0, st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH,
                            a.qs, a.qaux, a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt,
                            a.qtile0, a.self0, a.qrow, a.qcount, p0, p1, nparts, part.KP, qg,
-                           part.key, part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
+                           part.key, part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR, a.qskip);
     } else {
       hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, false, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                          st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
                          a.nqa, (int)(ldb / 64), a.ntotal, ntiles, a.nsplit, nqt, a.qtile0,
                          a.self0, a.qrow, a.qcount, p0, p1, nparts, part.KP, qg, part.key,
-                         part.id, a.xgmax, a.xgmin, nullptr, nullptr, nullptr, 0);
+                         part.id, a.xgmax, a.xgmin, nullptr, nullptr, nullptr, 0, a.qskip);
     }
     if (a.timing) a.timing->end(st);
     hipError_t e = hipGetLastError();

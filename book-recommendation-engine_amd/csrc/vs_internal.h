@@ -76,6 +76,13 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
                             const int* run = nullptr);
 // Small-batch MFMA path (nq <= kSkinnyMaxQ, KP <= 32, IP or L2 via norms):
 // one list per query per block, part.P == nblocks.
+// The deep bf16 stage for a few gathered queries (device-side count; the
+// kernel exits when it is 0 or above skinny_plane_max_queries()): lane lists
+// of 8 in the x1 layout [slot][part.P][part.KP] from the tile-major bf16 plane
+// (ld = the plane's K in elements) and the gathered query plane's tile 0.
+hipError_t launch_skinny_plane(const void* XH, const void* QH, int64_t ld, int ntotal,
+                               const int* qcount, Partials part, hipStream_t st);
+int skinny_plane_max_queries();
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,
                               int ntotal, int nblocks, Partials part, hipStream_t st);
@@ -107,6 +114,7 @@ struct X1Timing {
 };
 struct X1Args {
   X1Timing* timing = nullptr;
+  int qskip = 0;  // gathered stage: counts <= qskip are skinny_plane_topk's (x1 exits)
   int filter = FILTER_BF16;
   const void* XH = nullptr;      // database plane, tile-major (plane_offset)
   const float* xs = nullptr;     // int8: per-row factor s_x (IP) or s_x / |x| (COS)

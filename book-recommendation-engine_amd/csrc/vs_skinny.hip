@@ -270,6 +270,186 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
   }
 }
 
+// ---------------------------------------------------------------------------
+// skinny_plane_topk: the filter engine's deep bf16 stage for a FEW gathered
+// queries (at most kPlaneQ, a device-side count), HBM-bound.  The x1 pass
+// would multiply every database tile by a whole 256-query tile for them (a
+// 10M-row pass of ~18 ms for 26 queries at C3 k = 60, profiles/r05t); this
+// kernel streams the same bf16 plane once (30.7 GB at 10M x 1536: ~5 ms) and
+// leaves the x1 pass's lane-list layout, so the stage's verification is
+// unchanged.
+//   Plane: tile-major (vs_internal.h plane_offset): tile t's 64-B step s of
+//   its 256 rows is one 16-KB block.  Queries: the first kPlaneQ rows of the
+//   gathered query plane's tile 0, same layout.  Block b of the grid (P =
+//   gridDim.x blocks: the x1 deep stage's 4 * nsplit lane lists) takes tiles
+//   [b * ntiles / P, (b + 1) * ntiles / P) and writes, per query, its top KL
+//   (key -sum, row) to list b — every row of its tiles outside the list has a
+//   key >= the list's last entry, the lane lists' contract.
+//   Four waves; wave w owns rows 64 w .. 64 w + 63 of each tile (4 groups of
+//   16) against the 64 queries (4 groups of 16): 16 v_mfma_f32_16x16x32_bf16
+//   per 64-B step.  LDS-DMA into a ring of kPlaneNB images of 20 KB (16 KB of
+//   rows, 4 KB of queries), chunk c of row r at c ^ ((r >> 2) & 3).
+constexpr int kPlaneQ = 64;
+constexpr int kPlaneNB = 4;
+constexpr int kPlaneImg = 16384 + 4096;
+
+template <int KL>
+__global__ __launch_bounds__(256, 2) void skinny_plane_topk(
+    const char* __restrict__ XH, const char* __restrict__ QH, int nksteps, int ntiles, int ntotal,
+    const int* __restrict__ qcount, float* __restrict__ pkey, int* __restrict__ pid, int KP) {
+  const int cnt = *qcount;
+  if (cnt <= 0 || cnt > kPlaneQ) return;  // uniform: the x1 deep pass takes it
+  constexpr int kFold = kPlaneQ * 16 * KL;  // [query][16 lane lists][KL]
+  constexpr int kWords0 = kPlaneNB * kPlaneImg / 4;
+  constexpr int kWords = kWords0 > 2 * kFold ? kWords0 : 2 * kFold;
+  static_assert(2 * kWords * 4 <= 160 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) float lds[kWords];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int c16 = lane & 15;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(lds);
+  const int P = gridDim.x;
+  const int t0 = (int)((int64_t)blockIdx.x * ntiles / P);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * ntiles / P);
+  const int nst = (t1 - t0) * nksteps;  // steps of this block
+
+  float lk[4][KL];
+  int li[4][KL];
+#pragma unroll
+  for (int qg = 0; qg < 4; ++qg) list_init<KL, int>(lk[qg], li[qg]);
+
+  // DMA: lane L of a 1-KB piece moves 16 B of row (L >> 2) of a 16-row group,
+  // chunk slot L & 3, reading chunk (L & 3) ^ ((row >> 2) & 3) (the swizzle)
+  const uint32_t soff = (uint32_t)(lane >> 2) * 64u + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
+  // this wave's pieces of a step: row pieces 4 w .. 4 w + 3, query piece w
+  auto stage = [&](int gs) {
+    const int t = t0 + gs / nksteps, st = gs - (gs / nksteps) * nksteps;
+    const uint32_t base = lds0 + (uint32_t)((gs % kPlaneNB) * kPlaneImg);
+    const char* xb = XH + ((int64_t)t * nksteps + st) * 16384;
+    const char* qb = QH + (int64_t)st * 16384;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      skinny_glds(xb + (4 * w + i) * 1024, soff,
+                  __builtin_amdgcn_readfirstlane(base + (uint32_t)(4 * w + i) * 1024u));
+    skinny_glds(qb + w * 1024, soff, __builtin_amdgcn_readfirstlane(base + 16384u + (uint32_t)w * 1024u));
+  };
+  // fragment reads: row r (of the 16 KB rows, or of the queries), chunk g
+  auto frag = [&](const char* img, int r) -> bf16x8 {
+    return __builtin_bit_cast(bf16x8, *(const f32x4*)(img + r * 64 + ((g ^ ((r >> 2) & 3)) * 16)));
+  };
+
+  if (nst > 0) {
+#pragma unroll
+    for (int i = 0; i < kPlaneNB - 1; ++i)
+      if (i < nst) stage(i);  // uniform
+    if (nst >= 3) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (nst >= 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x4 acc[4][4];
+    for (int gs = 0; gs < nst; ++gs) {
+      const int st = gs % nksteps;
+      if (st == 0) {
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+          for (int qg = 0; qg < 4; ++qg) acc[rg][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      // step gs+NB-1 into the image step gs-1 used (every wave passed the
+      // barrier after reading it)
+      if (gs + kPlaneNB - 1 < nst) stage(gs + kPlaneNB - 1);
+      const char* img = (const char*)lds + (gs % kPlaneNB) * kPlaneImg;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = frag(img, 64 * w + 16 * i + c16);
+        b[i] = frag(img + 16384, 16 * i + c16);
+      }
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+        for (int qg = 0; qg < 4; ++qg)
+          acc[rg][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rg], b[qg], acc[rg][qg], 0, 0, 0);
+      if (st == nksteps - 1) {
+        // tile done: lane holds rows 16 rg + 4 g + i of the wave's 64 for
+        // query 16 qg + c16; keys -sum, rows past the corpus never enter
+        const int row0 = (t0 + gs / nksteps) * 256 + 64 * w + 4 * g;
+#pragma unroll
+        for (int qg = 0; qg < 4; ++qg)
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = row0 + 16 * rg + i;
+              const float key = -acc[rg][qg][i];
+              if (row < ntotal && lex_less(key, row, lk[qg][KL - 1], li[qg][KL - 1]))
+                list_insert<KL, int>(lk[qg], li[qg], key, row);
+            }
+      }
+      // retire step gs+1: the steps issued after it stay in flight
+      const int younger = min(gs + kPlaneNB - 1, nst - 1) - (gs + 1);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // fold: query q's 16 lists (4 waves x 4 lane groups) in LDS, tree merge,
+  // list b of every query slot written (slots past the count are never read)
+  float* mk = lds;
+  int* mi = (int*)(lds + kFold);
+  __syncthreads();
+  const int slot = w * 4 + g;
+#pragma unroll
+  for (int qg = 0; qg < 4; ++qg) {
+    const int base = ((16 * qg + c16) * 16 + slot) * KL;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      mk[base + j] = lk[qg][j];
+      mi[base + j] = li[qg][j];
+    }
+  }
+  __syncthreads();
+  for (int step = 1; step < 16; step <<= 1) {
+    // 64 queries x 8 pairs at step 1: 512 merges over 256 threads, two each
+    for (int m = tid; m < kPlaneQ * 16; m += 256) {
+      const int q = m >> 4, sl = m & 15;
+      if ((sl & (2 * step - 1)) != 0) continue;
+      float ok[KL];
+      int oi[KL];
+      const int a0 = (q * 16 + sl) * KL, b0 = (q * 16 + sl + step) * KL;
+      merge2_sorted<KL, int>(mk + a0, mi + a0, mk + b0, mi + b0, ok, oi);
+#pragma unroll
+      for (int j = 0; j < KL; ++j) {
+        mk[a0 + j] = ok[j];
+        mi[a0 + j] = oi[j];
+      }
+    }
+    __syncthreads();
+  }
+  for (int m = tid; m < kPlaneQ * KL; m += 256) {
+    const int q = m / KL, j = m - q * KL;
+    const int64_t o = ((int64_t)q * P + blockIdx.x) * KP + j;
+    pkey[o] = mk[q * 16 * KL + j];
+    pid[o] = mi[q * 16 * KL + j];
+  }
+}
+
+hipError_t launch_skinny_plane(const void* XH, const void* QH, int64_t ld, int ntotal,
+                               const int* qcount, Partials part, hipStream_t st) {
+  const int64_t ldb = ld * 2;  // bf16 plane
+  if (ldb % 64 != 0 || part.KP < 8 || part.P < 1 || !qcount) return hipErrorInvalidValue;
+  const int nksteps = (int)(ldb / 64);
+  const int ntiles = (ntotal + 255) / 256;
+  hipLaunchKernelGGL(skinny_plane_topk<8>, dim3(part.P), dim3(256), 0, st, (const char*)XH,
+                     (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key, part.id, part.KP);
+  return hipGetLastError();
+}
+int skinny_plane_max_queries() { return kPlaneQ; }
+
 template <int KP, int MODE, typename T>
 static hipError_t skinny_launch_t(int nq, const T* X, const float* xaux, const T* Q,
                                   const float* qaux, int64_t ld, int ntotal, int nblocks,

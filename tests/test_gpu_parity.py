@@ -828,3 +828,41 @@ def test_staged_engine_hands_clustered_queries_to_bf16(vf):
     Sr, Jr = flat.pgvector_cosine_topk(xb, 15, q_rows=np.arange(3000, 4000))
     bad = flat.selfjoin_mismatches(S, J, Sr, Jr, xb, np.arange(3000, 4000), strict=True)
     assert not bad, bad[:5]
+
+
+def test_deep_stage_few_queries_skinny(vf, monkeypatch):
+    """A few hard queries in a large batch (40 of 4,096, each beside 200
+    near-copies of its own direction): the int8 checks hand them on, and the
+    deep bf16 stage for at most 64 queries runs skinny_plane_topk (one stream
+    of the bf16 plane) instead of an x1 pass over a whole query tile.  Exact
+    on every hard query and a sample of the rest, and the same results with
+    the x1 deep pass (VS_SKINNY_DEEP=0)."""
+    from vsearch import _lib
+
+    rng = np.random.default_rng(123)
+    d = 256
+    xb = rng.uniform(-1, 1, (200_000, d)).astype(np.float32)
+    hard = rng.uniform(-1, 1, (40, d)).astype(np.float32)
+    pos = rng.choice(xb.shape[0], (40, 200), replace=False)
+    for j in range(40):
+        xb[pos[j]] = (hard[j] * (1.0 + 0.02 * rng.uniform(0, 1, (200, 1)))
+                      + 0.01 * rng.standard_normal((200, d))).astype(np.float32)
+    xq = rng.uniform(-1, 1, (4096, d)).astype(np.float32)
+    hq = rng.choice(4096, 40, replace=False)
+    xq[hq] = hard + 0.01 * rng.standard_normal((40, d)).astype(np.float32)
+    index = vf.IndexFlatIP(d)
+    index.add(xb)
+    rows = np.unique(np.concatenate([hq, np.arange(0, 4096, 64)]))
+    Dr, Ir = flat.knn_exact(xb, xq[rows], 10, IP)
+    out = {}
+    for skinny in ("1", "0"):
+        monkeypatch.setenv("VS_SKINNY_DEEP", skinny)
+        _lib.filter_stats(reset=True)
+        D, I = index.search(xq, 10)
+        second = _lib.filter_second_stats()
+        _lib.filter_stats(reset=True)
+        assert 1 <= second <= 64, second
+        bad = flat.mismatches(D[rows], I[rows], Dr, Ir, IP, xb, xq[rows], strict=True)
+        assert not bad, (skinny, bad[:5])
+        out[skinny] = (D, I)
+    assert np.array_equal(out["1"][1], out["0"][1])
