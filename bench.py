@@ -636,13 +636,30 @@ def run_knn(args, ctx):
         t1, k1, n1, _ = ctx.timed(lambda i: index.search_device(q1, k, stream=ctx.stream),
                                   args.batch1_steps, 3)
         kern1 = k1 / max(1, n1) / 1e3
-        bytes1 = n_shard * d * esz
+        kname1 = ctx.lib.timer_kernel()
+        # the small-batch filter pass streams a filter plane (int8: 1 B per
+        # element, bf16: 2), the exact kernels the stored rows
+        esz1 = {"skinny_plane_topk_i8": 1, "skinny_plane_topk": 2}.get(kname1, esz)
+        bytes1 = n_shard * d * esz1
         batch1 = {"ms_per_query": round(t1 / args.batch1_steps * 1e3, 4),
-                  "qps": round(args.batch1_steps / t1, 2), "kernel": ctx.lib.timer_kernel(),
+                  "qps": round(args.batch1_steps / t1, 2), "kernel": kname1,
                   "kernel_ms": round(kern1 * 1e3, 4),
+                  "bytes_per_query": bytes1,
                   "achieved_GBs": round(bytes1 / kern1 / 1e9, 1) if kern1 > 0 else None,
                   "frac_hbm_peak": round(bytes1 / kern1 / 1e9 / HBM_PEAK_GBS, 4)
                   if kern1 > 0 else None}
+        if kname1.startswith("skinny_plane"):
+            # beside it, the exact stream over the stored rows (VS_SMALL_FILTER=0)
+            os.environ["VS_SMALL_FILTER"] = "0"
+            t2, k2, n2, _ = ctx.timed(lambda i: index.search_device(q1, k, stream=ctx.stream),
+                                      args.batch1_steps, 3)
+            del os.environ["VS_SMALL_FILTER"]
+            kern2 = k2 / max(1, n2) / 1e3
+            batch1["exact_stream"] = {"ms_per_query": round(t2 / args.batch1_steps * 1e3, 4),
+                                      "kernel": ctx.lib.timer_kernel(),
+                                      "kernel_ms": round(kern2 * 1e3, 4),
+                                      "frac_hbm_peak": round(n_shard * d * esz / kern2 / 1e9 /
+                                                             HBM_PEAK_GBS, 4) if kern2 > 0 else None}
 
     # The service's wide searches (service.py:627 k = 30, :529-531 k = 60 over
     # a coalesced batch): inner product's rule reads the 2k - 1 best, i.e. 64

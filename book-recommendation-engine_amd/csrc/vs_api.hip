@@ -840,6 +840,15 @@ static bool dump_enabled() {
   return v;
 }
 
+// Small batches through the staged engine's skinny passes (env
+// VS_SMALL_FILTER=0 keeps the exact streaming kernels, for A/B; read at every
+// search), over indexes of at least kSmallFilterMinRows rows.
+constexpr int64_t kSmallFilterMinRows = 1 << 18;
+bool small_filter_on() {
+  const char* e = getenv("VS_SMALL_FILTER");
+  return !e || atoi(e) != 0;
+}
+
 // The deep stage's small-count kernel (env VS_SKINNY_DEEP=0 turns it off,
 // for A/B; read at every search).
 bool skinny_deep_on() {
@@ -892,6 +901,13 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   // loses 3 % with them; profiles/r05s)
   if (!gathered && !deep && plane == FILTER_BF16)
     x.nsplit = (int)std::min<int64_t>(ntiles, 2 * (int64_t)x.nsplit);
+  // A small batch (at most skinny_plane_max_queries() queries, the first stage
+  // of a search routed here by run_topk) streams its plane once through
+  // skinny_plane_topk instead of an x1 pass over a whole query tile: 2,048
+  // lists of 8 per query, the deep stage's count
+  const bool small = !gathered && !deep && a.nq <= skinny_plane_max_queries() && a.self0 < 0 &&
+                     (mode == MODE_IP || (mode == MODE_L2 && idx->l2aug()));  // the pass's IP
+  if (small) x.nsplit = (int)std::min<int64_t>(512, std::max<int64_t>(1, (ntiles + 3) / 4));
   x.nsplit = std::max(x.nsplit, 1);
   {  // A/B: more (shorter) database splits = more lane lists per query
     static const int mult = [] {
@@ -1010,7 +1026,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   x.qcount = gc;
   const BoundArgs ba = aug ? make_bound_args_l2aug(idx->ld, idx->aug, plane)
                            : make_bound_args(idx->ld, plane);
-  if (!gathered && x1_dump_applies(kmode, plane) && dump_enabled() &&
+  if (!gathered && !small && x1_dump_applies(kmode, plane) && dump_enabled() &&
       x1_pass_dumps(ntotal, x.nsplit)) {
     // query cuts + dump launches (vs_gemm_x1.hip header and "Query cuts"): the
     // cuts are set after the pass's first launch and are the verification's
@@ -1056,11 +1072,23 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
     // a self-join): skinny_plane_topk streams the plane once for them and
     // the x1 pass exits, or the reverse, by the device-side count
     if (gathered && deep && !i8 && kmode == MODE_IP && a.self0 < 0 && skinny_deep_on()) {
-      VS_HIP(launch_skinny_plane(x.XH, x.QH, x.ld, ntotal, gc, part, st), "vs: skinny deep stage");
+      VS_HIP(launch_skinny_plane(FILTER_BF16, x.XH, x.QH, x.ld, ntotal, gc, nullptr, nullptr, part,
+                                 st),
+             "vs: skinny deep stage");
       x.qskip = skinny_plane_max_queries();
     }
-    int nd = 0;
-    VS_HIP(launch_gemm_topk_x1(kmode, x, part, st, &nd), "vs: gemm_topk_x1 launch");
+    if (small) {
+      int* cnt = nullptr;
+      VS_HIP(scr.alloc((void**)&cnt, sizeof(int)), "vs: scratch");
+      VS_HIP(hipMemsetD32Async((hipDeviceptr_t)cnt, a.nq, 1, st), "vs: count");
+      KernelTimer ks(st, i8 ? "skinny_plane_topk_i8" : "skinny_plane_topk");
+      VS_HIP(launch_skinny_plane(plane, x.XH, x.QH, x.ld, ntotal, cnt, qs, x.xs, part, st),
+             "vs: skinny first stage");
+      ks.stop();
+    } else {
+      int nd = 0;
+      VS_HIP(launch_gemm_topk_x1(kmode, x, part, st, &nd), "vs: gemm_topk_x1 launch");
+    }
     x.timing = nullptr;
     whole.stop();
   }
@@ -1187,20 +1215,40 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
   const float* Qa = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
   const float* qinv = a.mode == MODE_COS ? ac : nullptr;
   const float* xinv = a.mode == MODE_COS ? a.xaux : nullptr;
+  // A small batch (its flagged queries are at most its a.nq <= kSkinnyMaxQ):
+  // the skinny fp32 kernel streams the rows once over the gathered queries
+  // (slots past the device-side count score garbage that no merge reads)
+  // instead of a GEMM over a whole query tile
+  const bool skinny = a.nq <= kSkinnyMaxQ && KP <= 32 && (a.nq <= 16 || KP <= 16) && a.self0 < 0 &&
+                      (a.mode == MODE_IP || a.mode == MODE_L2) && (idx->ld * idx->esize) % 128 == 0;
+  Partials sp;
+  if (skinny) {
+    sp.KP = KP;
+    sp.P = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (ntotal + 255) / 256));
+    VS_HIP(scr.alloc((void**)&sp.key, (size_t)kSkinnyMaxQ * sp.P * KP * sizeof(float)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&sp.id, (size_t)kSkinnyMaxQ * sp.P * KP * sizeof(int)), "vs: scratch");
+  }
   for (int w0 = 0; w0 < nslot; w0 += cap) {
     const int* wl = gl + w0;  // this window's query ids, wc[0] of them
     VS_HIP(launch_window_count(gc, w0, cap, wc, st), "vs: window");
-    VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, Qa, a.qaux, idx->ld, idx->esize, ntotal,
-                            cap, nsplit, a.self0, part, st, wl, wc),
-           "vs: gemm_topk launch");
     // the window's query rows and aux values, slot by slot, for the rescoring
     VS_HIP(launch_gather_queries(Qa, idx->ld, a.qaux, wl, wc, cap, a.self0, qc, ac, qrow, st),
            "vs: gathered queries");
-    VS_HIP(launch_merge_partials(MODE_L2, part, cap, KF, 0, 0.0f, Dk, Ik, KF, st, 0, nullptr, wc),
+    if (skinny) {
+      VS_HIP(launch_skinny_topk(KP, a.mode, a.nq, idx->codes, idx->esize, a.xaux, qc, ac, idx->ld,
+                                ntotal, sp.P, sp, st),
+             "vs: skinny_topk launch");
+    } else {
+      VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, Qa, a.qaux, idx->ld, idx->esize,
+                              ntotal, cap, nsplit, a.self0, part, st, wl, wc),
+             "vs: gemm_topk launch");
+    }
+    VS_HIP(launch_merge_partials(MODE_L2, skinny ? sp : part, skinny ? a.nq : cap, KF, 0, 0.0f, Dk,
+                                 Ik, KF, st, 0, nullptr, wc),
            "vs: merge");
     VS_HIP(launch_verify_rescore(a.mode, cap, KF, need, Dk, Ik, (const float*)idx->codes,
                                  idx->norms, qc, ac, idx->ld, make_bound_args(idx->ld, plane),
-                                 idx->bstats[plane], part, KP, vp.key, vp.id, vp.KP, flags, st,
+                                 idx->bstats[plane], skinny ? sp : part, KP, vp.key, vp.id, vp.KP, flags, st,
                                  qinv, xinv, nullptr, wc),
            "vs: rescore");
     VS_HIP(launch_merge_partials(a.mode, vp, cap, a.k, idx->id_base, a.min_score, a.D, a.I, a.k,
@@ -1429,6 +1477,19 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
   if (pref && strcmp(pref, "gemv") == 0 && small_ok && gemv_fits && nq <= kGemvMaxQ &&
       (mode == MODE_IP || direct))
     gemv = true;
+  // Small batches over a large fp32 index with a filter plane for the metric
+  // (inner product; L2 when faiss would take its BLAS branch): the staged
+  // engine with skinny passes — the int8 plane streamed once (a quarter of the
+  // fp32 bytes), candidates rescored and proven exactly as for large batches,
+  // the few queries it cannot settle through the bf16 plane and the fp32
+  // rows (skinny kernels too) — instead of streaming the fp32 rows.
+  if (small_filter_on() && idx->esize == 4 && engine == VS_ENGINE_AUTO && KF > 0 && KF <= 32 &&
+      nq <= kSkinnyMaxQ && a.self0 < 0 && ntotal >= kSmallFilterMinRows &&
+      (mode == MODE_IP || (mode == MODE_L2 && !a.l2_direct)) && (i8_ok || b16_ok)) {
+    if (i8_ok && b16_ok) i8_ok = adaptive_use_i8(idx);
+    if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
+    return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);
+  }
   Scratch scr(st);
   Partials part;
   part.KP = KP;

@@ -80,8 +80,11 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
 // kernel exits when it is 0 or above skinny_plane_max_queries()): lane lists
 // of 8 in the x1 layout [slot][part.P][part.KP] from the tile-major bf16 plane
 // (ld = the plane's K in elements) and the gathered query plane's tile 0.
-hipError_t launch_skinny_plane(const void* XH, const void* QH, int64_t ld, int ntotal,
-                               const int* qcount, Partials part, hipStream_t st);
+// filter FILTER_I8: the int8 plane with the x1 pass's keys (qs: the queries'
+// scales, xs: the rows' factors).
+hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64_t ld, int ntotal,
+                               const int* qcount, const float* qs, const float* xs, Partials part,
+                               hipStream_t st);
 int skinny_plane_max_queries();
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,

@@ -293,10 +293,14 @@ constexpr int kPlaneQ = 64;
 constexpr int kPlaneNB = 4;
 constexpr int kPlaneImg = 16384 + 4096;
 
-template <int KL>
+template <int KL, int EL>
 __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     const char* __restrict__ XH, const char* __restrict__ QH, int nksteps, int ntiles, int ntotal,
-    const int* __restrict__ qcount, float* __restrict__ pkey, int* __restrict__ pid, int KP) {
+    const int* __restrict__ qcount, float* __restrict__ pkey, int* __restrict__ pid, int KP,
+    const float* __restrict__ qs, const float* __restrict__ xs) {
+  // EL: the plane (FILTER_BF16: v_mfma_f32_16x16x32_bf16, key -sum; FILTER_I8:
+  // v_mfma_i32_16x16x64_i8, key -(sum * (s_q * s_x)) — the x1 pass's keys)
+  using Acc = typename std::conditional<EL == FILTER_I8, i32x4, f32x4>::type;
   const int cnt = *qcount;
   if (cnt <= 0 || cnt > kPlaneQ) return;  // uniform: the x1 deep pass takes it
   constexpr int kFold = kPlaneQ * 16 * KL;  // [query][16 lane lists][KL]
@@ -336,9 +340,14 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     skinny_glds(qb + w * 1024, soff, __builtin_amdgcn_readfirstlane(base + 16384u + (uint32_t)w * 1024u));
   };
   // fragment reads: row r (of the 16 KB rows, or of the queries), chunk g
-  auto frag = [&](const char* img, int r) -> bf16x8 {
-    return __builtin_bit_cast(bf16x8, *(const f32x4*)(img + r * 64 + ((g ^ ((r >> 2) & 3)) * 16)));
+  auto frag = [&](const char* img, int r) -> i32x4 {
+    return *(const i32x4*)(img + r * 64 + ((g ^ ((r >> 2) & 3)) * 16));
   };
+  float qsc[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EL == FILTER_I8) {
+#pragma unroll
+    for (int qg = 0; qg < 4; ++qg) qsc[qg] = qs[16 * qg + c16];
+  }
 
   if (nst > 0) {
 #pragma unroll
@@ -348,20 +357,20 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     else if (nst >= 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    f32x4 acc[4][4];
+    Acc acc[4][4];
     for (int gs = 0; gs < nst; ++gs) {
       const int st = gs % nksteps;
       if (st == 0) {
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
-          for (int qg = 0; qg < 4; ++qg) acc[rg][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          for (int qg = 0; qg < 4; ++qg) acc[rg][qg] = Acc{};
       }
       // step gs+NB-1 into the image step gs-1 used (every wave passed the
       // barrier after reading it)
       if (gs + kPlaneNB - 1 < nst) stage(gs + kPlaneNB - 1);
       const char* img = (const char*)lds + (gs % kPlaneNB) * kPlaneImg;
-      bf16x8 a[4], b[4];
+      i32x4 a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         a[i] = frag(img, 64 * w + 16 * i + c16);
@@ -370,23 +379,36 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
-        for (int qg = 0; qg < 4; ++qg)
-          acc[rg][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rg], b[qg], acc[rg][qg], 0, 0, 0);
+        for (int qg = 0; qg < 4; ++qg) {
+          if constexpr (EL == FILTER_I8)
+            acc[rg][qg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg], b[qg], acc[rg][qg], 0, 0, 0);
+          else
+            acc[rg][qg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, a[rg]), __builtin_bit_cast(bf16x8, b[qg]), acc[rg][qg],
+                0, 0, 0);
+        }
       if (st == nksteps - 1) {
         // tile done: lane holds rows 16 rg + 4 g + i of the wave's 64 for
         // query 16 qg + c16; keys -sum, rows past the corpus never enter
         const int row0 = (t0 + gs / nksteps) * 256 + 64 * w + 4 * g;
 #pragma unroll
-        for (int qg = 0; qg < 4; ++qg)
+        for (int rg = 0; rg < 4; ++rg) {
+          f32x4 fx = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EL == FILTER_I8) fx = *(const f32x4*)(xs + row0 + 16 * rg);
 #pragma unroll
-          for (int rg = 0; rg < 4; ++rg)
+          for (int qg = 0; qg < 4; ++qg)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int row = row0 + 16 * rg + i;
-              const float key = -acc[rg][qg][i];
+              float key;
+              if constexpr (EL == FILTER_I8)
+                key = -((float)acc[rg][qg][i] * (qsc[qg] * fx[i]));  // x1_key<FILTER_I8>
+              else
+                key = -acc[rg][qg][i];
               if (row < ntotal && lex_less(key, row, lk[qg][KL - 1], li[qg][KL - 1]))
                 list_insert<KL, int>(lk[qg], li[qg], key, row);
             }
+        }
       }
       // retire step gs+1: the steps issued after it stay in flight
       const int younger = min(gs + kPlaneNB - 1, nst - 1) - (gs + 1);
@@ -438,14 +460,23 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
   }
 }
 
-hipError_t launch_skinny_plane(const void* XH, const void* QH, int64_t ld, int ntotal,
-                               const int* qcount, Partials part, hipStream_t st) {
-  const int64_t ldb = ld * 2;  // bf16 plane
-  if (ldb % 64 != 0 || part.KP < 8 || part.P < 1 || !qcount) return hipErrorInvalidValue;
+hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64_t ld, int ntotal,
+                               const int* qcount, const float* qs, const float* xs, Partials part,
+                               hipStream_t st) {
+  const int64_t ldb = ld * (filter == FILTER_I8 ? 1 : 2);
+  if (ldb % 64 != 0 || part.KP < 8 || part.P < 1 || !qcount ||
+      (filter == FILTER_I8 && (!qs || !xs)))
+    return hipErrorInvalidValue;
   const int nksteps = (int)(ldb / 64);
   const int ntiles = (ntotal + 255) / 256;
-  hipLaunchKernelGGL(skinny_plane_topk<8>, dim3(part.P), dim3(256), 0, st, (const char*)XH,
-                     (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key, part.id, part.KP);
+  if (filter == FILTER_I8)
+    hipLaunchKernelGGL((skinny_plane_topk<8, FILTER_I8>), dim3(part.P), dim3(256), 0, st,
+                       (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key,
+                       part.id, part.KP, qs, xs);
+  else
+    hipLaunchKernelGGL((skinny_plane_topk<8, FILTER_BF16>), dim3(part.P), dim3(256), 0, st,
+                       (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key,
+                       part.id, part.KP, qs, xs);
   return hipGetLastError();
 }
 int skinny_plane_max_queries() { return kPlaneQ; }

@@ -866,3 +866,36 @@ def test_deep_stage_few_queries_skinny(vf, monkeypatch):
         assert not bad, (skinny, bad[:5])
         out[skinny] = (D, I)
     assert np.array_equal(out["1"][1], out["0"][1])
+
+
+@pytest.mark.parametrize("metric", [IP, flat.METRIC_L2])
+def test_small_batches_through_the_filter_planes(vf, metric, monkeypatch):
+    """Small batches (1 .. 64 queries) over an index of >= 2^18 rows run the
+    staged engine with skinny passes (skinny_plane_topk over the int8 plane,
+    then the bf16 plane and the fp32 rows for what it cannot settle): exact
+    against the oracle, including queries beside 200 near-copies of their own
+    direction that the int8 checks hand on, and the same labels as the exact
+    streaming kernels (VS_SMALL_FILTER=0).  L2 calls of fewer than 20 queries
+    keep faiss's sequential formula (the exact GEMV)."""
+    rng = np.random.default_rng(321)
+    d = 128
+    xb = rng.uniform(-1, 1, (300_000, d)).astype(np.float32)
+    hard = rng.uniform(-1, 1, (6, d)).astype(np.float32)
+    pos = rng.choice(xb.shape[0], (6, 200), replace=False)
+    for j in range(6):
+        xb[pos[j]] = (hard[j] * (1.0 + 0.02 * rng.uniform(0, 1, (200, 1)))
+                      + 0.01 * rng.standard_normal((200, d))).astype(np.float32)
+    index = vf.IndexFlatL2(d) if metric == flat.METRIC_L2 else vf.IndexFlatIP(d)
+    index.add(xb)
+    for nq in (1, 7, 32, 64):
+        xq = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+        nh = min(nq, 3)
+        xq[:nh] = hard[:nh] + 0.01 * rng.standard_normal((nh, d)).astype(np.float32)
+        monkeypatch.delenv("VS_SMALL_FILTER", raising=False)
+        D, I = index.search(xq, 10)
+        Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
+        assert not bad, (nq, bad[:5])
+        monkeypatch.setenv("VS_SMALL_FILTER", "0")
+        D0, I0 = index.search(xq, 10)
+        assert not flat.mismatches(D0, I0, Dr, Ir, metric, xb, xq), nq
