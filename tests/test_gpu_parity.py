@@ -894,7 +894,10 @@ def test_small_batches_through_the_filter_planes(vf, metric, monkeypatch):
         monkeypatch.delenv("VS_SMALL_FILTER", raising=False)
         D, I = index.search(xq, 10)
         Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
+        # (L2 under 20 queries: faiss's sequential formula, checked at the
+        # north star's tolerance like the other exact kernels)
+        strict = not (metric == flat.METRIC_L2 and nq < 20)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=strict)
         assert not bad, (nq, bad[:5])
         monkeypatch.setenv("VS_SMALL_FILTER", "0")
         D0, I0 = index.search(xq, 10)
