@@ -1236,7 +1236,7 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
            "vs: gathered queries");
     if (skinny) {
       VS_HIP(launch_skinny_topk(KP, a.mode, a.nq, idx->codes, idx->esize, a.xaux, qc, ac, idx->ld,
-                                ntotal, sp.P, sp, st),
+                                ntotal, sp.P, sp, st, wc),
              "vs: skinny_topk launch");
     } else {
       VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, Qa, a.qaux, idx->ld, idx->esize,

@@ -86,9 +86,12 @@ hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64
                                const int* qcount, const float* qs, const float* xs, Partials part,
                                hipStream_t st);
 int skinny_plane_max_queries();
+// qcount (optional, device): the kernel does nothing when *qcount is 0 (the
+// staged engine's last stage over a gathered batch, usually empty)
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,
-                              int ntotal, int nblocks, Partials part, hipStream_t st);
+                              int ntotal, int nblocks, Partials part, hipStream_t st,
+                              const int* qcount = nullptr);
 // The filter pass of the filter-and-verify engine (vs_gemm_x1.hip): one MFMA
 // product per fp32 product over a low-precision "filter plane" of rows and
 // queries: bf16 (RNE) on v_mfma_f32_32x32x16_bf16, or int8 with one fp32 scale

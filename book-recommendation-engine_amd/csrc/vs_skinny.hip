@@ -62,8 +62,12 @@ __global__ __launch_bounds__(256, 2) void skinny_topk(const T* __restrict__ X,
                                                       const float* __restrict__ qaux, int64_t ld,
                                                       int nq, int ntotal, int rows_per_block,
                                                       float* __restrict__ pkey,
-                                                      int* __restrict__ pid) {
+                                                      int* __restrict__ pid,
+                                                      const int* __restrict__ qcount) {
   static_assert(KP <= 32, "skinny path keeps at most 32 entries per list");
+  // a gathered batch (the staged engine's last stage): nothing to do when the
+  // device-side count is 0 (the lists are then never read)
+  if (qcount && *qcount <= 0) return;  // uniform
   constexpr int NB = skinny_nbuf<NQG>();
   constexpr int R = kSkinnyRows;
   // LDS, three lives: [NB images][128 X rows + 16*NQG query rows][128 B] during
@@ -484,53 +488,55 @@ int skinny_plane_max_queries() { return kPlaneQ; }
 template <int KP, int MODE, typename T>
 static hipError_t skinny_launch_t(int nq, const T* X, const float* xaux, const T* Q,
                                   const float* qaux, int64_t ld, int ntotal, int nblocks,
-                                  Partials part, hipStream_t st) {
+                                  Partials part, hipStream_t st, const int* qcount) {
   const int nt256 = (ntotal + 255) & ~255;
   int rpb = (nt256 + nblocks - 1) / nblocks;
   rpb = (rpb + 255) & ~255;  // whole 256-row tiles
   if (nq <= 16)
     hipLaunchKernelGGL((skinny_topk<KP, MODE, T, 1>), dim3(nblocks), dim3(256), 0, st, X, xaux,
-                       Q, qaux, ld, nq, ntotal, rpb, part.key, part.id);
+                       Q, qaux, ld, nq, ntotal, rpb, part.key, part.id, qcount);
   else
     hipLaunchKernelGGL((skinny_topk<KP, MODE, T, 2>), dim3(nblocks), dim3(256), 0, st, X, xaux,
-                       Q, qaux, ld, nq, ntotal, rpb, part.key, part.id);
+                       Q, qaux, ld, nq, ntotal, rpb, part.key, part.id, qcount);
   return hipGetLastError();
 }
 
 template <int KP>
 static hipError_t skinny_launch_kp(int mode, int nq, const void* X, int esize, const float* xaux,
                                    const void* Q, const float* qaux, int64_t ld, int ntotal,
-                                   int nblocks, Partials part, hipStream_t st) {
+                                   int nblocks, Partials part, hipStream_t st, const int* qcount) {
   if (esize == 4) {
     if (mode == MODE_L2)
       return skinny_launch_t<KP, MODE_L2, float>(nq, (const float*)X, xaux, (const float*)Q, qaux,
-                                                 ld, ntotal, nblocks, part, st);
+                                                 ld, ntotal, nblocks, part, st, qcount);
     return skinny_launch_t<KP, MODE_IP, float>(nq, (const float*)X, xaux, (const float*)Q, qaux,
-                                               ld, ntotal, nblocks, part, st);
+                                               ld, ntotal, nblocks, part, st, qcount);
   }
   if (mode == MODE_L2)
     return skinny_launch_t<KP, MODE_L2, uint16_t>(nq, (const uint16_t*)X, xaux,
                                                   (const uint16_t*)Q, qaux, ld, ntotal, nblocks,
-                                                  part, st);
+                                                  part, st, qcount);
   return skinny_launch_t<KP, MODE_IP, uint16_t>(nq, (const uint16_t*)X, xaux, (const uint16_t*)Q,
-                                                qaux, ld, ntotal, nblocks, part, st);
+                                                qaux, ld, ntotal, nblocks, part, st, qcount);
 }
 
 hipError_t launch_skinny_topk(int KP, int mode, int nq, const void* X, int esize,
                               const float* xaux, const void* Q, const float* qaux, int64_t ld,
-                              int ntotal, int nblocks, Partials part, hipStream_t st) {
+                              int ntotal, int nblocks, Partials part, hipStream_t st,
+                              const int* qcount) {
   if (nq < 1 || nq > kSkinnyMaxQ || part.KP != KP || part.P != nblocks ||
       (ld * esize) % 128 != 0 || (esize != 4 && esize != 2) || (mode != MODE_IP && mode != MODE_L2))
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:
-      return skinny_launch_kp<8>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part, st);
+      return skinny_launch_kp<8>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part, st,
+                                 qcount);
     case 16:
       return skinny_launch_kp<16>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part,
-                                  st);
+                                  st, qcount);
     case 32:
       return skinny_launch_kp<32>(mode, nq, X, esize, xaux, Q, qaux, ld, ntotal, nblocks, part,
-                                  st);
+                                  st, qcount);
     default:
       return hipErrorInvalidValue;
   }
