@@ -1082,7 +1082,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
       VS_HIP(scr.alloc((void**)&cnt, sizeof(int)), "vs: scratch");
       VS_HIP(hipMemsetD32Async((hipDeviceptr_t)cnt, a.nq, 1, st), "vs: count");
       KernelTimer ks(st, i8 ? "skinny_plane_topk_i8" : "skinny_plane_topk");
-      VS_HIP(launch_skinny_plane(plane, x.XH, x.QH, x.ld, ntotal, cnt, qs, x.xs, part, st),
+      VS_HIP(launch_skinny_plane(plane, x.XH, x.QH, x.ld, ntotal, cnt, qs, x.xs, part, st, a.nq),
              "vs: skinny first stage");
       ks.stop();
     } else {

@@ -84,7 +84,7 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
 // scales, xs: the rows' factors).
 hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64_t ld, int ntotal,
                                const int* qcount, const float* qs, const float* xs, Partials part,
-                               hipStream_t st);
+                               hipStream_t st, int nq_hint = 0);
 int skinny_plane_max_queries();
 // qcount (optional, device): the kernel does nothing when *qcount is 0 (the
 // staged engine's last stage over a gathered batch, usually empty)

@@ -297,16 +297,19 @@ constexpr int kPlaneQ = 64;
 constexpr int kPlaneNB = 4;
 constexpr int kPlaneImg = 16384 + 4096;
 
-template <int KL, int EL>
+template <int KL, int EL, int NQG>
 __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     const char* __restrict__ XH, const char* __restrict__ QH, int nksteps, int ntiles, int ntotal,
     const int* __restrict__ qcount, float* __restrict__ pkey, int* __restrict__ pid, int KP,
     const float* __restrict__ qs, const float* __restrict__ xs) {
+  // NQG query groups of 16 (1: at most 16 queries, a quarter of the MFMAs and
+  // fragment reads; 4: at most 64)
   // EL: the plane (FILTER_BF16: v_mfma_f32_16x16x32_bf16, key -sum; FILTER_I8:
   // v_mfma_i32_16x16x64_i8, key -(sum * (s_q * s_x)) — the x1 pass's keys)
   using Acc = typename std::conditional<EL == FILTER_I8, i32x4, f32x4>::type;
   const int cnt = *qcount;
-  if (cnt <= 0 || cnt > kPlaneQ) return;  // uniform: the x1 deep pass takes it
+  // uniform: the x1 deep pass (more than kPlaneQ) or the other variant takes it
+  if (cnt <= 0 || cnt > 16 * NQG || (NQG > 1 && cnt <= 16)) return;
   constexpr int kFold = kPlaneQ * 16 * KL;  // [query][16 lane lists][KL]
   constexpr int kWords0 = kPlaneNB * kPlaneImg / 4;
   constexpr int kWords = kWords0 > 2 * kFold ? kWords0 : 2 * kFold;
@@ -323,10 +326,10 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
   const int t1 = (int)((int64_t)(blockIdx.x + 1) * ntiles / P);
   const int nst = (t1 - t0) * nksteps;  // steps of this block
 
-  float lk[4][KL];
-  int li[4][KL];
+  float lk[NQG][KL];
+  int li[NQG][KL];
 #pragma unroll
-  for (int qg = 0; qg < 4; ++qg) list_init<KL, int>(lk[qg], li[qg]);
+  for (int qg = 0; qg < NQG; ++qg) list_init<KL, int>(lk[qg], li[qg]);
 
   // DMA: lane L of a 1-KB piece moves 16 B of row (L >> 2) of a 16-row group,
   // chunk slot L & 3, reading chunk (L & 3) ^ ((row >> 2) & 3) (the swizzle)
@@ -341,17 +344,19 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     for (int i = 0; i < 4; ++i)
       skinny_glds(xb + (4 * w + i) * 1024, soff,
                   __builtin_amdgcn_readfirstlane(base + (uint32_t)(4 * w + i) * 1024u));
-    skinny_glds(qb + w * 1024, soff, __builtin_amdgcn_readfirstlane(base + 16384u + (uint32_t)w * 1024u));
+    // query piece w (NQG = 1: every wave the same piece 0, identical bytes to
+    // identical LDS addresses, so every wave issues 5 loads per step)
+    const int qp = NQG == 1 ? 0 : w;
+    skinny_glds(qb + qp * 1024, soff,
+                __builtin_amdgcn_readfirstlane(base + 16384u + (uint32_t)qp * 1024u));
   };
   // fragment reads: row r (of the 16 KB rows, or of the queries), chunk g
   auto frag = [&](const char* img, int r) -> i32x4 {
     return *(const i32x4*)(img + r * 64 + ((g ^ ((r >> 2) & 3)) * 16));
   };
-  float qsc[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (EL == FILTER_I8) {
+  float qsc[NQG];
 #pragma unroll
-    for (int qg = 0; qg < 4; ++qg) qsc[qg] = qs[16 * qg + c16];
-  }
+  for (int qg = 0; qg < NQG; ++qg) qsc[qg] = EL == FILTER_I8 ? qs[16 * qg + c16] : 0.0f;
 
   if (nst > 0) {
 #pragma unroll
@@ -361,29 +366,28 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     else if (nst >= 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    Acc acc[4][4];
+    Acc acc[4][NQG];
     for (int gs = 0; gs < nst; ++gs) {
       const int st = gs % nksteps;
       if (st == 0) {
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
-          for (int qg = 0; qg < 4; ++qg) acc[rg][qg] = Acc{};
+          for (int qg = 0; qg < NQG; ++qg) acc[rg][qg] = Acc{};
       }
       // step gs+NB-1 into the image step gs-1 used (every wave passed the
       // barrier after reading it)
       if (gs + kPlaneNB - 1 < nst) stage(gs + kPlaneNB - 1);
       const char* img = (const char*)lds + (gs % kPlaneNB) * kPlaneImg;
-      i32x4 a[4], b[4];
+      i32x4 a[4], b[NQG];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = frag(img, 64 * w + 16 * i + c16);
-        b[i] = frag(img + 16384, 16 * i + c16);
-      }
+      for (int i = 0; i < 4; ++i) a[i] = frag(img, 64 * w + 16 * i + c16);
+#pragma unroll
+      for (int i = 0; i < NQG; ++i) b[i] = frag(img + 16384, 16 * i + c16);
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg)
 #pragma unroll
-        for (int qg = 0; qg < 4; ++qg) {
+        for (int qg = 0; qg < NQG; ++qg) {
           if constexpr (EL == FILTER_I8)
             acc[rg][qg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg], b[qg], acc[rg][qg], 0, 0, 0);
           else
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
           f32x4 fx = {0.f, 0.f, 0.f, 0.f};
           if constexpr (EL == FILTER_I8) fx = *(const f32x4*)(xs + row0 + 16 * rg);
 #pragma unroll
-          for (int qg = 0; qg < 4; ++qg)
+          for (int qg = 0; qg < NQG; ++qg)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int row = row0 + 16 * rg + i;
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
   __syncthreads();
   const int slot = w * 4 + g;
 #pragma unroll
-  for (int qg = 0; qg < 4; ++qg) {
+  for (int qg = 0; qg < NQG; ++qg) {
     const int base = ((16 * qg + c16) * 16 + slot) * KL;
 #pragma unroll
     for (int j = 0; j < KL; ++j) {
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
   __syncthreads();
   for (int step = 1; step < 16; step <<= 1) {
     // 64 queries x 8 pairs at step 1: 512 merges over 256 threads, two each
-    for (int m = tid; m < kPlaneQ * 16; m += 256) {
+    for (int m = tid; m < 16 * NQG * 16; m += 256) {
       const int q = m >> 4, sl = m & 15;
       if ((sl & (2 * step - 1)) != 0) continue;
       float ok[KL];
@@ -456,7 +460,7 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     }
     __syncthreads();
   }
-  for (int m = tid; m < kPlaneQ * KL; m += 256) {
+  for (int m = tid; m < 16 * NQG * KL; m += 256) {
     const int q = m / KL, j = m - q * KL;
     const int64_t o = ((int64_t)q * P + blockIdx.x) * KP + j;
     pkey[o] = mk[q * 16 * KL + j];
@@ -466,21 +470,28 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
 
 hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64_t ld, int ntotal,
                                const int* qcount, const float* qs, const float* xs, Partials part,
-                               hipStream_t st) {
+                               hipStream_t st, int nq_hint) {
   const int64_t ldb = ld * (filter == FILTER_I8 ? 1 : 2);
   if (ldb % 64 != 0 || part.KP < 8 || part.P < 1 || !qcount ||
       (filter == FILTER_I8 && (!qs || !xs)))
     return hipErrorInvalidValue;
   const int nksteps = (int)(ldb / 64);
   const int ntiles = (ntotal + 255) / 256;
-  if (filter == FILTER_I8)
-    hipLaunchKernelGGL((skinny_plane_topk<8, FILTER_I8>), dim3(part.P), dim3(256), 0, st,
-                       (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key,
-                       part.id, part.KP, qs, xs);
-  else
-    hipLaunchKernelGGL((skinny_plane_topk<8, FILTER_BF16>), dim3(part.P), dim3(256), 0, st,
-                       (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key,
-                       part.id, part.KP, qs, xs);
+  // nq_hint: the host's bound on the count (0: unknown, up to kPlaneQ): the
+  // 16-query variant runs for counts <= 16, the 64-query one above; each exits
+  // on the other's counts, so both are launched unless the bound decides
+#define VS_SP(EL_, NQG_)                                                                       \
+  hipLaunchKernelGGL((skinny_plane_topk<8, EL_, NQG_>), dim3(part.P), dim3(256), 0, st,         \
+                     (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key, \
+                     part.id, part.KP, qs, xs)
+  if (filter == FILTER_I8) {
+    VS_SP(FILTER_I8, 1);
+    if (nq_hint <= 0 || nq_hint > 16) VS_SP(FILTER_I8, 4);
+  } else {
+    VS_SP(FILTER_BF16, 1);
+    if (nq_hint <= 0 || nq_hint > 16) VS_SP(FILTER_BF16, 4);
+  }
+#undef VS_SP
   return hipGetLastError();
 }
 int skinny_plane_max_queries() { return kPlaneQ; }
