@@ -902,3 +902,27 @@ def test_small_batches_through_the_filter_planes(vf, metric, monkeypatch):
         monkeypatch.setenv("VS_SMALL_FILTER", "0")
         D0, I0 = index.search(xq, 10)
         assert not flat.mismatches(D0, I0, Dr, Ir, metric, xb, xq), nq
+
+
+def test_l2_small_calls_use_faiss_sequential_formula(vf):
+    """faiss's IndexFlatL2 takes its sequential branch (dis = sum (x - y)^2) for
+    calls of fewer than 20 queries and its BLAS branch (|x|^2 + |y|^2 - 2 x.y,
+    clamped at 0) from 20 on.  A query equal to a stored row
+    is at distance exactly 0 on the sequential branch; calls of 1, 5 and 19
+    queries keep that (the exact GEMV), and every distance is the direct sum's
+    value within the fp32 contract; a call of 32 queries is checked at the
+    same tolerance (the BLAS formula's roundings, the filter engine's keys)."""
+    rng = np.random.default_rng(77)
+    d = 128
+    xb = rng.uniform(-1, 1, (300_000, d)).astype(np.float32)
+    index = vf.IndexFlatL2(d)
+    index.add(xb)
+    for nq in (1, 5, 19, 32):
+        src = rng.choice(xb.shape[0], nq, replace=False)
+        xq = xb[src].copy()
+        D, I = index.search(xq, 5)
+        Dr, Ir = flat.knn_exact(xb, xq, 5, flat.METRIC_L2)
+        assert not flat.mismatches(D, I, Dr, Ir, flat.METRIC_L2, xb, xq), nq
+        assert (I[:, 0] == src).all(), nq
+        if nq < 20:
+            assert (D[:, 0] == 0.0).all(), (nq, D[:, 0])
