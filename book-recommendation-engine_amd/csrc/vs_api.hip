@@ -848,6 +848,14 @@ bool small_filter_on() {
   const char* e = getenv("VS_SMALL_FILTER");
   return !e || atoi(e) != 0;
 }
+// L2 calls of fewer than 20 queries (faiss's sequential formula: the
+// verification rescored with MODE_L2D) through the planes too (env
+// VS_SMALL_L2D=0 keeps them on the exact GEMV, for A/B)
+bool small_l2d_ok(int mode, const SearchArgs& a) {
+  if (!(mode == MODE_L2 && a.l2_direct)) return true;
+  const char* e = getenv("VS_SMALL_L2D");
+  return !e || atoi(e) != 0;
+}
 
 // The deep stage's small-count kernel (env VS_SKINNY_DEEP=0 turns it off,
 // for A/B; read at every search).
@@ -946,6 +954,10 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const bool aug = mode == MODE_L2 && idx->l2aug();
   if (aug && (idx->aug_m <= 0 || self_rows)) return fail(VS_E_INVALID, "vs: int8 L2 plane");
   const int kmode = aug ? MODE_IP : mode;  // the pass's own metric
+  // the verification's exact keys: an L2 call of fewer than 20 queries takes
+  // faiss's sequential formula (the rounded exact sum of (x - q)^2), larger
+  // ones its BLAS formula
+  const int vmode = mode == MODE_L2 && a.l2_direct ? MODE_L2D : mode;
   const int64_t pb = idx->planebytes(plane);
   const char* QH = nullptr;
   const float* qs = nullptr;    // int8: query scales
@@ -1124,7 +1136,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(scr.alloc((void**)&qcount, 2 * sizeof(int)), "vs: scratch");
   const float* qinv = mode == MODE_COS ? qaux : nullptr;
   const float* xinv = mode == MODE_COS ? a.xaux : nullptr;
-  VS_HIP(launch_verify_rescore(mode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
+  VS_HIP(launch_verify_rescore(vmode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
                                Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
                                st, qinv, xinv, qr2, gc, x.qcut),
          "vs: verify");
@@ -1135,14 +1147,14 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, gathered ? nullptr : dst + 0, st),
          "vs: flags");
   if (wide_enabled())
-    VS_HIP(launch_verify_wide(mode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
+    VS_HIP(launch_verify_wide(vmode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
                               idx->norms, Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
                               vp.KP, flags, st, qinv, xinv, qr2, Dk, Ik, dst + 4, x.qcut),
            "vs: verify wide");
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, last_plane ? dst + 2 : dst + 3,
                               nullptr, st),
          "vs: flags");
-  VS_HIP(launch_merge_partials(mode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
+  VS_HIP(launch_merge_partials(vmode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
                                a.raw, gl, gc),
          "vs: merge");
   // what is still flagged (usually nothing: every tile exits), as query ids of `a`
@@ -1246,13 +1258,14 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
     VS_HIP(launch_merge_partials(MODE_L2, skinny ? sp : part, skinny ? a.nq : cap, KF, 0, 0.0f, Dk,
                                  Ik, KF, st, 0, nullptr, wc),
            "vs: merge");
-    VS_HIP(launch_verify_rescore(a.mode, cap, KF, need, Dk, Ik, (const float*)idx->codes,
+    VS_HIP(launch_verify_rescore(a.mode == MODE_L2 && a.l2_direct ? MODE_L2D : a.mode, cap, KF,
+                                 need, Dk, Ik, (const float*)idx->codes,
                                  idx->norms, qc, ac, idx->ld, make_bound_args(idx->ld, plane),
                                  idx->bstats[plane], skinny ? sp : part, KP, vp.key, vp.id, vp.KP, flags, st,
                                  qinv, xinv, nullptr, wc),
            "vs: rescore");
-    VS_HIP(launch_merge_partials(a.mode, vp, cap, a.k, idx->id_base, a.min_score, a.D, a.I, a.k,
-                                 st, a.raw, wl, wc),
+    VS_HIP(launch_merge_partials(a.mode == MODE_L2 && a.l2_direct ? MODE_L2D : a.mode, vp, cap,
+                                 a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st, a.raw, wl, wc),
            "vs: merge");
   }
   return VS_OK;
@@ -1485,7 +1498,7 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
   // rows (skinny kernels too) — instead of streaming the fp32 rows.
   if (small_filter_on() && idx->esize == 4 && engine == VS_ENGINE_AUTO && KF > 0 && KF <= 32 &&
       nq <= kSkinnyMaxQ && a.self0 < 0 && ntotal >= kSmallFilterMinRows &&
-      (mode == MODE_IP || (mode == MODE_L2 && !a.l2_direct)) && (i8_ok || b16_ok)) {
+      (mode == MODE_IP || mode == MODE_L2) && (i8_ok || b16_ok) && small_l2d_ok(mode, a)) {
     if (i8_ok && b16_ok) i8_ok = adaptive_use_i8(idx);
     if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
     return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);

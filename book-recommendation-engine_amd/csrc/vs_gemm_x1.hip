@@ -2143,8 +2143,12 @@ __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, doubl
     const double u = ldexp(1.0, -24);
     double b = ba.gam * hx * hq + hx * rq + rx * hq + rx * rq;
     b *= 1.0 + 1e-6;
-    return (2.0 * b + 8.0 * u * (qn2 + ax2) + 2.0 * u * (qn2 + ba.aug_nref + 2.01 * hx * hq)) *
-           (1.0 + 1e-6);
+    double B = 2.0 * b + 8.0 * u * (qn2 + ax2) + 2.0 * u * (qn2 + ba.aug_nref + 2.01 * hx * hq);
+    // MODE_L2D (faiss's sequential formula, keys the rounded exact sum of
+    // (x - q)^2): the pass's keys follow the stored fp32 norms, each within
+    // norm_inf / 2 (relative) of the exact one, and the key's own rounding
+    if (mode == MODE_L2D) B += (ba.norm_inf + 4.0 * u) * (qn2 + ax2);
+    return B * (1.0 + 1e-6);
   }
   const double xm = sqrt((double)__uint_as_float(stats[0]) * (1.0 + ba.norm_inf));
   const double rx = sqrt((double)__uint_as_float(stats[1]));
@@ -2152,9 +2156,10 @@ __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, doubl
   const double hq = sqrt(qh2), rq = sqrt(qr2), qn = sqrt(qn2);
   double b = ba.gam * hx * hq + hx * rq + rx * hq + rx * rq + 2.0 * ldexp(1.0, -24) * xm * qn;
   b *= 1.0 + 1e-6;
-  if (mode == MODE_L2) {  // key = (|q|^2 + |x|^2) - 2 ip, every step rounded
+  if (mode == MODE_L2 || mode == MODE_L2D) {  // key = (|q|^2 + |x|^2) - 2 ip, every step rounded
     const double xm2 = (double)__uint_as_float(stats[0]);
     b = 2.0 * b + 8.0 * ldexp(1.0, -24) * (qn2 + xm2);
+    if (mode == MODE_L2D) b += (ba.norm_inf + 4.0 * ldexp(1.0, -24)) * (qn2 + xm2);
   } else if (mode == MODE_COS) {
     // keys -(s qinv xinv) with qinv, xinv from the stored norms (relative error
     // ~gam(ld) each, 1.5 norm_inf together); |s_a - s_e| / (|x||q|) <=
@@ -2203,17 +2208,25 @@ __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow
   }
 }
 
-// exact dot product of two fp32 rows (fp64 accumulation across the wave)
+// exact dot product of two fp32 rows (fp64 accumulation across the wave);
+// DIFF: the exact sum of (x - q)^2 instead (faiss's sequential L2 formula,
+// MODE_L2D: each difference of two floats is exact in fp64, its square too)
+template <bool DIFF = false>
 __device__ __forceinline__ double wave_dot(const float* __restrict__ x, const float* __restrict__ q,
                                            int64_t ld, int lane) {
   double acc = 0.0;
   for (int64_t c = lane * 4; c < ld; c += 256) {
     const f32x4 xv = *(const f32x4*)(x + c);
     const f32x4 qv = *(const f32x4*)(q + c);
-    acc = fma((double)xv.x, (double)qv.x, acc);
-    acc = fma((double)xv.y, (double)qv.y, acc);
-    acc = fma((double)xv.z, (double)qv.z, acc);
-    acc = fma((double)xv.w, (double)qv.w, acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if constexpr (DIFF) {
+        const double t = (double)xv[e] - (double)qv[e];
+        acc = fma(t, t, acc);
+      } else {
+        acc = fma((double)xv[e], (double)qv[e], acc);
+      }
+    }
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   return acc;
@@ -2235,6 +2248,7 @@ __device__ __forceinline__ void load_qslice(const float* __restrict__ q, int64_t
     qs.v[i] = c < ld ? *(const f32x4*)(q + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }
+template <bool DIFF = false>
 __device__ __forceinline__ void wave_dot2(const float* __restrict__ xa, const float* __restrict__ xb,
                                           const QSlice& qs, int64_t ld, int lane, double& ra,
                                           double& rb) {
@@ -2251,8 +2265,15 @@ __device__ __forceinline__ void wave_dot2(const float* __restrict__ xa, const fl
     if (lane * 4 + 256 * i >= ld) break;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      a = fma((double)va[i][e], (double)qs.v[i][e], a);
-      b = fma((double)vb[i][e], (double)qs.v[i][e], b);
+      if constexpr (DIFF) {
+        const double ta = (double)va[i][e] - (double)qs.v[i][e];
+        const double tb = (double)vb[i][e] - (double)qs.v[i][e];
+        a = fma(ta, ta, a);
+        b = fma(tb, tb, b);
+      } else {
+        a = fma((double)va[i][e], (double)qs.v[i][e], a);
+        b = fma((double)vb[i][e], (double)qs.v[i][e], b);
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -2270,6 +2291,7 @@ __device__ __forceinline__ float exact_key(float ip, int q, int r, const float* 
                                            const float* __restrict__ xinv) {
   return MODE == MODE_L2    ? l2_from_ip(qn[q], xn[r], ip)
          : MODE == MODE_COS ? -(ip * (qinv[q] * xinv[r]))
+         : MODE == MODE_L2D ? ip  // the rounded exact sum of (x - q)^2
                             : -ip;
 }
 
@@ -2334,7 +2356,8 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     for (int j = 0; j < KF; j += 2) {
       const int ra = sid[j], rb = j + 1 < KF ? sid[j + 1] : -1;
       double da, db;
-      wave_dot2(X + (int64_t)max(ra, 0) * ld, X + (int64_t)max(rb, 0) * ld, qsl, ld, lane, da, db);
+      wave_dot2<MODE == MODE_L2D>(X + (int64_t)max(ra, 0) * ld, X + (int64_t)max(rb, 0) * ld, qsl, ld,
+                                  lane, da, db);
       if (lane == 0) {
         ek[j] = ra < 0 ? FLT_MAX : exact_key<MODE>((float)da, q, ra, qn, xn, qinv, xinv);
         if (j + 1 < KF) ek[j + 1] = rb < 0 ? FLT_MAX : exact_key<MODE>((float)db, q, rb, qn, xn, qinv, xinv);
@@ -2347,7 +2370,7 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
         if (lane == 0) ek[j] = FLT_MAX;
         continue;
       }
-      const double acc = wave_dot(X + (int64_t)r * ld, qrow, ld, lane);
+      const double acc = wave_dot<MODE == MODE_L2D>(X + (int64_t)r * ld, qrow, ld, lane);
       if (lane == 0) ek[j] = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
     }
   }
@@ -2377,7 +2400,8 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
   }
   __syncthreads();
   const float eM = eMs;
-  const double bkey = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
+  const double bkey = bound_key(MODE, ba, qh2, qr2,
+                                MODE == MODE_L2 || MODE == MODE_L2D ? (double)qn[q] : qn2, stats);
   const bool pass = !bounded || ((double)T - bkey > (double)eM && isfinite(T) && isfinite(eM) &&
                                   isfinite(bkey));
   if (lane == 0) fail[q] = pass ? 0 : 1;
@@ -2407,6 +2431,8 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
     VS_VERIFY_NE(MODE_IP);
   else if (mode == MODE_L2)
     VS_VERIFY_NE(MODE_L2);
+  else if (mode == MODE_L2D)
+    VS_VERIFY_NE(MODE_L2D);
   else if (mode == MODE_COS && qinv && xinv)
     VS_VERIFY_NE(MODE_COS);
   else
@@ -2557,7 +2583,8 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
       T = fminf(T, qcut[q]);
     }
     const double bkey =
-        bound_key(MODE, ba, qs[0], qs[1], MODE == MODE_L2 ? (double)qn[q] : qs[2], stats);
+        bound_key(MODE, ba, qs[0], qs[1],
+                  MODE == MODE_L2 || MODE == MODE_L2D ? (double)qn[q] : qs[2], stats);
     // Any threshold T' <= T works (every row outside the set still has an
     // approximate key >= T'): with a_M the M-th smallest approximate key (the
     // merge's Dk), the M best-approximate rows have exact keys <= a_M + B, so
@@ -2626,14 +2653,15 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
         for (int j = wv; j < nu; j += 8) {
           const int ra = cid[j], rb = j + 4 < nu ? cid[j + 4] : ra;
           double da, db;
-          wave_dot2(X + (int64_t)ra * ld, X + (int64_t)rb * ld, qsl, ld, lane, da, db);
+          wave_dot2<MODE == MODE_L2D>(X + (int64_t)ra * ld, X + (int64_t)rb * ld, qsl, ld, lane, da,
+                                      db);
           put(j, ra, da);
           if (j + 4 < nu) put(j + 4, rb, db);
         }
       } else {
         for (int j = wv; j < nu; j += 4) {
           const int r = cid[j];
-          put(j, r, wave_dot(X + (int64_t)r * ld, qrow, ld, lane));
+          put(j, r, wave_dot<MODE == MODE_L2D>(X + (int64_t)r * ld, qrow, ld, lane));
         }
       }
       if (tid < nk) {  // the reused exact keys after the rescored ones
@@ -2693,6 +2721,8 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
     VS_WIDE(MODE_IP);
   else if (mode == MODE_L2)
     VS_WIDE(MODE_L2);
+  else if (mode == MODE_L2D)
+    VS_WIDE(MODE_L2D);
   else if (mode == MODE_COS && qinv && xinv)
     VS_WIDE(MODE_COS);
   else
@@ -2741,7 +2771,8 @@ __global__ __launch_bounds__(64) void qbound_kernel(const float* __restrict__ Q,
   double qh2, qr2, qn2;
   query_split_norms(Q + (int64_t)q * ld, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2,
                     ba.aug_q2);
-  double b = bound_key(MODE, ba, qh2, qr2, MODE == MODE_L2 ? (double)qn[q] : qn2, stats);
+  double b = bound_key(MODE, ba, qh2, qr2,
+                                MODE == MODE_L2 || MODE == MODE_L2D ? (double)qn[q] : qn2, stats);
   // the augmented L2 pass cuts its lists in the inner-product keys A, whose
   // map qn + 2A doubles distances: half the L2 bound there
   if (ba.l2aug) b *= 0.5;

@@ -876,7 +876,8 @@ def test_small_batches_through_the_filter_planes(vf, metric, monkeypatch):
     against the oracle, including queries beside 200 near-copies of their own
     direction that the int8 checks hand on, and the same labels as the exact
     streaming kernels (VS_SMALL_FILTER=0).  L2 calls of fewer than 20 queries
-    keep faiss's sequential formula (the exact GEMV)."""
+    keep faiss's sequential formula: their candidates are rescored as the
+    rounded exact sum of (x - q)^2 (MODE_L2D)."""
     rng = np.random.default_rng(321)
     d = 128
     xb = rng.uniform(-1, 1, (300_000, d)).astype(np.float32)
@@ -894,10 +895,9 @@ def test_small_batches_through_the_filter_planes(vf, metric, monkeypatch):
         monkeypatch.delenv("VS_SMALL_FILTER", raising=False)
         D, I = index.search(xq, 10)
         Dr, Ir = flat.knn_exact(xb, xq, 10, metric)
-        # (L2 under 20 queries: faiss's sequential formula, checked at the
-        # north star's tolerance like the other exact kernels)
-        strict = not (metric == flat.METRIC_L2 and nq < 20)
-        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=strict)
+        # (L2 under 20 queries: faiss's sequential formula, rescored as the
+        # rounded exact sum of (x - q)^2: strict as well)
+        bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
         assert not bad, (nq, bad[:5])
         monkeypatch.setenv("VS_SMALL_FILTER", "0")
         D0, I0 = index.search(xq, 10)
@@ -909,20 +909,27 @@ def test_l2_small_calls_use_faiss_sequential_formula(vf):
     calls of fewer than 20 queries and its BLAS branch (|x|^2 + |y|^2 - 2 x.y,
     clamped at 0) from 20 on.  A query equal to a stored row
     is at distance exactly 0 on the sequential branch; calls of 1, 5 and 19
-    queries keep that (the exact GEMV), and every distance is the direct sum's
-    value within the fp32 contract; a call of 32 queries is checked at the
-    same tolerance (the BLAS formula's roundings, the filter engine's keys)."""
+    queries keep that (the filter engine rescores them as the rounded exact
+    sum of (x - q)^2; with VS_SMALL_FILTER=0 the exact GEMV), and every
+    distance is the direct sum's value within the fp32 contract; a call of 32
+    queries is checked at the same tolerance (the BLAS formula's roundings)."""
     rng = np.random.default_rng(77)
     d = 128
     xb = rng.uniform(-1, 1, (300_000, d)).astype(np.float32)
     index = vf.IndexFlatL2(d)
     index.add(xb)
-    for nq in (1, 5, 19, 32):
-        src = rng.choice(xb.shape[0], nq, replace=False)
-        xq = xb[src].copy()
-        D, I = index.search(xq, 5)
-        Dr, Ir = flat.knn_exact(xb, xq, 5, flat.METRIC_L2)
-        assert not flat.mismatches(D, I, Dr, Ir, flat.METRIC_L2, xb, xq), nq
-        assert (I[:, 0] == src).all(), nq
-        if nq < 20:
-            assert (D[:, 0] == 0.0).all(), (nq, D[:, 0])
+    import os
+    for small in ("1", "0"):
+        os.environ["VS_SMALL_FILTER"] = small
+        try:
+            for nq in (1, 5, 19, 32):
+                src = rng.choice(xb.shape[0], nq, replace=False)
+                xq = xb[src].copy()
+                D, I = index.search(xq, 5)
+                Dr, Ir = flat.knn_exact(xb, xq, 5, flat.METRIC_L2)
+                assert not flat.mismatches(D, I, Dr, Ir, flat.METRIC_L2, xb, xq), (small, nq)
+                assert (I[:, 0] == src).all(), (small, nq)
+                if nq < 20:
+                    assert (D[:, 0] == 0.0).all(), (small, nq, D[:, 0])
+        finally:
+            del os.environ["VS_SMALL_FILTER"]
