@@ -1345,9 +1345,11 @@ static int x1_split_den() {
   return e ? std::max(0, atoi(e)) : kX1SplitDen;
 }
 constexpr int kSplitMinTiles = 16;
-static bool x1_quarter_on() {
+// (default: the bf16 plane's passes only — clustered C3 +1.4 %, C3's int8
+// pass -1 %, profiles/r05u)
+static bool x1_quarter_on(int el) {
   const char* e = getenv("VS_X1_QUARTER");
-  return e && atoi(e) != 0;
+  return e ? atoi(e) != 0 : el == FILTER_BF16;
 }
 
 template <int KR, int MODE, int EL>
@@ -1383,14 +1385,14 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   const bool hyb = dump && !split && x1_hybrid_on() && tiles0 >= kHybMinTiles;
   const bool later_dump = cutting || hyb;  // launches c > 0 are dump launches
   // the launches as part ranges [p0, p1) of nparts
-  // Quarter-chunk list launches (env VS_X1_QUARTER=1, A/B; off by default): a
+  // Quarter-chunk list launches (env VS_X1_QUARTER=0/1; default: bf16 passes): a
   // cutting pass of nchunk launches lists only parts [0, 1) of 4 nchunk, then a
   // dump launch over [1, 4) and one launch per chunk.  The list launch runs at
   // ~2/3 of a dump launch's rate (a k = 60 pass of 5 chunks spent 15 of its
   // 58 ms in it, profiles/r05t), but cuts set from a quarter of the rows are
   // looser: C3 dumps 1.7x the rows, 76.5k vs 77.4k queries/s; k = 60 equal,
   // clustered +1.4 % (profiles/r05u).
-  const bool quarter = cutting && !split && nchunk >= 4 && x1_quarter_on() &&
+  const bool quarter = cutting && !split && nchunk >= 4 && x1_quarter_on(EL) &&
                        per_block / (4 * nchunk) >= 2;
   const int nparts = split ? den : quarter ? 4 * nchunk : nchunk;
   const int nlaunch = split ? 2 : quarter ? nchunk + 1 : nchunk;
