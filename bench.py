@@ -650,10 +650,16 @@ def run_knn(args, ctx):
                   if kern1 > 0 else None}
         if kname1.startswith("skinny_plane"):
             # beside it, the exact stream over the stored rows (VS_SMALL_FILTER=0)
+            prev = os.environ.get("VS_SMALL_FILTER")
             os.environ["VS_SMALL_FILTER"] = "0"
-            t2, k2, n2, _ = ctx.timed(lambda i: index.search_device(q1, k, stream=ctx.stream),
-                                      args.batch1_steps, 3)
-            del os.environ["VS_SMALL_FILTER"]
+            try:
+                t2, k2, n2, _ = ctx.timed(lambda i: index.search_device(q1, k, stream=ctx.stream),
+                                          args.batch1_steps, 3)
+            finally:
+                if prev is None:
+                    del os.environ["VS_SMALL_FILTER"]
+                else:
+                    os.environ["VS_SMALL_FILTER"] = prev
             kern2 = k2 / max(1, n2) / 1e3
             batch1["exact_stream"] = {"ms_per_query": round(t2 / args.batch1_steps * 1e3, 4),
                                       "kernel": ctx.lib.timer_kernel(),
