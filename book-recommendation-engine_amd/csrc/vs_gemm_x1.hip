@@ -1347,9 +1347,13 @@ static int x1_split_den() {
 constexpr int kSplitMinTiles = 16;
 // (default: the bf16 plane's passes only — clustered C3 +1.4 %, C3's int8
 // pass -1 %, profiles/r05u)
-static bool x1_quarter_on(int el) {
+// VS_X1_QUARTER=<F>: the list launch covers 1/F of the first chunk (0: off,
+// 1: 1/4 as F = 4)
+static int x1_first_den(int el) {
   const char* e = getenv("VS_X1_QUARTER");
-  return e ? atoi(e) != 0 : el == FILTER_BF16;
+  if (!e) return el == FILTER_BF16 ? 4 : 0;
+  const int v = atoi(e);
+  return v == 1 ? 4 : v >= 2 ? v : 0;
 }
 
 template <int KR, int MODE, int EL>
@@ -1392,15 +1396,15 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // 58 ms in it, profiles/r05t), but cuts set from a quarter of the rows are
   // looser: C3 dumps 1.7x the rows, 76.5k vs 77.4k queries/s; k = 60 equal,
   // clustered +1.4 % (profiles/r05u).
-  const bool quarter = cutting && !split && nchunk >= 4 && x1_quarter_on(EL) &&
-                       per_block / (4 * nchunk) >= 2;
-  const int nparts = split ? den : quarter ? 4 * nchunk : nchunk;
+  const int F = x1_first_den(EL);
+  const bool quarter = cutting && !split && nchunk >= 4 && F >= 2 && per_block / (F * nchunk) >= 2;
+  const int nparts = split ? den : quarter ? F * nchunk : nchunk;
   const int nlaunch = split ? 2 : quarter ? nchunk + 1 : nchunk;
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nlaunch; ++c) {
-    const int p0 = split ? (c == 0 ? 0 : 1) : quarter ? (c == 0 ? 0 : c == 1 ? 1 : 4 * (c - 1)) : c;
-    const int p1 = split ? (c == 0 ? 1 : den) : quarter ? (c == 0 ? 1 : 4 * c) : c + 1;
+    const int p0 = split ? (c == 0 ? 0 : 1) : quarter ? (c == 0 ? 0 : c == 1 ? 1 : F * (c - 1)) : c;
+    const int p1 = split ? (c == 0 ? 1 : den) : quarter ? (c == 0 ? 1 : F * c) : c + 1;
     // the timed span of this launch alone (the cut and replay kernels between
     // launches stay outside the spans); the first launch of a pass whose later
     // launches dump is timed apart ("<name>_list")
