@@ -157,6 +157,14 @@ def parse(argv=None):
                         "k = 60) for the wide-k leg, comma-separated")
     p.add_argument("--wide-k-batch", type=int, default=4096)
     p.add_argument("--wide-k-steps", type=int, default=3)
+    p.add_argument("--any-k", type=int, default=100,
+                   help="k of the any-k leg (the agent-chosen k of search_catalog, "
+                        "mcp_book_server.py:115,142): batch 1 and the full batch through "
+                        "the paged exact engine; 0 skips it")
+    p.add_argument("--clustered-steps", type=int, default=3,
+                   help="C3 on one GPU: after the headline, the same search over unit-norm "
+                        "clustered rows (text-embedding-like, --data clustered) timed for "
+                        "this many steps as the `clustered` record; 0 skips it")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=1024)
@@ -682,8 +690,14 @@ def run_knn(args, ctx):
             ctx.lib.filter_stats(reset=True)
             tw, kmw, nw, (Dw, Iw) = ctx.timed(
                 lambda i: index.search_device(qw, kw, stream=ctx.stream), args.wide_k_steps, 1)
-            wmi, wni = ctx.lib.timer_read_kernel("gemm_topk_x1_i8")
-            wmp, _ = ctx.lib.timer_read_kernel("gemm_topk_x1_i8_pass")
+            # the plane the searches' first pass ran on (the adaptive order may
+            # start on bf16) and that pass's dump launches and whole-pass spans
+            wk = ctx.lib.timer_kernel()
+            if is_x1(wk):
+                wk, _, wmi, wni, wsplit = x1_dominant(ctx, 0.0, kmw, nw)
+                wmp = wsplit["whole_pass"][1]
+            else:
+                wmi, wni, wmp = kmw, nw, 0.0
             ww = ctx.lib.filter_wide_stats()
             w2 = ctx.lib.filter_second_stats()
             wwe, wwr = ctx.lib.filter_wide_sets()
@@ -692,7 +706,7 @@ def run_knn(args, ctx):
             wide.append({"k": kw, "batch": bw, "steps": args.wide_k_steps,
                          "ms_per_search": round(tw / args.wide_k_steps * 1e3, 3),
                          "queries_per_s": round(args.wide_k_steps * bw / tw, 1),
-                         "kernel": "gemm_topk_x1_i8",
+                         "kernel": wk,
                          "kernel_ms_per_dispatch": round(wmi / max(1, wni), 3),
                          "first_pass_ms_per_search": round(wmp / args.wide_k_steps, 3),
                          "filter_queries": wq, "wide_checked": ww,
@@ -700,6 +714,31 @@ def run_knn(args, ctx):
                          "wide_rescored_mean": round(wwr / ww, 1) if ww else 0.0,
                          "to_bf16_stage": w2, "exact_redo_queries": wf,
                          "result_sane": bool((Iwh >= 0).all() and (Iwh < args.ntotal).all())})
+
+    # Any k (faiss answers every k; the agent picks search_catalog's k,
+    # mcp_book_server.py:115,142): k past one 64-entry page runs the paged exact
+    # engine (vs_api.hip run_paged), at batch 1 (the live tool) and at the full
+    # batch.  Measured apart; not part of `value`.
+    anyk = None
+    if args.any_k > 0 and not gemv:
+        anyk = []
+        for bk, steps in ((1, 3), (B, 1)):
+            qk = xq[:bk].contiguous()
+            tk, kmk, nk, (Dk, Ik) = ctx.timed(
+                lambda i: index.search_device(qk, args.any_k, stream=ctx.stream), steps, 1)
+            Ikh, Dkh = Ik.cpu().numpy(), Dk.cpu().numpy()
+            ok = bool((Ikh >= 0).all() and (Ikh < args.ntotal).all())
+            ok &= bool((np.diff(Dkh, axis=1) <= 0).all() if metric == vfaiss.METRIC_INNER_PRODUCT
+                       else (np.diff(Dkh, axis=1) >= 0).all())
+            anyk.append({"k": args.any_k, "batch": bk, "steps": steps,
+                         "ms_per_search": round(tk / steps * 1e3, 3),
+                         "queries_per_s": round(steps * bk / tk, 1),
+                         "kernel": ctx.lib.timer_kernel(),
+                         "kernel_ms_per_search": round(kmk / steps, 3),
+                         "engine": "paged exact (vs_api.hip run_paged): ceil(k / 64) pages of "
+                                   "64 lexicographic entries, more where inner product's tie "
+                                   "rule needs them",
+                         "result_sane": ok})
 
     if ctx.rank == 0:
         cpu = None
@@ -726,10 +765,32 @@ def run_knn(args, ctx):
                                     "dump_launches": dump_record(*dmp)}
         res["batch1"] = batch1
         res["wide_k"] = wide
+        res["any_k"] = anyk
         res["cpu_baseline"] = cpu
+        # the filter planes the index kept (a memory shortage drops bf16, then
+        # both: the exact fp32 engine alone, an order of magnitude slower)
+        res["filter_planes"] = list(index.shard.filter_planes)
         res["result_sane"] = sane
         return res
     return None
+
+
+def clustered_record(res):
+    """The headline-shaped summary of a clustered run (run_knn with --data
+    clustered), for the `clustered` record beside the uniform headline."""
+    fv = res.get("filter_verify") or {}
+    rf = res.get("roofline") or {}
+    return {"value": res["value"], "unit": res["unit"], "ms_per_step": res["ms_per_step"],
+            "steps": res["steps"], "data": res["data"], "kernel": rf.get("kernel"),
+            "roofline": {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
+                                                 "kernel_ms_per_dispatch", "whole_pass")
+                         if k in rf},
+            "first_stage_planes": rf.get("first_stage_planes"),
+            "to_bf16_stage": fv.get("to_bf16_stage"),
+            "exact_redo_queries": fv.get("fallback_queries"),
+            "exact_check": fv.get("exact_check"),
+            "filter_planes": res.get("filter_planes"),
+            "result_sane": res.get("result_sane")}
 
 
 def run_selfjoin(args, ctx):
@@ -993,6 +1054,20 @@ def main():
         res = run_dry(args, ctx)
     elif args.workload in ("c3", "c2"):
         res = run_knn(args, ctx)
+        if (args.workload == "c3" and args.data == "uniform" and ctx.world == 1
+                and args.clustered_steps > 0 and args.dtype == "f32"):
+            # embedding-like rows beside the uniform headline (the headline's
+            # index is gone with run_knn's frame): same shape, same engine
+            import copy
+            import gc
+
+            gc.collect()
+            ca = copy.copy(args)
+            ca.data, ca.steps, ca.warmup = "clustered", args.clustered_steps, 1
+            ca.batch1_steps, ca.wide_k_steps, ca.any_k, ca.no_cpu_baseline = 0, 0, 0, True
+            cres = run_knn(ca, ctx)
+            if res is not None and cres is not None:
+                res["clustered"] = clustered_record(cres)
     elif args.workload == "c4":
         res = run_selfjoin(args, ctx)
     else:

@@ -66,6 +66,7 @@ struct vs_index {
   // rows stay in place, NaN-filled (no kernel admits them), until a pack; faiss
   // labels are positions among the live rows (searches map their rows through
   // the sorted dead list, launch_label_map).  ntotal counts the rows in place.
+  std::string notice;  // the last plane loss (vs_notice), empty if none
   std::vector<int64_t> dead;
   int64_t* ddead = nullptr;  // device copy of `dead`
   int64_t ddead_cap = 0;
@@ -393,7 +394,7 @@ const char* g_timer_kernel = "";
 // second filter stage, [4] wide-set entries, [5] of them rescored (the rest
 // reuse the first check's keys), [6] rows stored by dump launches (one
 // (row, raw sum) slot each), [7] lane lists out of dump slots.  One buffer per device.
-constexpr int kStatSlots = 8;
+constexpr int kStatSlots = 9;  // [8]: queries ranked by the exact-key stream
 std::mutex g_stats_mu;
 std::vector<unsigned long long*> g_dev_stats;
 
@@ -491,10 +492,21 @@ int engine_from_env() {
 // VS_FILTER=bf16 | i8 keeps only that plane (A/B).
 void planes_for(vs_index* idx) {
   const char* e = getenv("VS_FILTER");
+  if (e && strcmp(e, "none") == 0) {  // no planes: the exact fp32 engine alone
+    idx->plane_on[FILTER_BF16] = idx->plane_on[FILTER_I8] = false;
+    return;
+  }
   const bool f32 = idx->esize == 4;
   const bool i8able = f32 && (idx->metric == VS_METRIC_INNER_PRODUCT || idx->metric == VS_METRIC_L2);
   idx->plane_on[FILTER_BF16] = f32 && !(i8able && e && strcmp(e, "i8") == 0);
   idx->plane_on[FILTER_I8] = i8able && !(e && strcmp(e, "bf16") == 0);
+}
+
+// An L2 index without rows forgets its augmentation (vs_reset, or removals
+// down to ntotal = 0): the first add after it chooses m, C and nref again.
+void reset_l2aug(vs_index* idx) {
+  idx->aug_m = 0;
+  idx->aug = L2Aug{};
 }
 
 // The augmentation of an L2 index's int8 plane, fixed by its first add (rows
@@ -537,12 +549,22 @@ const float* plane_norms(const vs_index* idx, int p) {
 
 // The filter plane and residual norms of fp32 rows [r0, r0+n) (after the rows
 // and their norms are in place).
-int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st) {
+int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st, bool appended = false) {
   if (idx->esize != 4 || n <= 0) return VS_OK;
   for (int p = 0; p < 2; ++p) {
     if (!idx->plane_on[p] || idx->bstats[p]) continue;
     VS_HIP(hipMalloc(&idx->bstats[p], 4 * sizeof(unsigned)), "vs: bound maxima");
     VS_HIP(hipMemsetAsync(idx->bstats[p], 0, 4 * sizeof(unsigned), st), "vs: bound maxima");
+  }
+  // An add that at least doubles an L2 index re-derives its augmentation over
+  // every row (a few first rows would otherwise fix m, C and nref for good, and
+  // rows of other norms get coarse codes and a wide bound); amortised O(1) per
+  // row, like the storage's own growth.
+  if (appended && idx->l2aug() && idx->aug_m > 0 && r0 > 0 && n >= r0) {
+    reset_l2aug(idx);
+    for (int p = 0; p < 2; ++p)
+      if (idx->bstats[p])
+        VS_HIP(hipMemsetAsync(idx->bstats[p], 0, 4 * sizeof(unsigned), st), "vs: bound maxima");
   }
   if (idx->l2aug() && idx->aug_m == 0 && (idx->plane_on[FILTER_I8] || idx->plane_on[FILTER_BF16])) {
     // the first rows fix the augmentation (and the int8 plane's width)
@@ -619,10 +641,18 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
     anorm = nullptr;
     anorm_b = nullptr;
   };
+  // test hook (tests/test_gpu_planes.py): VS_TEST_PLANE_OOM=1 fails the bf16
+  // plane's allocation as a full HBM would, 2 every plane's
+  static const int plane_oom = [] {
+    const char* v = getenv("VS_TEST_PLANE_OOM");
+    return v ? atoi(v) : 0;
+  }();
   auto allocate = [&](int64_t c) -> hipError_t {
     hipError_t e = hipMalloc(&codes, (size_t)c * idx->rowbytes());
     if (e == hipSuccess) e = hipMalloc(&norms, (size_t)c * sizeof(float));
     for (int p = 0; p < 2; ++p) {
+      if (e == hipSuccess && on[p] && (plane_oom >= 2 || (plane_oom == 1 && p == FILTER_BF16)))
+        e = hipErrorOutOfMemory;
       if (e == hipSuccess && on[p]) e = hipMalloc(&fplane[p], (size_t)c * idx->planebytes(p));
       if (e == hipSuccess && on[p]) e = hipMalloc(&rn2[p], (size_t)c * sizeof(float));
     }
@@ -721,6 +751,19 @@ int ensure_capacity(vs_index* idx, int64_t rows, hipStream_t st) {
   VS_HIP(hipStreamSynchronize(st), "vs: storage growth");
   VS_HIP(wait_readers(idx), "vs: storage growth");
   free_storage(idx);
+  if (on[0] != idx->plane_on[0] || on[1] != idx->plane_on[1]) {
+    // a plane lost to a memory shortage: said once on stderr and kept for
+    // vs_notice (searches stay exact; the engines that remain are slower)
+    char buf[256];
+    snprintf(buf, sizeof(buf),
+             "vsearch: HBM short at %lld rows: filter planes dropped (int8 %s, bf16 %s); "
+             "searches use %s",
+             (long long)cap, on[FILTER_I8] ? "kept" : "dropped",
+             on[FILTER_BF16] ? "kept" : "dropped",
+             on[FILTER_I8] || on[FILTER_BF16] ? "the remaining plane" : "the exact fp32 engine");
+    idx->notice = buf;
+    fprintf(stderr, "%s\n", buf);
+  }
   idx->plane_on[0] = on[0];
   idx->plane_on[1] = on[1];
   idx->codes = codes;
@@ -809,8 +852,8 @@ int run_gemm(vs_index* idx, const SearchArgs& a, int need, hipStream_t st,
 }
 
 int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st);
-int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl = nullptr,
-               const int* gc = nullptr);
+int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl = nullptr,
+              const int* gc = nullptr);
 int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
                       hipStream_t st, const int* gl, const int* gc);
 
@@ -1182,12 +1225,20 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
 // sums, one rounding), so every key the staged engine returns is the fp32
 // rounding of the exact score (oracle/flat.py key_window).  The check verify
 // computes is not used here: this is the last stage.
+// Slots of the exact-key stream per launch (its lists: kExactSlots x up to
+// 256 row blocks x KP entries); launches past the device-side count exit.
+constexpr int kExactSlots = 256;
+bool exact_stream_on() {
+  const char* e = getenv("VS_EXACT_STREAM");
+  return !e || atoi(e) != 0;
+}
+
 int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
                       hipStream_t st, const int* gl, const int* gc) {
   // more than the 64 entries one exact page holds (inner product, k > 32): the
   // two-page exact engine over the gathered queries (its keys are the fp32
   // engine's own, as in a search that never went through the filter)
-  if (KF > 64) return run_wide_k(idx, a, st, gl, gc);
+  if (KF > 64) return run_paged(idx, a, st, gl, gc);
   const int ntotal = (int)idx->ntotal;
   const int KP = kp_for(KF);
   const int nslot = (int)round_up(a.nq, kBQ);
@@ -1227,6 +1278,31 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
   const float* Qa = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
   const float* qinv = a.mode == MODE_COS ? ac : nullptr;
   const float* xinv = a.mode == MODE_COS ? a.xaux : nullptr;
+  const int emode = a.mode == MODE_L2 && a.l2_direct ? MODE_L2D : a.mode;
+  // The candidates are proven with the fp32 GEMM's own error bound (no plane
+  // residuals: BoundArgs::rows_exact); a query it cannot settle (more than
+  // KF - k rows inside the bound of its k-th: dense near-ties) is ranked over
+  // every row by its exact key instead (vs_exact.hip; env VS_EXACT_STREAM=0
+  // keeps the fp32 candidates, for A/B), so every answer of the staged engine
+  // is the exact top-k of the rescored keys.
+  BoundArgs ba = make_bound_args(idx->ld, FILTER_BF16);
+  ba.rows_exact = 1;
+  const bool stream_ok = exact_stream_on() && exact_stream_nq(idx->ld) > 0 && KP <= 64;
+  unsigned long long* dstats = device_stats(idx->device);
+  int *fl = nullptr, *fc = nullptr, *ol = nullptr, *ewc = nullptr;
+  Partials ep;
+  if (stream_ok) {
+    VS_HIP(scr.alloc((void**)&fl, (size_t)cap * sizeof(int)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&fc, sizeof(int)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&ol, (size_t)cap * sizeof(int)), "vs: scratch");
+    VS_HIP(scr.alloc((void**)&ewc, sizeof(int)), "vs: scratch");
+    ep.KP = kp_for(need);
+    ep.P = (int)std::min<int64_t>(256, std::max<int64_t>(1, ((int64_t)ntotal + 1023) / 1024));
+    VS_HIP(scr.alloc((void**)&ep.key, (size_t)kExactSlots * ep.P * ep.KP * sizeof(float)),
+           "vs: scratch");
+    VS_HIP(scr.alloc((void**)&ep.id, (size_t)kExactSlots * ep.P * ep.KP * sizeof(int)),
+           "vs: scratch");
+  }
   // A small batch (its flagged queries are at most its a.nq <= kSkinnyMaxQ):
   // the skinny fp32 kernel streams the rows once over the gathered queries
   // (slots past the device-side count score garbage that no merge reads)
@@ -1258,15 +1334,39 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
     VS_HIP(launch_merge_partials(MODE_L2, skinny ? sp : part, skinny ? a.nq : cap, KF, 0, 0.0f, Dk,
                                  Ik, KF, st, 0, nullptr, wc),
            "vs: merge");
-    VS_HIP(launch_verify_rescore(a.mode == MODE_L2 && a.l2_direct ? MODE_L2D : a.mode, cap, KF,
-                                 need, Dk, Ik, (const float*)idx->codes,
-                                 idx->norms, qc, ac, idx->ld, make_bound_args(idx->ld, plane),
-                                 idx->bstats[plane], skinny ? sp : part, KP, vp.key, vp.id, vp.KP, flags, st,
-                                 qinv, xinv, nullptr, wc),
+    VS_HIP(launch_verify_rescore(emode, cap, KF, need, Dk, Ik, (const float*)idx->codes,
+                                 idx->norms, qc, ac, idx->ld, ba, idx->bstats[plane],
+                                 skinny ? sp : part, KP, vp.key, vp.id, vp.KP, flags, st, qinv,
+                                 xinv, nullptr, wc),
            "vs: rescore");
-    VS_HIP(launch_merge_partials(a.mode == MODE_L2 && a.l2_direct ? MODE_L2D : a.mode, vp, cap,
-                                 a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st, a.raw, wl, wc),
+    VS_HIP(launch_merge_partials(emode, vp, cap, a.k, idx->id_base, a.min_score, a.D, a.I, a.k,
+                                 st, a.raw, wl, wc),
            "vs: merge");
+    if (!stream_ok) continue;
+    // the queries the fp32 bound leaves open: every row ranked by its exact key
+    VS_HIP(launch_compact_flags(flags, cap, fl, fc, dstats ? dstats + 8 : nullptr, nullptr, st),
+           "vs: exact stream");
+    VS_HIP(launch_compose_list(wl, fl, fc, cap, ol, st), "vs: exact stream");
+    ExactStreamArgs ea;
+    ea.X = (const float*)idx->codes;
+    ea.xn = idx->norms;
+    ea.xinv = xinv;
+    ea.ld = idx->ld;
+    ea.ntotal = ntotal;
+    ea.Q = qc;
+    ea.qaux = ac;
+    ea.qrow = a.self0 >= 0 ? qrow : nullptr;
+    ea.slots = fl;
+    ea.count = fc;
+    ea.nslot = kExactSlots;
+    for (int s0 = 0; s0 < cap; s0 += kExactSlots) {
+      ea.s0 = s0;
+      VS_HIP(launch_window_count(fc, s0, kExactSlots, ewc, st), "vs: exact stream");
+      VS_HIP(launch_exact_stream(ep.KP, emode, ea, ep, st), "vs: exact stream");
+      VS_HIP(launch_merge_partials(emode, ep, kExactSlots, a.k, idx->id_base, a.min_score, a.D,
+                                   a.I, a.k, st, a.raw, ol + s0, ewc),
+             "vs: merge");
+    }
   }
   return VS_OK;
 }
@@ -1336,102 +1436,141 @@ int adaptive_record(vs_index* idx, const int* handed, int n, hipStream_t st) {
   return VS_OK;
 }
 
-// Inner-product searches whose answer needs more than the 64 entries a list
-// holds: faiss's tie rule with k > 32 (it reads the 2k-1 best (key, label)
-// entries; service.py:529-531 oversamples to k = 60) and raw searches with
-// 64 < k <= 128 (a shard's half of a sharded k > 32 search).  Two pages:
-//  1. the lexicographic top-64 of every query (the exact engine, raw order);
-//  2. for the queries that may need more (page_check: the k-th key's run of
-//     equal keys reaches entry 63; raw: the page is full), the next 64 entries,
-//     by the same kernel with the list admission floored at entry 63 (so every
-//     row's key is the same instructions' result in both pages), gathered;
-//  3. page_finish: the pages concatenated, faiss's rule, the k outputs.
-// The small-batch GEMV serves one or two fp32 queries (the k = 60 single query);
-// everything else runs the fp32 / bf16 MFMA GEMM.
+// The paged exact engine: any k, every metric, for what one 64-entry list
+// cannot answer — k > 64, raw (shard) lists past 64, and faiss's inner-product
+// tie rule past k = 32 (it reads the k-th key's run of equal keys up to 2k - 1
+// entries; service.py:529-531 oversamples to k = 60, and the live tool's k is
+// the agent's, mcp_book_server.py:115,142).  faiss's IndexFlat::search has no k
+// limit; neither has this.  A query's answer is read off its lexicographic
+// (key, row) order in pages of 64 entries:
+//  1. page 1: the exact kernel's top-64 (FLOOR form with the floor (-inf, -1));
+//  2. page_step: a query takes page p + 1 only while its answer needs it (fewer
+//     than k entries so far, or the rule's run of k-th key ties reaching the
+//     page's end below 2k - 1) and its page came back full; page p + 1 = the
+//     same kernel with the admission floored at page p's last entry, over the
+//     queries that need it (gathered on the device; launches past the count
+//     exit at once), so every row's key is the same instructions' result in
+//     every page;
+//  3. page_finish: the pages side by side, faiss's rule (unless raw or not
+//     inner product), the k outputs (empty past the rows there are).
+// Kernels: the fp32 GEMV for one or two fp32 inner-product queries and for
+// faiss's sequential L2 branch (calls under 20 queries, groups of up to 8);
+// everything else the fp32 / bf16 MFMA GEMM (self-joins included).  Query
+// windows keep the pages within ~2 GB whatever k and the batch.
 // gl / gc: a gathered batch, queries gl[0 .. *gc) of `a` (the staged engine's
-// last stage for k > 32; device-side count), whose rows alone are written.
-int run_wide_k(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl, const int* gc) {
-  const int nq = a.nq;
+// last stage for inner product k > 32; device-side count), whose rows alone
+// are written.
+int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl, const int* gc) {
   const bool gathered = gl != nullptr;
   const int ntotal = (int)idx->ntotal;
-  Scratch scr(st);
-  float *D1 = nullptr, *D2 = nullptr, *fkey = nullptr;
-  int64_t *I1 = nullptr, *I2 = nullptr;
-  int *fid = nullptr, *flags = nullptr, *qlist = nullptr, *qcount = nullptr;
-  const int nslot = (int)round_up(nq, kBQ);
-  VS_HIP(scr.alloc((void**)&D1, (size_t)nq * 64 * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&I1, (size_t)nq * 64 * sizeof(int64_t)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&D2, (size_t)nq * 64 * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&I2, (size_t)nq * 64 * sizeof(int64_t)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&fkey, (size_t)nq * sizeof(float)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&fid, (size_t)nq * sizeof(int)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&flags, (size_t)nq * sizeof(int)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&qlist, (size_t)nslot * sizeof(int)), "vs: scratch");
-  VS_HIP(scr.alloc((void**)&qcount, sizeof(int)), "vs: scratch");
+  const bool rule = a.mode == MODE_IP && !a.raw;
+  const int64_t need = rule ? 2 * (int64_t)a.k - 1 : (int64_t)a.k;
+  // entries past the rows in place never exist: the last page is never needed
+  const int64_t npages = std::max<int64_t>(1, (std::min<int64_t>(need, ntotal) + 63) / 64);
+  const int64_t KA = npages * 64;
   const bool gemv_fits =
       (size_t)kGemvMaxQ * idx->ld * sizeof(float) + 4 * kGemvMaxQ * 64 * 8 <= 64 * 1024;
-  const bool gemv = !gathered && a.self0 < 0 && nq <= 2 && idx->esize == 4 && gemv_fits;
-  Partials gp;  // GEMV lists (both pages)
-  gp.KP = 64;
+  const bool l2d = a.mode == MODE_L2 && a.l2_direct && idx->esize == 4 && gemv_fits && a.self0 < 0;
+  const bool gemv = !gathered && a.self0 < 0 && idx->esize == 4 && gemv_fits &&
+                    (l2d || (a.mode == MODE_IP && a.nq <= 2));
+  const int pmode = l2d ? MODE_L2D : a.mode;
+  // query windows: GEMV groups of up to 8, else pages of at most ~2 GB
+  int64_t W = a.nq;
   if (gemv) {
-    const int nblocks = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (idx->ntotal + 255) / 256));
-    gp.P = nblocks;
-    const size_t n = (size_t)nq * gp.P * gp.KP;
-    VS_HIP(scr.alloc((void**)&gp.key, n * sizeof(float)), "vs: scratch");
-    VS_HIP(scr.alloc((void**)&gp.id, n * sizeof(int)), "vs: scratch");
-    KernelTimer tm(st, "gemv_topk");
-    VS_HIP(launch_gemv_topk(64, MODE_IP, nq, idx->codes, idx->esize, a.qbuf, idx->ld, ntotal,
-                            nblocks, gp, st),
-           "vs: gemv_topk launch");
-    tm.stop();
-    VS_HIP(launch_merge_partials(MODE_IP, gp, nq, 64, idx->id_base, a.min_score, D1, I1, 64, st, 1),
-           "vs: merge launch");
-  } else {
-    SearchArgs p1 = a;
-    p1.k = 64;
-    p1.raw = 1;
-    p1.D = D1;
-    p1.I = I1;
-    const int rc = run_gemm(idx, p1, 64, st, gl, gc);
-    if (rc) return rc;
+    W = kGemvMaxQ;
+  } else if (!gathered) {
+    W = std::max<int64_t>(kBQ, ((int64_t)2 << 30) / (KA * 12) / kBQ * kBQ);
   }
-  if (gathered)  // only the gathered queries' rows of D1 exist
-    VS_HIP(hipMemsetAsync(flags, 0, (size_t)nq * sizeof(int), st), "vs: page check");
-  VS_HIP(launch_page_check(D1, I1, nq, a.k, a.raw, idx->id_base, fkey, fid, flags, st, gl, gc),
-         "vs: page check");
-  VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, nullptr, nullptr, st), "vs: flags");
-  if (gemv) {  // every block exits at once when no query needs the second page
-    VS_HIP(launch_gemv_topk(64, MODE_IP, nq, idx->codes, idx->esize, a.qbuf, idx->ld, ntotal, gp.P,
-                            gp, st, fkey, fid, qcount),
-           "vs: gemv_topk launch");
-    VS_HIP(launch_merge_partials(MODE_IP, gp, nq, 64, idx->id_base, a.min_score, D2, I2, 64, st, 1),
-           "vs: merge launch");
+  const int64_t nw_max = std::min<int64_t>(W, a.nq);
+  const int64_t nrow = gathered ? a.nq_pad : round_up(std::max<int64_t>(nw_max, kGemvMaxQ), kBQ);
+  Scratch scr(st);
+  float* Dacc = nullptr;
+  int64_t* Iacc = nullptr;
+  float* fkey = nullptr;
+  int *fid = nullptr, *member = nullptr, *active = nullptr, *qlist = nullptr, *qcount = nullptr;
+  VS_HIP(scr.alloc((void**)&Dacc, (size_t)nrow * KA * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&Iacc, (size_t)nrow * KA * sizeof(int64_t)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&fkey, (size_t)nrow * sizeof(float)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&fid, (size_t)nrow * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&member, (size_t)nrow * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&active, (size_t)nrow * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qlist, (size_t)nrow * sizeof(int)), "vs: scratch");
+  VS_HIP(scr.alloc((void**)&qcount, sizeof(int)), "vs: scratch");
+  // the page kernels' partial lists
+  Partials part;
+  part.KP = 64;
+  int nsplit = 1, cap = 0;
+  int* wc = nullptr;
+  if (gemv) {
+    part.P = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (ntotal + 255) / 256));
+    VS_HIP(scr.alloc((void**)&part.key, (size_t)kGemvMaxQ * part.P * 64 * sizeof(float)),
+           "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, (size_t)kGemvMaxQ * part.P * 64 * sizeof(int)),
+           "vs: scratch");
+    VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
   } else {
-    // the flagged queries, gathered, in slot windows of lists of at most ~1 GB
-    Partials part;
-    part.KP = 64;
     const int ntiles = (ntotal + kBN - 1) / kBN;
-    const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, 256));
+    nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, 256));
     part.P = 2 * nsplit;
-    const int cap = (int)std::min<int64_t>(
-        nslot, std::max<int64_t>(kBQ, ((int64_t)1 << 30) / ((int64_t)part.P * 64 * 8) / kBQ * kBQ));
+    // gathered slots run in windows whose lists stay within ~1 GB
+    cap = (int)std::min<int64_t>(
+        nrow, std::max<int64_t>(kBQ, ((int64_t)1 << 30) / ((int64_t)part.P * 64 * 8) / kBQ * kBQ));
     VS_HIP(scr.alloc((void**)&part.key, (size_t)cap * part.P * 64 * sizeof(float)), "vs: scratch");
     VS_HIP(scr.alloc((void**)&part.id, (size_t)cap * part.P * 64 * sizeof(int)), "vs: scratch");
-    int* wc = nullptr;
     VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
-    const void* qmat = a.qb16 ? a.qb16 : (const void*)a.qbuf;
-    for (int w0 = 0; w0 < nslot; w0 += cap) {
-      VS_HIP(launch_window_count(qcount, w0, cap, wc, st), "vs: window");
-      VS_HIP(launch_gemm_topk(64, MODE_IP, idx->codes, a.xaux, qmat, a.qaux, idx->ld, idx->esize,
-                              ntotal, cap, nsplit, -1, part, st, qlist + w0, wc, fkey, fid),
-             "vs: gemm_topk launch");
-      VS_HIP(launch_merge_partials(MODE_IP, part, cap, 64, idx->id_base, a.min_score, D2, I2, 64,
-                                   st, 1, qlist + w0, wc),
-             "vs: merge launch");
-    }
   }
-  VS_HIP(launch_page_finish(D1, I1, D2, I2, flags, nq, a.k, a.raw, a.D, a.I, st, gl, gc),
-         "vs: pages");
+  for (int64_t q0 = 0; q0 < a.nq; q0 += W) {
+    const int nw = (int)std::min<int64_t>(W, a.nq - q0);
+    const int nslot = (int)round_up(nw, kBQ);
+    // this window's queries (offsets into the staged rows / aux / outputs)
+    const int64_t eoff = q0 * idx->ld;
+    const float* qf = a.qbuf ? a.qbuf + eoff : nullptr;
+    const void* qmat = a.qb16 ? (const void*)((const uint16_t*)a.qb16 + eoff) : (const void*)qf;
+    const float* qaux = a.qaux ? a.qaux + q0 : nullptr;
+    const int64_t self0 = a.self0 >= 0 ? a.self0 + q0 : -1;
+    VS_HIP(hipMemsetAsync(Iacc, 0xFF, (size_t)nw * KA * sizeof(int64_t), st), "vs: pages");
+    if (gathered) {
+      VS_HIP(hipMemsetAsync(member, 0, (size_t)nw * sizeof(int), st), "vs: pages");
+      VS_HIP(hipMemsetAsync(active, 0, (size_t)nw * sizeof(int), st), "vs: pages");
+    }
+    VS_HIP(launch_page_init(nw, gemv ? kGemvMaxQ : nw, gl, gc, member, active, fkey, fid, st),
+           "vs: pages");
+    VS_HIP(launch_compact_flags(active, nw, qlist, qcount, nullptr, nullptr, st), "vs: pages");
+    for (int64_t p = 0; p < npages; ++p) {
+      if (p > 0) {
+        VS_HIP(launch_page_step(Dacc, Iacc, KA, (int)p - 1, nw, a.k, rule ? 1 : 0, pmode, active,
+                                fkey, fid, st),
+               "vs: pages");
+        VS_HIP(launch_compact_flags(active, nw, qlist, qcount, nullptr, nullptr, st), "vs: pages");
+      }
+      if (gemv) {  // every query's lists (finished ones empty); none: the launch exits
+        KernelTimer tm(st, p == 0 && !gathered ? "gemv_topk" : nullptr);
+        VS_HIP(launch_gemv_topk(64, pmode, nw, idx->codes, idx->esize, qf, idx->ld, ntotal, part.P,
+                                part, st, fkey, fid, qcount),
+               "vs: gemv_topk launch");
+        tm.stop();
+        VS_HIP(launch_page_gate(qcount, nw, wc, st), "vs: pages");
+        VS_HIP(launch_merge_partials(pmode, part, nw, 64, 0, -INFINITY, Dacc + p * 64,
+                                     Iacc + p * 64, KA, st, 1, nullptr, wc),
+               "vs: merge launch");
+        continue;
+      }
+      for (int w0 = 0; w0 < nslot; w0 += cap) {
+        VS_HIP(launch_window_count(qcount, w0, cap, wc, st), "vs: window");
+        KernelTimer tm(st, p == 0 && w0 == 0 && !gathered ? "gemm_topk" : nullptr);
+        VS_HIP(launch_gemm_topk(64, a.mode, idx->codes, a.xaux, qmat, qaux, idx->ld, idx->esize,
+                                ntotal, cap, nsplit, self0, part, st, qlist + w0, wc, fkey, fid),
+               "vs: gemm_topk launch");
+        tm.stop();
+        VS_HIP(launch_merge_partials(a.mode, part, cap, 64, 0, -INFINITY, Dacc + p * 64,
+                                     Iacc + p * 64, KA, st, 1, qlist + w0, wc),
+               "vs: merge launch");
+      }
+    }
+    VS_HIP(launch_page_finish(pmode, Dacc, Iacc, KA, nw, a.k, rule ? 1 : 0, member, idx->id_base,
+                              a.min_score, a.D + q0 * a.k, a.I + q0 * a.k, st),
+           "vs: pages");
+  }
   return VS_OK;
 }
 
@@ -1469,7 +1608,7 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
                       nq > kSkinnyMaxQ && (i8_ok || b16_ok);
   // more entries than one exact page holds (inner product k > 32, raw k > 64)
   // and no filter pass for them: the two-page exact engine
-  if (need > VS_MAX_K && !staged) return run_wide_k(idx, a, st);
+  if (need > VS_MAX_K && !staged) return run_paged(idx, a, st);
   const int KP = kp_for(need);
 
   // Small batches stream the corpus once.  fp32 L2 searches whose CALL has
@@ -1555,7 +1694,7 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
     if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
     if (b16_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);
   }
-  if (need > VS_MAX_K) return run_wide_k(idx, a, st);
+  if (need > VS_MAX_K) return run_paged(idx, a, st);
   // No plane serves this metric (the cosine self-join of an L2 index, whose
   // planes hold the rows augmented for L2): the staged engine's last stage over
   // every query — the exact fp32 GEMM, its candidates rescored in fp64 — so the
@@ -1671,7 +1810,12 @@ int vs_reserve(vs_index* idx, int64_t n) {
   // come before the next pack (1 / pack_den of the rows): at C5's size a
   // storage growth (a copy beside the old rows) does not fit in HBM
   const int64_t want = std::max(n, idx->ntotal);
-  return ensure_capacity(idx, idx->tombstones() ? want + want / pack_den() : want, nullptr);
+  if (idx->tombstones() && want / pack_den() > 0) {
+    // the headroom is a convenience: without room for it, the exact request
+    if (ensure_capacity(idx, want + want / pack_den(), nullptr) == VS_OK) return VS_OK;
+    (void)hipGetLastError();
+  }
+  return ensure_capacity(idx, want, nullptr);
 }
 
 int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
@@ -1711,7 +1855,7 @@ int vs_add(vs_index* idx, const float* x, int64_t n, int flags, void* stream) {
   }
   VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add: norms");
-  rc = derive_plane(idx, idx->ntotal, n, st);
+  rc = derive_plane(idx, idx->ntotal, n, st, true);
   if (rc) return rc;
   // Source host buffers may be released by the caller as soon as we return.
   VS_HIP(hipStreamSynchronize(st), "vs_add: synchronise");
@@ -1735,7 +1879,7 @@ int vs_add_synthetic(vs_index* idx, int64_t n, uint64_t seed, int64_t row0, void
          "vs_add_synthetic: fill");
   VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add_synthetic: norms");
-  rc = derive_plane(idx, idx->ntotal, n, st);
+  rc = derive_plane(idx, idx->ntotal, n, st, true);
   if (rc) return rc;
   VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic: synchronise");
   idx->ntotal += n;
@@ -1765,7 +1909,7 @@ int vs_add_synthetic_ids(vs_index* idx, const int64_t* ids, int64_t n, uint64_t 
          "vs_add_synthetic_ids: fill");
   VS_HIP(launch_row_norms(idx->codes, idx->esize, idx->ld, idx->ntotal, n, idx->norms, st),
          "vs_add_synthetic_ids: norms");
-  rc = derive_plane(idx, idx->ntotal, n, st);
+  rc = derive_plane(idx, idx->ntotal, n, st, true);
   if (rc) return rc;
   VS_HIP(hipStreamSynchronize(st), "vs_add_synthetic_ids: synchronise");
   idx->ntotal += n;
@@ -1782,6 +1926,11 @@ int vs_reset(vs_index* idx) {
     if (idx->bstats[p]) VS_HIP(hipMemset(idx->bstats[p], 0, 4 * sizeof(unsigned)), "vs_reset");
   idx->ntotal = 0;
   idx->dead.clear();
+  // an empty index starts over: the planes a memory shortage dropped come back
+  // (the next add allocates them with the rows), and the next add's rows fix a
+  // fresh L2 augmentation
+  planes_for(idx);
+  reset_l2aug(idx);
   return VS_OK;
 }
 
@@ -1824,6 +1973,8 @@ int vs_set_engine(vs_index* idx, int engine) {
   return VS_OK;
 }
 
+const char* vs_notice(const vs_index* idx) { return idx ? idx->notice.c_str() : ""; }
+
 int vs_filter_plane(const vs_index* idx, int* out) {
   if (!idx || !out) return fail(VS_E_INVALID, "vs_filter_plane: null argument");
   *out = (idx->plane_on[FILTER_I8] ? VS_FILTER_I8 : 0) |
@@ -1844,11 +1995,9 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
   if (!idx) return fail(VS_E_INVALID, "vs_search: null index");
   if (n < 0) return fail(VS_E_INVALID, "vs_search: n < 0");
   if (k <= 0) return fail(VS_E_INVALID, "vs_search: k must be > 0");  // faiss: FAISS_THROW_IF_NOT(k > 0)
-  // raw inner-product searches (a shard's half of a sharded k > 32 search) go to
-  // 2 * VS_MAX_K
-  if (k > VS_MAX_K && !(k <= 2 * VS_MAX_K && (flags & VS_RAW_ORDER) &&
-                        idx->metric == VS_METRIC_INNER_PRODUCT))
-    return fail(VS_E_UNSUPPORTED, "vs_search: k > VS_MAX_K (64) not supported");
+  // any k, as faiss-cpu's IndexFlat::search (k > 64: the paged exact engine,
+  // run_paged); the bound only keeps 2k - 1 inside the engines' int arithmetic
+  if (k > INT_MAX / 2) return fail(VS_E_INVALID, "vs_search: k too large");
   if (n == 0) return VS_OK;
   if (!x || !D || !I) return fail(VS_E_INVALID, "vs_search: null buffer");
   hipStream_t st = (hipStream_t)stream;
@@ -2213,6 +2362,9 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
       VS_HIP(hipStreamSynchronize(st), "vs_remove_ids: synchronise");
     }
   }
+  // every row removed: the next add's rows fix a fresh L2 augmentation (the
+  // old one followed rows that are gone)
+  if (idx->ntotal == 0) reset_l2aug(idx);
   if (nremoved) *nremoved = nrem;
   return VS_OK;
 }
@@ -2220,19 +2372,27 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
 int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_self,
                 float min_sim, float* D, int64_t* I, int flags, void* stream) {
   if (!idx) return fail(VS_E_INVALID, "vs_selfjoin: null index");
-  {  // the self-join reads its query rows in place: pack the tombstones first
-    std::unique_lock<std::shared_mutex> wl(idx->mu);
-    const int rc = pack_dead(idx);
-    if (rc) return rc;
-  }
   if (k <= 0) return fail(VS_E_INVALID, "vs_selfjoin: k must be > 0");
-  if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_selfjoin: k > VS_MAX_K (64) not supported yet");
-  if (q0 < 0 || nq < 0 || q0 + nq > idx->ntotal)
-    return fail(VS_E_INVALID, "vs_selfjoin: query rows out of range");
-  if (nq == 0) return VS_OK;
-  if (!D || !I) return fail(VS_E_INVALID, "vs_selfjoin: null buffer");
+  if (k > INT_MAX / 2) return fail(VS_E_INVALID, "vs_selfjoin: k too large");
+  if (q0 < 0 || nq < 0) return fail(VS_E_INVALID, "vs_selfjoin: query rows out of range");
+  if (nq > 0 && (!D || !I)) return fail(VS_E_INVALID, "vs_selfjoin: null buffer");
   hipStream_t st = (hipStream_t)stream;
+  // The self-join reads its query rows in place and emits row numbers as labels,
+  // so it runs on an index without tombstones: under the shared lock it checks
+  // for them, and if a removal left some, packs them under the unique lock and
+  // looks again (a removal can land between the two locks).
   std::shared_lock<std::shared_mutex> lk(idx->mu);
+  while (!idx->dead.empty()) {
+    lk.unlock();
+    {
+      std::unique_lock<std::shared_mutex> wl(idx->mu);
+      const int rc = pack_dead(idx);
+      if (rc) return rc;
+    }
+    lk.lock();
+  }
+  if (q0 + nq > idx->ntotal) return fail(VS_E_INVALID, "vs_selfjoin: query rows out of range");
+  if (nq == 0) return VS_OK;
   DeviceGuard g(idx->device);
   ReaderMark mark(idx, st);
   const bool out_dev = (flags & VS_OUT_DEVICE) != 0;
@@ -2283,9 +2443,8 @@ int vs_merge_topk(const float* D_parts, const int64_t* I_parts, int64_t nparts, 
                   int64_t k_in, int64_t k, int metric, float* D, int64_t* I, void* stream) {
   if (nparts < 1 || nq < 0 || k_in < 1 || k < 1)
     return fail(VS_E_INVALID, "vs_merge_topk: bad sizes");
-  if (k > VS_MAX_K) return fail(VS_E_UNSUPPORTED, "vs_merge_topk: k > VS_MAX_K");
-  if (k_in > 2 * VS_MAX_K || nparts > 64)
-    return fail(VS_E_UNSUPPORTED, "vs_merge_topk: k_in > 2 * VS_MAX_K or more than 64 parts");
+  if (k > INT_MAX / 2) return fail(VS_E_INVALID, "vs_merge_topk: k too large");
+  if (nparts > 64) return fail(VS_E_UNSUPPORTED, "vs_merge_topk: more than 64 parts");
   if (metric != VS_METRIC_L2 && metric != VS_METRIC_INNER_PRODUCT)
     return fail(VS_E_INVALID, "vs_merge_topk: bad metric");
   if (nq == 0) return VS_OK;
@@ -2368,6 +2527,15 @@ int vs_filter_second_stats(int64_t* second) {
   int rc = read_filter_stats(c, 0);
   if (rc) return rc;
   *second = (int64_t)c[3];
+  return VS_OK;
+}
+
+int vs_filter_exact_stats(int64_t* streamed) {
+  if (!streamed) return fail(VS_E_INVALID, "vs_filter_exact_stats: null output");
+  unsigned long long c[kStatSlots];
+  int rc = read_filter_stats(c, 0);
+  if (rc) return rc;
+  *streamed = (int64_t)c[8];
   return VS_OK;
 }
 

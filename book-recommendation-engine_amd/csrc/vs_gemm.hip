@@ -37,12 +37,12 @@ namespace vs {
 // (which share a database split and differ in query tile) are packed onto one XCD
 // so the 4 MiB L2 there serves each database tile to all query tiles in flight.
 //
-// FLOOR (inner product, KP = 64 only): the lists admit only entries that come
-// strictly after the query's floor (fkey[q], fid[q]) in (key, row) order — the
-// second page of a query's lexicographic order, which faiss's inner-product tie
-// rule reads for k > 32 (vs_api.hip run_wide_k).  The keys are the same
-// instructions' as without the floor, so a row's key is bit-identical in both
-// pages.
+// FLOOR (KP = 64 only, every metric): the lists admit only entries that come
+// strictly after the query's floor (fkey[q], fid[q]) in (key, row) order — page
+// p + 1 of a query's lexicographic order starts after page p's last entry
+// (vs_api.hip run_paged: any k, and faiss's inner-product tie rule, which reads
+// up to 2k - 1 entries).  Every page of a search runs this instantiation (page 1
+// with the floor (-inf, -1)), so a row's key is bit-identical in all pages.
 template <int KP, int MODE, typename T, bool FLOOR = false>
 __global__ __launch_bounds__(256, (KP >= 64 ? 1 : 2)) void gemm_topk(
     const T* __restrict__ X, const float* __restrict__ xaux, const T* __restrict__ Q,
@@ -295,10 +295,24 @@ hipError_t launch_gemm_topk(int KP, int mode, const void* X, const float* xaux, 
       (esize != 4 && esize != 2) || ((qlist == nullptr) != (qcount == nullptr)) ||
       ((fkey == nullptr) != (fid == nullptr)))
     return hipErrorInvalidValue;
-  if (fkey) {  // the second page of an inner-product search (64-entry lists)
-    if (KP != 64 || mode != MODE_IP) return hipErrorInvalidValue;
-    return gemm_dispatch_mode<64, MODE_IP, true>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
-                                                 nsplit, self0, part, st, qlist, qcount, fkey, fid);
+  if (fkey) {  // a page after a floor (the paged engine, 64-entry lists)
+    if (KP != 64) return hipErrorInvalidValue;
+    switch (mode) {
+      case MODE_IP:
+        return gemm_dispatch_mode<64, MODE_IP, true>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
+                                                     nsplit, self0, part, st, qlist, qcount, fkey,
+                                                     fid);
+      case MODE_L2:
+        return gemm_dispatch_mode<64, MODE_L2, true>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
+                                                     nsplit, self0, part, st, qlist, qcount, fkey,
+                                                     fid);
+      case MODE_COS:
+        return gemm_dispatch_mode<64, MODE_COS, true>(X, xaux, Q, qaux, ld, esize, ntotal, nq_pad,
+                                                      nsplit, self0, part, st, qlist, qcount, fkey,
+                                                      fid);
+      default:
+        return hipErrorInvalidValue;
+    }
   }
   switch (KP) {
     case 8:

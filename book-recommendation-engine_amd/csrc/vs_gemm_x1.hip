@@ -1953,7 +1953,12 @@ hipError_t l2aug_params(const float* X, int64_t ld, int64_t r0, int64_t n, const
       out->C = (float)c;
       out->nref = nref;
       out->Cb = std::ldexp(1.0f, (int)std::lround(std::log2(c)));
-      out->m = (int)std::min<double>(4096.0, std::max(64.0, std::ceil(need / 64.0) * 64.0));
+      // capped at ld / 8 (at least 64 columns): a few tiny-but-nonzero rows
+      // would otherwise widen every row of the plane (up to 4096 columns);
+      // past the cap a row's extra entries exceed its max|x| and only its own
+      // scale coarsens (quantize_i8_l2aug_kernel: s = max(max|x|, |E| / m) / 127)
+      const double cap = std::max(64.0, std::ceil((double)ld / 8.0 / 64.0) * 64.0);
+      out->m = (int)std::min<double>(cap, std::max(64.0, std::ceil(need / 64.0) * 64.0));
     }
   }
   (void)hipFree(acc);
@@ -2157,7 +2162,7 @@ __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, doubl
     return B * (1.0 + 1e-6);
   }
   const double xm = sqrt((double)__uint_as_float(stats[0]) * (1.0 + ba.norm_inf));
-  const double rx = sqrt((double)__uint_as_float(stats[1]));
+  const double rx = ba.rows_exact ? 0.0 : sqrt((double)__uint_as_float(stats[1]));
   const double hx = xm + rx;
   const double hq = sqrt(qh2), rq = sqrt(qr2), qn = sqrt(qn2);
   double b = ba.gam * hx * hq + hx * rq + rx * hq + rx * rq + 2.0 * ldexp(1.0, -24) * xm * qn;
@@ -2171,7 +2176,8 @@ __device__ __forceinline__ double bound_key(int mode, const BoundArgs& ba, doubl
     // ~gam(ld) each, 1.5 norm_inf together); |s_a - s_e| / (|x||q|) <=
     // gam (1+rho)^2 + 2 rho (1+rho) + rho^2 + 2^-23, rho = max |r(x)| / |x| (the queries are stored rows); two roundings
     // of a key of magnitude <= 1 add 2^-22
-    const double rho = sqrt((double)__uint_as_float(stats[2]) * (1.0 + ba.norm_inf));
+    const double rho =
+        ba.rows_exact ? 0.0 : sqrt((double)__uint_as_float(stats[2]) * (1.0 + ba.norm_inf));
     const double rel = ba.gam * (1 + rho) * (1 + rho) + 2 * rho * (1 + rho) + rho * rho +
                        ldexp(1.0, -23);
     b = (rel * (1.0 + 1.5 * ba.norm_inf) + ldexp(1.0, -22)) * (1.0 + 1e-6);
@@ -2355,6 +2361,10 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
   const float* qrow = Q + (int64_t)q * ld;
   double qh2, qr2, qn2;
   query_split_norms(qrow, ld, lane, qr2i8 ? qr2i8 + q : nullptr, qh2, qr2, qn2, ba.aug_q2);
+  if (ba.rows_exact) {  // the fp32 GEMM multiplied q itself
+    qh2 = qn2;
+    qr2 = 0.0;
+  }
   __syncthreads();  // sid
   if (ld <= 256 * kQV) {  // two candidates per step, the query in registers
     QSlice qsl;

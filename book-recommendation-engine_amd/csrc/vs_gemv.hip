@@ -28,8 +28,9 @@ __device__ __forceinline__ void widen_chunk(const uint4 v, float (&f)[16 / sizeo
 }
 
 // FLOOR: query q's list admits only rows strictly after (fkey[q], fid[q]) in
-// (key, row) order (the second page of an inner-product search, vs_api.hip
-// run_wide_k); `run` (optional device flag): nothing to do when *run == 0.
+// (key, row) order (page p + 1 of the paged engine, vs_api.hip run_paged; a
+// query with nothing left to page gets the floor (+inf, INT_MAX) and an empty
+// list); `run` (optional device flag): nothing to do when *run == 0.
 template <int NQ, int KP, int MODE, typename T, bool FLOOR = false>
 __global__ __launch_bounds__(256) void gemv_topk(const T* __restrict__ X,
                                                  const float* __restrict__ Q, int64_t ld,
@@ -171,10 +172,15 @@ static hipError_t gemv_dispatch_t(int mode, const T* X, const float* Q, int64_t 
   rpb = (rpb + 15) & ~15;
   const size_t lds = (size_t)NQ * ld * sizeof(float) + (size_t)4 * NQ * KP * 8;
   if (fkey) {
-    if constexpr (KP == 64 && NQ <= 2) {
-      if (mode != MODE_IP) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_IP, T, true>), dim3(nblocks), dim3(256), lds, st,
-                         X, Q, ld, ntotal, rpb, part.key, part.id, fkey, fid, run);
+    if constexpr (KP == 64) {
+      if (mode == MODE_IP)
+        hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_IP, T, true>), dim3(nblocks), dim3(256), lds,
+                           st, X, Q, ld, ntotal, rpb, part.key, part.id, fkey, fid, run);
+      else if (mode == MODE_L2D)
+        hipLaunchKernelGGL((gemv_topk<NQ, KP, MODE_L2D, T, true>), dim3(nblocks), dim3(256), lds,
+                           st, X, Q, ld, ntotal, rpb, part.key, part.id, fkey, fid, run);
+      else
+        return hipErrorInvalidValue;
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
@@ -224,7 +230,7 @@ hipError_t launch_gemv_topk(int KP, int mode, int nq, const void* X, int esize, 
                             const float* fkey, const int* fid, const int* run) {
   if (nq < 1 || nq > kGemvMaxQ || part.KP != KP || part.P != nblocks || (ld * esize) % 16 != 0 ||
       (esize != 4 && esize != 2) || ((fkey == nullptr) != (fid == nullptr)) ||
-      (fkey && (KP != 64 || nq > 2 || mode != MODE_IP)))
+      (fkey && (KP != 64 || (mode != MODE_IP && mode != MODE_L2D))))
     return hipErrorInvalidValue;
   switch (KP) {
     case 8:

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <climits>
 #include <cstdint>
 
 namespace vs {
@@ -179,6 +180,10 @@ struct BoundArgs {
   int l2aug = 0;
   double aug_q2 = 0.0;
   double aug_nref = 0.0;  // the augmentation's reference norm (launch_l2aug_map)
+  // the pass multiplied the fp32 rows and queries themselves (the exact
+  // engine's fp32 GEMM, the staged engine's last stage): no residuals, only the
+  // fp32 accumulation (gam as for bf16 products) and the key's own roundings
+  int rows_exact = 0;
 };
 BoundArgs make_bound_args(int64_t ld, int filter);
 // The augmentation of an L2 index's int8 plane (launch_quantize_i8_l2aug).
@@ -348,21 +353,48 @@ hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t
 // Shard lists [nparts][nq][k_in] (scores, int64 labels) -> [nq][k].
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts,
                               int nq, int k_in, int k, float* D, int64_t* I, hipStream_t st);
-// Inner product with k > 32 (vs_support.hip): D1/I1 = the first page (the
-// lexicographic top-64 of each query: scores, labels with id_base); flags[q] =
-// a second page is needed (the k-th key's run of equal keys reaches entry 63, or
-// raw and the page is full), fkey/fid = its floor (key and local row of entry 63).
-// gl / gc (optional): a gathered batch, queries gl[0 .. *gc) of the nq rows
-// (the other rows' flags are left as they are).
-hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, int raw,
-                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st,
-                             const int* gl = nullptr, const int* gc = nullptr);
-// The two pages -> (D, I) rows of k <= 128 entries (faiss's rule unless raw);
-// D2/I2 rows are read only where flags[q].
-hipError_t launch_page_finish(const float* D1, const int64_t* I1, const float* D2,
-                              const int64_t* I2, const int* flags, int nq, int k, int raw,
-                              float* D, int64_t* I, hipStream_t st, const int* gl = nullptr,
-                              const int* gc = nullptr);
+// The exact-key stream (vs_exact.hip): for the gathered slots
+// slots[s0 .. s0 + min(*count - s0, nslot)) of a query batch whose rows sit at
+// Q + slot * ld (aux values qaux[slot]: |q|^2 for L2, 1/|q| for cosine; qrow[slot]:
+// the row to exclude, or -1; qrow may be null), the top-KP of every row by the
+// rescoring's exact key (fp64 sums, vs_gemm_x1.hip exact_key), as part.P lists
+// per slot (part.P row blocks).  NQ queries per group: exact_stream_nq(ld)
+// (0: ld too large for the LDS staging).
+struct ExactStreamArgs {
+  const float* X = nullptr;     // fp32 rows [ntotal][ld]
+  const float* xn = nullptr;    // |x|^2 (L2)
+  const float* xinv = nullptr;  // 1/|x| (cosine)
+  int64_t ld = 0;
+  int ntotal = 0;
+  const float* Q = nullptr;
+  const float* qaux = nullptr;
+  const int* qrow = nullptr;
+  const int* slots = nullptr;
+  const int* count = nullptr;
+  int s0 = 0, nslot = 0;
+};
+int exact_stream_nq(int64_t ld);
+hipError_t launch_exact_stream(int KP, int mode, const ExactStreamArgs& a, Partials part,
+                               hipStream_t st);
+// The paged exact engine (vs_support.hip, "paged exact engine"; vs_api.hip
+// run_paged).  Dacc/Iacc [n][KA]: the pages side by side (scores, local rows).
+// page_init: member/active flags (every q < n, or gl[0 .. *gc) of zeroed rows)
+// and the first page's floor (-inf, -1) for fkey/fid[0 .. nfloor).
+hipError_t launch_page_init(int n, int nfloor, const int* gl, const int* gc, int* member,
+                            int* active, float* fkey, int* fid, hipStream_t st);
+// After page `page`: active[q] = query q needs the next page (its page was full
+// and it has fewer than k entries, or `rule` and the k-th key's run of ties
+// reaches the page's end below 2k - 1), fkey/fid = its floor (+inf when not).
+hipError_t launch_page_step(const float* Dacc, const int64_t* Iacc, int64_t KA, int page, int n,
+                            int64_t k, int rule, int mode, int* active, float* fkey, int* fid,
+                            hipStream_t st);
+// *out = *count > 0 ? n : 0 (the device-side count of a GEMV page's lists).
+hipError_t launch_page_gate(const int* count, int n, int* out, hipStream_t st);
+// The member queries' k outputs (faiss's inner-product rule when `rule`), rows
+// q * k of D / I, labels + id_base, min_score applied as merge_partials does.
+hipError_t launch_page_finish(int mode, float* Dacc, int64_t* Iacc, int64_t KA, int n, int64_t k,
+                              int rule, const int* member, int64_t id_base, float min_score,
+                              float* D, int64_t* I, hipStream_t st);
 // out[r] = sum_j X[r][j]^2 for rows [r0, r0+n) (fp32 or bf16 rows).
 hipError_t launch_row_norms(const void* X, int esize, int64_t ld, int64_t r0, int64_t n,
                             float* out, hipStream_t st);

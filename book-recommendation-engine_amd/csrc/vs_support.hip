@@ -313,23 +313,33 @@ __global__ __launch_bounds__(64) void merge_parts_kernel(const float* __restrict
                             D + (int64_t)q * k + lane, I + (int64_t)q * k + lane);
 }
 
-__global__ void merge_parts_wide_kernel(const float* __restrict__ Dp,
-                                        const int64_t* __restrict__ Ip, int nparts, int nq,
-                                        int k_in, int need, int k, float* __restrict__ D,
-                                        int64_t* __restrict__ I);
+__global__ void merge_parts_big_kernel(const float* __restrict__ Dp,
+                                       const int64_t* __restrict__ Ip, int nparts, int nq,
+                                       int64_t k_in, int64_t need, int64_t k, int asc,
+                                       float* __restrict__ sk, int64_t* __restrict__ si,
+                                       float* __restrict__ D, int64_t* __restrict__ I);
 
 hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int nparts, int nq,
                               int k_in, int k, float* D, int64_t* I, hipStream_t st) {
-  if (k < 1 || k > 64 || nq < 0 || nparts < 1 || k_in < 1) return hipErrorInvalidValue;
+  if (k < 1 || nq < 0 || nparts < 1 || k_in < 1) return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   // the pool keeps the lexicographically best `need` entries of all parts: k for
   // L2; for inner product the 2k-1 that faiss's tie rule reads
   const bool asc = (mode == MODE_L2 || mode == MODE_L2D);
-  if (!asc && 2 * k - 1 > 64) {  // raw shard lists of up to 128 entries
-    if (k_in > 128 || nparts > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(merge_parts_wide_kernel, dim3(nq), dim3(64), 0, st, Dp, Ip, nparts, nq,
-                       k_in, 2 * k - 1, k, D, I);
-    return hipGetLastError();
+  if ((!asc && 2 * k - 1 > 64) || k > 64) {  // beyond one 64-entry list
+    if (nparts > 64) return hipErrorInvalidValue;
+    const int64_t need = asc ? (int64_t)k : 2 * (int64_t)k - 1;
+    ScratchChunk chunk;
+    hipError_t e = scratch_chunk_get((size_t)nq * need * (sizeof(float) + sizeof(int64_t)), st,
+                                     &chunk);
+    if (e != hipSuccess) return e;
+    int64_t* si = (int64_t*)chunk.p;
+    float* sk = (float*)(si + (size_t)nq * need);
+    hipLaunchKernelGGL(merge_parts_big_kernel, dim3((nq + 63) / 64), dim3(64), 0, st, Dp, Ip,
+                       nparts, nq, (int64_t)k_in, need, (int64_t)k, asc ? 1 : 0, sk, si, D, I);
+    e = hipGetLastError();
+    scratch_chunk_put(chunk, st);
+    return e;
   }
   const int need = asc ? k : 2 * k - 1;
   const int KP = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 64;
@@ -351,129 +361,205 @@ hipError_t launch_merge_parts(int mode, const float* Dp, const int64_t* Ip, int 
 }
 
 // ---------------------------------------------------------------------------
-// Inner product with k > 32 (faiss's tie rule reads the 2k-1 <= 127 best (key,
-// label) entries; lists hold 64): the search's first page is its lexicographic
-// top-64 (D1/I1, scores + labels with id_base), and where the rule may need more
-// — the k-th key's run of equal keys reaching entry 63 — a second page holds the
-// next 64 entries after entry 63 (D2/I2, rows of the flagged queries only).  Raw
-// searches with 64 < k <= 128 take both pages whenever the first is full.
-// One thread per query: flags[q], and the floor of the second page (the key and
-// local row of entry 63).
-__global__ __launch_bounds__(256) void page_check_kernel(const float* __restrict__ D1,
-                                                         const int64_t* __restrict__ I1, int nq,
-                                                         int k, int raw, int64_t id_base,
-                                                         float* __restrict__ fkey,
-                                                         int* __restrict__ fid,
-                                                         int* __restrict__ flags,
-                                                         const int* __restrict__ gl,
-                                                         const int* __restrict__ gc) {
-  const int j0 = blockIdx.x * 256 + threadIdx.x;
-  if (j0 >= nq || (gc && j0 >= *gc)) return;
-  const int q = gl ? gl[j0] : j0;  // a gathered batch: its queries' rows only
-  const float* d = D1 + (int64_t)q * 64;
-  const int64_t* i = I1 + (int64_t)q * 64;
-  const bool full = i[63] >= 0;
-  flags[q] = full && (raw || d[63] == d[k - 1]) ? 1 : 0;
-  fkey[q] = -d[63];  // key = -score (inner product)
-  fid[q] = full ? (int)(i[63] - id_base) : -1;
-}
-
-hipError_t launch_page_check(const float* D1, const int64_t* I1, int nq, int k, int raw,
-                             int64_t id_base, float* fkey, int* fid, int* flags, hipStream_t st,
-                             const int* gl, const int* gc) {
-  if (nq <= 0) return hipSuccess;
-  if (k < 1 || k > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(page_check_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, D1, I1, nq, k,
-                     raw, id_base, fkey, fid, flags, gl, gc);
-  return hipGetLastError();
-}
-
-// One wave per query: the two pages concatenated (the second page starts after
-// the first's last entry, so the concatenation is the lexicographic top-128),
-// then faiss's tie rule (unless raw) and the k outputs.
-__global__ __launch_bounds__(64) void page_finish_kernel(
-    const float* __restrict__ D1, const int64_t* __restrict__ I1, const float* __restrict__ D2,
-    const int64_t* __restrict__ I2, const int* __restrict__ flags, int k, int raw,
-    float* __restrict__ D, int64_t* __restrict__ I, const int* __restrict__ gl,
-    const int* __restrict__ gc) {
-  __shared__ float sk[128];
-  __shared__ int64_t si[128];
-  if (gc && (int)blockIdx.x >= *gc) return;
-  const int q = gl ? gl[blockIdx.x] : (int)blockIdx.x;  // a gathered batch: its rows only
-  const int lane = threadIdx.x;
-  const bool two = flags[q] != 0;
-  const int64_t o = (int64_t)q * 64 + lane;
-  const int64_t a = I1[o];
-  sk[lane] = a >= 0 ? -D1[o] : FLT_MAX;
-  si[lane] = a >= 0 ? a : -1;
-  const int64_t b = two ? I2[o] : -1;
-  sk[64 + lane] = b >= 0 ? -D2[o] : FLT_MAX;
-  si[64 + lane] = b >= 0 ? b : -1;
-  __syncthreads();
-  if (lane == 0 && !raw) faiss_ip_tie_order<int64_t>(sk, si, 128, k);
-  __syncthreads();
-  for (int j = lane; j < k; j += 64) {
-    const int64_t id = si[j];
-    D[(int64_t)q * k + j] = id >= 0 ? -sk[j] : -FLT_MAX;
-    I[(int64_t)q * k + j] = id;
+// The paged exact engine (vs_api.hip run_paged): any k, every metric.  A
+// query's answer is read off its lexicographic (key, row) order in pages of 64
+// entries, page p + 1 computed by the FLOOR form of the exact kernels (entries
+// strictly after page p's last one).  The pages of a window of n queries land
+// side by side in Dacc/Iacc [n][KA] (scores and local rows; -1 past the end).
+//
+// page_init: member[q] = the query belongs to this call (every q < n, or the
+// gathered ones gl[0 .. *gc), whose member/active rows the host zeroed before),
+// active[q] = member[q], floor (-inf, -1) (page 1 admits every row).
+__global__ __launch_bounds__(256) void page_init_kernel(int n, int nfloor,
+                                                        const int* __restrict__ gl,
+                                                        const int* __restrict__ gc,
+                                                        int* __restrict__ member,
+                                                        int* __restrict__ active,
+                                                        float* __restrict__ fkey,
+                                                        int* __restrict__ fid) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < nfloor) {
+    fkey[j] = -INFINITY;
+    fid[j] = -1;
   }
-}
-
-hipError_t launch_page_finish(const float* D1, const int64_t* I1, const float* D2,
-                              const int64_t* I2, const int* flags, int nq, int k, int raw,
-                              float* D, int64_t* I, hipStream_t st, const int* gl, const int* gc) {
-  if (nq <= 0) return hipSuccess;
-  if (k < 1 || k > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(page_finish_kernel, dim3(nq), dim3(64), 0, st, D1, I1, D2, I2, flags, k, raw,
-                     D, I, gl, gc);
-  return hipGetLastError();
-}
-
-// Shard merge when the inner-product rule needs more than 64 entries (k > 32):
-// each part is a raw lexicographic list of k_in <= 128 entries; one thread
-// merges them (nparts x 127 steps) into LDS, then the rule and the k outputs.
-__global__ __launch_bounds__(64) void merge_parts_wide_kernel(const float* __restrict__ Dp,
-                                                              const int64_t* __restrict__ Ip,
-                                                              int nparts, int nq, int k_in,
-                                                              int need, int k,
-                                                              float* __restrict__ D,
-                                                              int64_t* __restrict__ I) {
-  __shared__ float sk[128];
-  __shared__ int64_t si[128];
-  __shared__ int head[64];  // nparts <= 64 (launcher)
-  const int q = blockIdx.x;
-  const int lane = threadIdx.x;
-  head[lane] = 0;
-  __syncthreads();
-  if (lane == 0) {
-    for (int j = 0; j < 128; ++j) {
-      float bk = FLT_MAX;
-      int64_t bi = -1;
-      int bp = -1;
-      if (j < need) {
-        for (int p = 0; p < nparts; ++p) {
-          if (head[p] >= k_in) continue;
-          const int64_t off = ((int64_t)p * nq + q) * k_in + head[p];
-          const int64_t id = Ip[off];
-          if (id < 0) continue;
-          const float key = -Dp[off];
-          if (bp < 0 || lex_less(key, id, bk, bi)) {
-            bk = key;
-            bi = id;
-            bp = p;
-          }
-        }
-      }
-      if (bp >= 0) ++head[bp];
-      sk[j] = bp >= 0 ? bk : FLT_MAX;
-      si[j] = bp >= 0 ? bi : -1;
+  if (gl) {
+    if (j < *gc) {
+      member[gl[j]] = 1;
+      active[gl[j]] = 1;
     }
-    faiss_ip_tie_order<int64_t>(sk, si, 128, k);
+  } else if (j < n) {
+    member[j] = 1;
+    active[j] = 1;
   }
-  __syncthreads();
-  for (int j = lane; j < k; j += 64) {
-    const int64_t id = si[j];
-    D[(int64_t)q * k + j] = id >= 0 ? -sk[j] : -FLT_MAX;
+}
+
+hipError_t launch_page_init(int n, int nfloor, const int* gl, const int* gc, int* member,
+                            int* active, float* fkey, int* fid, hipStream_t st) {
+  const int m = n > nfloor ? n : nfloor;
+  if (m <= 0) return hipSuccess;
+  if ((gl == nullptr) != (gc == nullptr)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(page_init_kernel, dim3((m + 255) / 256), dim3(256), 0, st, n, nfloor, gl, gc,
+                     member, active, fkey, fid);
+  return hipGetLastError();
+}
+
+// After page `page` of the active queries: does query q need the next page?
+// Only when the page came back full (64 entries: the order has more rows) and
+// the answer needs more entries: fewer than k so far, or — faiss's
+// inner-product rule (`rule`), which reads the k-th key's run of equal keys up
+// to 2k - 1 entries (faiss_ip_tie_order) — the run reaches the page's end.
+// Then the floor is the page's last entry; otherwise (+inf, INT_MAX), which
+// empties a query's list in a GEMV page (its lists are computed for every query).
+__global__ __launch_bounds__(256) void page_step_kernel(const float* __restrict__ Dacc,
+                                                        const int64_t* __restrict__ Iacc,
+                                                        int64_t KA, int page, int n, int64_t k,
+                                                        int rule, int l2, int* __restrict__ active,
+                                                        float* __restrict__ fkey,
+                                                        int* __restrict__ fid) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  bool more = false;
+  if (active[q]) {
+    const float* d = Dacc + (int64_t)q * KA;
+    const int64_t* i = Iacc + (int64_t)q * KA;
+    const int64_t cnt = (int64_t)(page + 1) * 64;  // entries so far when the page is full
+    const bool full = i[cnt - 1] >= 0;
+    more = full && cnt < KA &&
+           (cnt < k || (rule && cnt < 2 * k - 1 && d[cnt - 1] == d[k - 1]));
+    if (more) {
+      fkey[q] = l2 ? d[cnt - 1] : -d[cnt - 1];  // score -> key
+      fid[q] = (int)i[cnt - 1];
+    }
+  }
+  if (!more) {
+    fkey[q] = INFINITY;
+    fid[q] = INT_MAX;
+  }
+  active[q] = more ? 1 : 0;
+}
+
+hipError_t launch_page_step(const float* Dacc, const int64_t* Iacc, int64_t KA, int page, int n,
+                            int64_t k, int rule, int mode, int* active, float* fkey, int* fid,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (KA % 64 != 0 || (int64_t)(page + 1) * 64 > KA || k < 1) return hipErrorInvalidValue;
+  const int l2 = (mode == MODE_L2 || mode == MODE_L2D) ? 1 : 0;
+  hipLaunchKernelGGL(page_step_kernel, dim3((n + 255) / 256), dim3(256), 0, st, Dacc, Iacc, KA,
+                     page, n, k, rule, l2, active, fkey, fid);
+  return hipGetLastError();
+}
+
+// *out = n when *count > 0, else 0 (a GEMV page's lists exist for every query
+// of its window, or for none when its launch exited).
+__global__ void page_gate_kernel(const int* __restrict__ count, int n, int* __restrict__ out) {
+  if (threadIdx.x == 0) *out = *count > 0 ? n : 0;
+}
+
+hipError_t launch_page_gate(const int* count, int n, int* out, hipStream_t st) {
+  hipLaunchKernelGGL(page_gate_kernel, dim3(1), dim3(64), 0, st, count, n, out);
+  return hipGetLastError();
+}
+
+// faiss's inner-product rule over a member query's concatenated pages (one
+// thread per query; scores turned into keys in place, the rule, back).
+__global__ __launch_bounds__(64) void page_rule_kernel(float* __restrict__ Dacc,
+                                                       int64_t* __restrict__ Iacc, int64_t KA,
+                                                       int n, int64_t k,
+                                                       const int* __restrict__ member) {
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= n || !member[q]) return;
+  float* d = Dacc + (int64_t)q * KA;
+  int64_t* i = Iacc + (int64_t)q * KA;
+  int64_t nv = 0;
+  while (nv < KA && i[nv] >= 0) ++nv;
+  if (nv == 0) return;
+  for (int64_t j = 0; j < nv; ++j) d[j] = -d[j];
+  faiss_ip_tie_order<int64_t>(d, i, (int)nv, (int)k);
+  for (int64_t j = 0; j < nv; ++j) d[j] = -d[j];
+}
+
+// The k outputs of every member query (grid: n x ceil(k / 256)); entries past
+// the pages are empty (k > the rows there are).
+__global__ __launch_bounds__(256) void page_emit_kernel(
+    int mode, const float* __restrict__ Dacc, const int64_t* __restrict__ Iacc, int64_t KA,
+    int64_t k, int rule, const int* __restrict__ member, int64_t id_base, float min_score,
+    float* __restrict__ D, int64_t* __restrict__ I) {
+  const int q = blockIdx.x;
+  const int64_t j = (int64_t)blockIdx.y * 256 + threadIdx.x;
+  if (!member[q] || j >= k) return;
+  const int64_t id = j < KA ? Iacc[(int64_t)q * KA + j] : -1;
+  const float s = id >= 0 ? Dacc[(int64_t)q * KA + j] : 0.0f;
+  const bool l2 = mode == MODE_L2 || mode == MODE_L2D;
+  emit_result(mode, l2 ? s : -s, id, id_base, min_score, D + (int64_t)q * k + j,
+              I + (int64_t)q * k + j);
+}
+
+hipError_t launch_page_finish(int mode, float* Dacc, int64_t* Iacc, int64_t KA, int n, int64_t k,
+                              int rule, const int* member, int64_t id_base, float min_score,
+                              float* D, int64_t* I, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (k < 1 || KA % 64 != 0 || (k + 255) / 256 > 65535) return hipErrorInvalidValue;
+  // the inner-product rule itself, where the pages passed over a run of k-th key
+  // ties, runs over the first 2k - 1 entries only, as faiss_ip_tie_order reads them
+  if (rule) {
+    hipLaunchKernelGGL(page_rule_kernel, dim3((n + 63) / 64), dim3(64), 0, st, Dacc, Iacc, KA, n, k,
+                       member);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(page_emit_kernel, dim3(n, (unsigned)((k + 255) / 256)), dim3(256), 0, st, mode,
+                     Dacc, Iacc, KA, k, rule, member, id_base, min_score, D, I);
+  return hipGetLastError();
+}
+
+// Shard merge beyond one 64-entry list (k > 64, or inner product's 2k - 1 > 64):
+// each part is a raw lexicographic list of k_in entries; one thread per query
+// merges the parts' heads (nparts <= 64) into its `need` best entries in
+// scratch (sk/si [nq][need]), then faiss's rule (inner product) and the k outputs.
+__global__ __launch_bounds__(64) void merge_parts_big_kernel(
+    const float* __restrict__ Dp, const int64_t* __restrict__ Ip, int nparts, int nq, int64_t k_in,
+    int64_t need, int64_t k, int asc, float* __restrict__ sk, int64_t* __restrict__ si,
+    float* __restrict__ D, int64_t* __restrict__ I) {
+  __shared__ int64_t heads[64 * 64];
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= nq) return;
+  int64_t* head = heads + threadIdx.x * 64;
+  for (int p = 0; p < nparts; ++p) head[p] = 0;
+  float* ok = sk + (int64_t)q * need;
+  int64_t* oi = si + (int64_t)q * need;
+  int64_t n = 0;
+  for (; n < need; ++n) {
+    float bk = FLT_MAX;
+    int64_t bi = -1;
+    int bp = -1;
+    for (int p = 0; p < nparts; ++p) {
+      if (head[p] >= k_in) continue;
+      const int64_t off = ((int64_t)p * nq + q) * k_in + head[p];
+      const int64_t id = Ip[off];
+      if (id < 0) {
+        head[p] = k_in;  // a raw list ends at its first empty entry
+        continue;
+      }
+      const float key = asc ? Dp[off] : -Dp[off];
+      if (bp < 0 || lex_less(key, id, bk, bi)) {
+        bk = key;
+        bi = id;
+        bp = p;
+      }
+    }
+    if (bp < 0) break;
+    ++head[bp];
+    ok[n] = bk;
+    oi[n] = bi;
+  }
+  for (int64_t j = n; j < need; ++j) {
+    ok[j] = FLT_MAX;
+    oi[j] = -1;
+  }
+  if (!asc && n > 0) faiss_ip_tie_order<int64_t>(ok, oi, (int)n, (int)k);
+  for (int64_t j = 0; j < k; ++j) {
+    const int64_t id = j < need ? oi[j] : -1;
+    D[(int64_t)q * k + j] = id >= 0 ? (asc ? ok[j] : -ok[j]) : (asc ? FLT_MAX : -FLT_MAX);
     I[(int64_t)q * k + j] = id;
   }
 }

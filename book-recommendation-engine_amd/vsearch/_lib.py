@@ -58,6 +58,7 @@ SIGNATURES = {
     "vs_set_id_base": (_c_int, [_vp, _c_i64]),
     "vs_set_engine": (_c_int, [_vp, _c_int]),
     "vs_filter_plane": (_c_int, [_vp, ctypes.POINTER(_c_int)]),
+    "vs_notice": (ctypes.c_char_p, [_vp]),
     "vs_search": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
     "vs_reconstruct_n": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp]),
     "vs_remove_ids": (_c_int, [_vp, _vp, _c_i64, _i64p]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "vs_filter_stats": (_c_int, [_i64p, _i64p, _c_int]),
     "vs_filter_wide_stats": (_c_int, [_i64p]),
     "vs_filter_second_stats": (_c_int, [_i64p]),
+    "vs_filter_exact_stats": (_c_int, [_i64p]),
     "vs_filter_wide_sets": (_c_int, [_i64p, _i64p]),
     "vs_filter_dump_stats": (_c_int, [_i64p, _i64p]),
 }
@@ -237,6 +239,15 @@ def filter_second_stats() -> int:
     filter engine since the last filter_stats reset (read it before that reset)."""
     v = ctypes.c_int64(0)
     check(load().vs_filter_second_stats(ctypes.byref(v)))
+    return v.value
+
+
+def filter_exact_stats() -> int:
+    """Queries the staged engine's last stage ranked over every row by the
+    exact key (the fp32 bound could not prove its candidates) since the last
+    filter_stats reset (read it before that reset)."""
+    v = ctypes.c_int64(0)
+    check(load().vs_filter_exact_stats(ctypes.byref(v)))
     return v.value
 
 

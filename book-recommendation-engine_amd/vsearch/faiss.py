@@ -211,6 +211,13 @@ class IndexFlat(Index):
         _lib.check(self._lib.vs_filter_plane(self._h, ctypes.byref(v)), "vs_filter_plane")
         return tuple(n for bit, n in ((1, "i8"), (2, "bf16")) if v.value & bit)
 
+    @property
+    def notice(self) -> str:
+        """The library's last notice for this index ("" if none): a filter plane
+        dropped because HBM ran short while the storage grew."""
+        v = self._lib.vs_notice(self._h)
+        return v.decode() if v else ""
+
     def set_id_base(self, base: int) -> None:
         _lib.check(self._lib.vs_set_id_base(self._h, int(base)), "vs_set_id_base")
 

@@ -11,9 +11,9 @@ ties included:
   * inner product: faiss's CMin heap tie rule is a function of the 2k-1
     lexicographically best (-score, label) pairs of the whole corpus
     (oracle/flat.py faiss_order), so each shard returns its RAW best
-    m = 2k-1 pairs (VS_RAW_ORDER, no tie rule applied; up to 127 for k <= 64:
-    the shard's two-page search, vs_api.hip run_wide_k) and the merge
-    (vs_merge_topk) applies the rule once to the union of those lists.
+    m = 2k-1 pairs (VS_RAW_ORDER, no tie rule applied; any k: the shard's
+    paged search, vs_api.hip run_paged) and the merge (vs_merge_topk, any
+    k_in) applies the rule once to the union of those lists.
 The exchange is B*m*12 bytes per rank: latency-bound, not link-bound.
 
 Appends go to the last shard; removals compact inside each shard and shift the
@@ -128,7 +128,7 @@ class ShardedIndexFlat:
     def shard_k(self, k: int) -> int:
         """Entries each shard contributes to the merge (see the module docstring)."""
         if self.metric_type == vfaiss.METRIC_INNER_PRODUCT:
-            return 2 * int(k) - 1  # <= 2 * MAX_K - 1: raw searches go to 2 * MAX_K
+            return 2 * int(k) - 1  # raw searches page past 64 entries (any k)
         return int(k)
 
     def search(self, x, k: int):

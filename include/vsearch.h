@@ -47,9 +47,8 @@ extern "C" {
  * (key, label), key = distance (L2) or -score (IP), in that order, instead of
  * faiss's inner-product tie order.  The per-shard half of an exact row-sharded
  * search: faiss's IP tie rule is a function of the 2k-1 best (key, label) pairs
- * of the union, so each shard returns its raw best 2k-1 (inner product: k up to
- * 2 * VS_MAX_K under this flag) and vs_merge_topk applies the rule once
- * (vsearch/sharded.py).  No effect on L2. */
+ * of the union, so each shard returns its raw best 2k-1 (any k) and
+ * vs_merge_topk applies the rule once (vsearch/sharded.py).  No effect on L2. */
 #define VS_RAW_ORDER 4
 
 /* Status codes. */
@@ -59,9 +58,11 @@ extern "C" {
 #define VS_E_OOM (-3)     /* device allocation failed                          */
 #define VS_E_UNSUPPORTED (-4)
 
-/* Largest k of a search (register lists of up to 64 entries; inner-product
- * searches that need more — faiss's tie rule at k > 32, raw k up to 128 — read a
- * second page of 64 after the first, vs_api.hip run_wide_k). */
+/* The entries one exact page holds (register lists of 64).  Not a limit on k:
+ * searches and self-joins that need more — k > 64, raw k > 64, faiss's
+ * inner-product tie rule at k > 32 — read further pages of 64, each after the
+ * previous page's last (key, label) (vs_api.hip run_paged), as faiss-cpu's
+ * IndexFlat::search answers any k. */
 #define VS_MAX_K 64
 
 typedef struct vs_index vs_index;
@@ -143,6 +144,11 @@ int vs_set_engine(vs_index* idx, int engine);
 #define VS_FILTER_I8 1
 #define VS_FILTER_BF16 2
 int vs_filter_plane(const vs_index* idx, int* out);
+/* The last notice of the index: a filter plane dropped because HBM ran short
+ * while the storage grew (searches stay exact on the plane that remains or the
+ * exact fp32 engine, but slower); "" if none.  Library-specific.  The pointer
+ * stays valid until the next mutation of the index. */
+const char* vs_notice(const vs_index* idx);
 
 /* Rows [0,ntotal) get labels id_base + row.  Used by the row-sharded multi-GPU
  * index so that per-shard results carry global faiss labels. */
@@ -154,8 +160,9 @@ int vs_set_id_base(vs_index* idx, int64_t id_base);
  * lower label first; inner product follows faiss's CMin-heap rule (equal scores
  * come out in DESCENDING label order, and which tied labels stay depends on the
  * labels of the better rows — vs_support.hip faiss_ip_tie_order, exact for
- * every k <= VS_MAX_K: the rule reads the 2k-1 <= 127 best entries, taken from
- * a second page where the k-th key's run of equal keys fills the first).  L2 calls with n < 20 use faiss's sequential branch (direct sum of
+ * every k: the rule reads up to the 2k-1 best entries, taken from further
+ * pages where the k-th key's run of equal keys fills a page).  Any k > 0
+ * (k > ntotal pads; k > INT_MAX/2: VS_E_INVALID).  L2 calls with n < 20 use faiss's sequential branch (direct sum of
  * squares), n >= 20 the BLAS branch (|q|^2 + |x|^2 - 2 q.x clamped at 0).
  * Asynchronous on `stream` when every buffer is on the device (no host wait).
  * Caller: FAISS.similarity_search_with_score_by_vector, reached from
@@ -179,7 +186,7 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
  *   ORDER BY vec <=> src.vec LIMIT 15
  * at src/graph_refresher/main.py:339-354 and src/incremental_workers/similarity/main.py:80-87.
  * For stored rows q in [q0, q0+nq): the k rows with largest cosine similarity
- * dot/sqrt(|a|^2 |b|^2) (ties: lower row first), excluding row q itself when
+ * dot/sqrt(|a|^2 |b|^2) (ties: lower row first; any k, as SQL's LIMIT), excluding row q itself when
  * exclude_self != 0.  Entries whose similarity is < min_sim (the
  * graph_refresher's S.similarity_threshold filter, main.py:350-354) are returned
  * as (-FLT_MAX, -1).  Zero-norm rows never match (pgvector yields NaN for them).
@@ -190,7 +197,7 @@ int vs_selfjoin(vs_index* idx, int64_t q0, int64_t nq, int64_t k, int exclude_se
 /* Merge nparts per-shard top-k lists into one (faiss: the ResultHandler merge;
  * GPU-side half of the RCCL all-gather top-k merge).  Inputs are DEVICE arrays
  * laid out [nparts][nq][k_in] (scores + int64 labels, -1 = empty; raw order for
- * inner product, k_in <= 2 * VS_MAX_K, nparts <= 64); outputs are DEVICE arrays
+ * inner product, any k_in and k, nparts <= 64); outputs are DEVICE arrays
  * [nq][k].  metric picks the order (L2 ascending, IP descending). */
 int vs_merge_topk(const float* D_parts, const int64_t* I_parts, int64_t nparts, int64_t nq,
                   int64_t k_in, int64_t k, int metric, float* D, int64_t* I, void* stream);
@@ -218,6 +225,11 @@ int vs_filter_wide_stats(int64_t* wide);
 /* Queries the staged engine handed from the int8 plane to the bf16 plane since
  * the last vs_filter_stats reset.  Diagnostic only: no reference interface. */
 int vs_filter_second_stats(int64_t* second);
+/* Queries the staged engine's last stage could not prove from its fp32 GEMM
+ * candidates (dense near-ties inside the fp32 bound) and ranked over every row
+ * by the exact key instead (vs_exact.hip), since the last vs_filter_stats
+ * reset.  Diagnostic only: no reference interface. */
+int vs_filter_exact_stats(int64_t* streamed);
 /* Entries the wide checks examined (summed over queries) and how many of them
  * were read from HBM and rescored (the rest reuse the first check's exact keys),
  * since the last vs_filter_stats reset.  Diagnostic only: no reference interface. */

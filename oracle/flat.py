@@ -354,3 +354,66 @@ def pgvector_cosine_topk(x, k: int, q_rows=None, exclude_self: bool = True,
         S[drop] = -FLT_MAX
         I[drop] = -1
     return S, I
+
+
+def mismatches_vec(D, I, Dr, Ir, metric: int, xb, xq, rtol: float = 1e-5, qchunk: int = 128):
+    """mismatches() for large k, vectorised (the fp32 contract only): the same
+    checks — unique valid labels, padding where the oracle pads, D within
+    tolerance of the returned label's exact score, a label other than the
+    oracle's j-th only within both tolerances (a tie) — on numpy arrays in
+    query chunks.  Returns a list of problems (empty = parity)."""
+    xb64 = np.asarray(xb, dtype=np.float64)
+    xq64 = np.asarray(xq, dtype=np.float64)
+    D = np.asarray(D)
+    I = np.asarray(I)
+    Ir = np.asarray(Ir)
+    nb2 = np.einsum("ij,ij->i", xb64, xb64)
+    nq2 = np.einsum("ij,ij->i", xq64, xq64)
+    bad = []
+    if np.any(I >= xb64.shape[0]):
+        return [("label out of range",)]
+    pad = (I < 0) != (Ir < 0)
+    if pad.any():
+        q = int(np.nonzero(pad.any(axis=1))[0][0])
+        return [(q, "padding differs", I[q].tolist(), Ir[q].tolist())]
+    srt = np.sort(np.where(I >= 0, I, -np.arange(1, I.shape[1] + 1)[None, :]), axis=1)
+    dup = (np.diff(srt, axis=1) == 0).any(axis=1)
+    if dup.any():
+        return [(int(np.nonzero(dup)[0][0]), "duplicate labels")]
+    empty = I < 0
+    if np.any(D[empty] != neutral(metric)):
+        return [("padding score",)]
+
+    def scores(ids, q0, q1):
+        safe = np.where(ids >= 0, ids, 0)
+        ip = np.einsum("qd,qkd->qk", xq64[q0:q1], xb64[safe])
+        if metric == METRIC_INNER_PRODUCT:
+            return ip
+        return np.maximum(nq2[q0:q1, None] + nb2[safe] - 2.0 * ip, 0.0)
+
+    def tol(s, ids, q0, q1):
+        scale = np.maximum(1.0, np.abs(s))
+        if metric == METRIC_L2:
+            scale = np.maximum(scale, nq2[q0:q1, None] + nb2[np.where(ids >= 0, ids, 0)])
+        return 1e-5 * scale * (rtol / 1e-5)
+
+    for q0 in range(0, I.shape[0], qchunk):
+        q1 = min(I.shape[0], q0 + qchunk)
+        ids, rids = I[q0:q1], Ir[q0:q1]
+        valid = ids >= 0
+        s_got = scores(ids, q0, q1)
+        t_got = tol(s_got, ids, q0, q1)
+        off = valid & (np.abs(D[q0:q1].astype(np.float64) - s_got) > t_got)
+        for q, j in zip(*np.nonzero(off)):
+            bad.append((q0 + int(q), int(j), "score", float(D[q0 + q, j]), float(s_got[q, j])))
+        diff = valid & (ids != rids)
+        if diff.any():
+            s_ref = scores(rids, q0, q1)
+            t_ref = tol(s_ref, rids, q0, q1)
+            lab = diff & (np.abs(s_got - s_ref) > t_got + t_ref)
+            for q, j in zip(*np.nonzero(lab)):
+                bad.append((q0 + int(q), int(j), "label", int(ids[q, j]), int(rids[q, j]),
+                            float(s_got[q, j]), float(s_ref[q, j])))
+        if len(bad) > 20:
+            break
+    return bad

@@ -2,7 +2,7 @@
 collected): a real HIP shard of ShardedIndexFlat on GPU 0 beside its peers,
 torch.distributed over gloo (RCCL refuses two ranks on one GPU), so the N > 1
 path of the row-sharded search runs on a one-GPU box: raw per-shard 2k-1
-lists (VS_RAW_ORDER, the two-page search past k = 32), the all-gather, and
+lists (VS_RAW_ORDER, the paged search past k = 32: any k), the all-gather, and
 vs_merge_topk over `world` parts on the GPU (sharded.py search /
 search_device), plus removals and appends across shards.  Each check compares
 with the fp64 oracle over the whole corpus; rank 0 prints one JSON line of
@@ -53,7 +53,8 @@ def main():
         check(f"{mn}_counterexample", D, I, xc, q1, 4, metric, True)
 
         # tie-heavy integer rows (exact scores): labels and scores bit for bit,
-        # k past 32 (raw 2k-1 = 127 entries: both pages on every shard)
+        # k past 32 (raw 2k-1 entries: several pages on every shard; k = 100
+        # and 300 past one page's 64 and the merge past 128 entries)
         rng = np.random.default_rng(11 + metric)
         x = rng.integers(-2, 3, size=(3001, 8)).astype(np.float32)
         xq = rng.integers(-2, 3, size=(37, 8)).astype(np.float32)
@@ -61,7 +62,7 @@ def main():
         idx.add_global(x)
         lo, hi = shard_bounds(3001, world, rank)
         res[f"{mn}_layout"] = bool(idx.ntotal == 3001 and idx.shard.ntotal == hi - lo)
-        for k in (1, 4, 10, 33, 64):
+        for k in (1, 4, 10, 33, 64, 100, 300):
             D, I = idx.search(xq, k)
             check(f"{mn}_ties_k{k}", D, I, x, xq, k, metric, True)
             # the device path: the same lists through search_device
@@ -77,7 +78,7 @@ def main():
         res[f"{mn}_remove_count"] = bool(n == nr and idx.ntotal == xr.shape[0])
         idx.add_global(x[:17])
         x2 = np.concatenate([xr, x[:17]])
-        for k in (10, 60):
+        for k in (10, 60, 150):
             D, I = idx.search(xq, k)
             check(f"{mn}_mutated_k{k}", D, I, x2, xq, k, metric, True)
 
@@ -87,7 +88,7 @@ def main():
         qf = rng.standard_normal((512, 1536)).astype(np.float32)
         idf = ShardedIndexFlat(1536, metric, device=0)
         idf.add_global(xf)
-        for k in (10, 50):
+        for k in (10, 50, 100):
             Dd, Id = idf.search_device(torch.from_numpy(qf).cuda(), k)
             torch.cuda.synchronize()
             check(f"{mn}_float_device_k{k}", Dd.cpu().numpy(), Id.cpu().numpy(), xf, qf, k,

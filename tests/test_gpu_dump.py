@@ -129,6 +129,35 @@ def test_dump_slot_overflow_hands_queries_on(lib):
     assert over > 0, (dumps, over)
 
 
+@pytest.mark.parametrize("engine", ["auto", "i8v"])
+def test_dense_near_ties_reach_the_exact_stream(lib, engine):
+    """Round 5's first form of the test above: the copies' factors 1 + 1e-3 pos / N
+    put them ~7e-9 apart (relative), far inside the fp32 GEMM's rounding, so no
+    fp32 candidate list of the last stage holds a provable top-k (thousands of
+    copies inside its bound).  The last stage proves its candidates with the
+    fp32 GEMM's own bound and hands what it cannot prove to the exact-key stream
+    (vs_exact.hip: every row ranked by the rescoring's key): STRICT parity."""
+    from vsearch import faiss as vfaiss
+
+    rng = np.random.default_rng(77)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    dup = rng.uniform(-1, 1, D_).astype(np.float32)
+    pos = np.sort(rng.choice(N, 150_000, replace=False))
+    xb[pos] = dup[None, :] * (1.0 + 1e-3 * pos[:, None] / N).astype(np.float32)
+    xq = (dup[None, :] + 0.3 * rng.uniform(-1, 1, (B, D_))).astype(np.float32)
+    index = vfaiss.IndexFlat(D_, IP)
+    index.add(xb)
+    index.set_engine(engine)
+    lib.filter_stats(reset=True)
+    D, I = index.search(xq, 10)
+    streamed = lib.filter_exact_stats()
+    lib.filter_stats(reset=True)
+    assert streamed > 0
+    Dr, Ir = flat.knn_exact(xb, xq[SAMPLE], 10, IP)
+    bad = flat.mismatches(D[SAMPLE], I[SAMPLE], Dr, Ir, IP, xb, xq[SAMPLE], strict=True)
+    assert not bad, bad[:5]
+
+
 def test_dump_launches_queries_pointing_away(lib):
     """Every inner product below 0 (rows in [0, 1), queries in [-1, 0)): the
     lists' floors are above 0, where the largest row factor bounds nothing (a

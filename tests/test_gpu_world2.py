@@ -2,7 +2,7 @@
 torch.distributed over gloo (RCCL refuses two ranks on one device; the
 8-GPU node runs the same code over RCCL).  Covers what the CPU gloo tests
 cannot: ShardedIndexFlat with libvsearch shards — raw per-shard 2k-1 lists
-(the two-page search for k > 32), the all-gather and vs_merge_topk over two
+(the paged search past k = 32, k up to 300), the all-gather and vs_merge_topk over two
 parts on the GPU, removals/appends across shards, a search on a stream other than torch's
 current one (tests/gpu_world_worker.py)
 — and bench.py's own N = 2 paths: the row-sharded search with its live
@@ -57,7 +57,7 @@ def test_sharded_world2_real_shards_match_oracle():
     res = _run_ranks([os.path.join(ROOT, "tests", "gpu_world_worker.py")], 2, 100)
     bad = [k for k, v in res.items() if not v]
     assert not bad, bad
-    assert len(res) == 2 * (1 + 1 + 10 + 1 + 2 + 2 + 1)
+    assert len(res) == 2 * (1 + 1 + 14 + 1 + 3 + 3 + 1)
 
 
 _BENCH_ENV = {"VS_BENCH_BACKEND": "gloo", "VS_BENCH_DEVICE": "0"}

@@ -172,6 +172,38 @@ def test_mismatch_checker_catches_errors():
     assert flat.mismatches(D2, I, D, I, L2, xb, xq)
 
 
+@pytest.mark.parametrize("metric", [L2, IP])
+def test_vectorised_checker_agrees_with_mismatches(metric):
+    """mismatches_vec (the large-k checker of tests/test_gpu_wide_k.py) accepts
+    what mismatches accepts and catches what it catches: the fp32 results
+    themselves, swapped labels, off scores, padding and duplicates; and the C
+    heap agrees with the numpy rule past one 64-entry page (k up to 300)."""
+    rng = np.random.default_rng(5)
+    xb = rng.standard_normal((400, 8)).astype(np.float32)
+    xq = rng.standard_normal((20, 8)).astype(np.float32)
+    for k in (5, 100, 450):
+        Dr, Ir = flat.knn_exact(xb, xq, k, metric)
+        Df, If = flat.knn_faiss_fp32(xb, xq, k, metric)
+        assert not flat.mismatches_vec(Df, If, Dr, Ir, metric, xb, xq)
+        assert not flat.mismatches(Df, If, Dr, Ir, metric, xb, xq)
+        I2 = Ir.copy()
+        I2[3, [1, 4]] = Ir[3, [4, 1]]
+        assert flat.mismatches_vec(Dr, I2, Dr, Ir, metric, xb, xq)
+        D2 = Dr.copy()
+        D2[7, 2] += 0.01
+        assert flat.mismatches_vec(D2, Ir, Dr, Ir, metric, xb, xq)
+        I3 = Ir.copy()
+        I3[0, 1] = Ir[0, 0]
+        assert flat.mismatches_vec(Dr, I3, Dr, Ir, metric, xb, xq)
+    xi = rng.integers(-2, 3, size=(600, 3)).astype(np.float32)
+    qi = rng.integers(-2, 3, size=(4, 3)).astype(np.float32)
+    for k in (65, 100, 300):
+        Dc, Ic = cfaiss.knn_seq(xi, qi, k, metric)
+        Dn, In = flat.knn_exact(xi, qi, k, metric)
+        np.testing.assert_array_equal(Ic, In)
+        np.testing.assert_array_equal(Dc, Dn)
+
+
 def _engine_keys(xb, xq, metric):
     """The filter engine's final keys restated in numpy: fp64 dot products
     rounded once, fp64-summed norms rounded once, L2 by faiss's BLAS formula in
