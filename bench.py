@@ -968,8 +968,12 @@ def run_c5(args, ctx):
         gen = np.concatenate([np.delete(gen, rm), np.arange(g0, g0 + nmut, dtype=np.int64)])
     assert index.ntotal == gen.size
     n_shard = index.shard.ntotal
-    esz = 2 if args.dtype == "bf16" else 4
     kname = ctx.lib.timer_kernel()
+    # the small-batch filter pass streams the index's int8 plane (1 B per
+    # element; the verification then reads a few candidate rows), the exact
+    # kernels the stored rows (bf16: 2 B)
+    esz = {"skinny_plane_topk_i8": 1, "skinny_plane_topk": 2}.get(
+        kname, 2 if args.dtype == "bf16" else 4)
     traffic, tsrc = pmc_traffic(args.workload, "void vs::" + kname + "<")
     rf = roofline("hbm", n_shard * d * esz * args.steps, kms, nl,
                   f"{n_shard}*{d}*{esz} B per search (batch {B} over the rank's shard)",
@@ -983,6 +987,11 @@ def run_c5(args, ctx):
         # fp32 exact reference over the same (mutated) corpus, rebuilt chunk by chunk
         chunk = 4_000_000
         parts_D, parts_I = [], []
+        # the reference chunks keep no filter planes (rows only: beside the
+        # bf16 index and its int8 plane, HBM holds 4M fp32 rows but not their
+        # planes too); their exact fp32 engine answers
+        prev = os.environ.get("VS_FILTER")
+        os.environ["VS_FILTER"] = "none"
         for a in range(0, gen.size, chunk):
             ref = vfaiss.IndexFlat(d, metric, device=ctx.local)
             ref.add_synthetic_ids(gen[a:a + chunk], seed=1234)
@@ -994,6 +1003,10 @@ def run_c5(args, ctx):
             parts_D.append(Dr)
             parts_I.append(Ir)
             del ref
+        if prev is None:
+            del os.environ["VS_FILTER"]
+        else:
+            os.environ["VS_FILTER"] = prev
         Dm = torch.empty((nr, k), dtype=torch.float32, device="cuda")
         Im = torch.empty((nr, k), dtype=torch.int64, device="cuda")
         Dall = torch.stack(parts_D).contiguous()

@@ -71,7 +71,11 @@ struct vs_index {
   int64_t* ddead = nullptr;  // device copy of `dead`
   int64_t ddead_cap = 0;
   int64_t live() const { return ntotal - (int64_t)dead.size(); }
-  bool tombstones() const { return !plane_on[0] && !plane_on[1]; }
+  // removals fill rows with NaN in place (labels mapped at search time) instead
+  // of compacting at once: bf16 indexes (C5: 154 GB of rows cannot move at every
+  // removal; an int8 plane of theirs has its factors set to NaN with them) and
+  // indexes without planes
+  bool tombstones() const { return esize == 2 || (!plane_on[0] && !plane_on[1]); }
   bool l2aug() const { return metric == VS_METRIC_L2 && esize == 4; }
   int64_t planebytes(int p) const {
     if (!l2aug()) return ld * filter_bytes(p);
@@ -497,7 +501,11 @@ void planes_for(vs_index* idx) {
     return;
   }
   const bool f32 = idx->esize == 4;
-  const bool i8able = f32 && (idx->metric == VS_METRIC_INNER_PRODUCT || idx->metric == VS_METRIC_L2);
+  // bf16 indexes: an int8 plane for inner product (C5: the small-batch filter
+  // pass streams 1 B per element instead of the rows' 2; the verification
+  // rescores the stored bf16 values)
+  const bool i8able = f32 ? (idx->metric == VS_METRIC_INNER_PRODUCT || idx->metric == VS_METRIC_L2)
+                          : idx->metric == VS_METRIC_INNER_PRODUCT;
   idx->plane_on[FILTER_BF16] = f32 && !(i8able && e && strcmp(e, "i8") == 0);
   idx->plane_on[FILTER_I8] = i8able && !(e && strcmp(e, "bf16") == 0);
 }
@@ -550,7 +558,7 @@ const float* plane_norms(const vs_index* idx, int p) {
 // The filter plane and residual norms of fp32 rows [r0, r0+n) (after the rows
 // and their norms are in place).
 int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st, bool appended = false) {
-  if (idx->esize != 4 || n <= 0) return VS_OK;
+  if (n <= 0 || (idx->esize != 4 && !idx->plane_on[FILTER_I8])) return VS_OK;
   for (int p = 0; p < 2; ++p) {
     if (!idx->plane_on[p] || idx->bstats[p]) continue;
     VS_HIP(hipMalloc(&idx->bstats[p], 4 * sizeof(unsigned)), "vs: bound maxima");
@@ -581,8 +589,8 @@ int derive_plane(vs_index* idx, int64_t r0, int64_t n, hipStream_t st, bool appe
                                       idx->rn2[FILTER_I8], idx->anorm, st),
              "vs: int8 L2 filter plane");
   } else if (idx->plane_on[FILTER_I8]) {
-    VS_HIP(launch_quantize_i8((const float*)idx->codes, idx->ld, r0, n,
-                              (int8_t*)idx->fplane[FILTER_I8], idx->fscale, idx->rn2[FILTER_I8], st),
+    VS_HIP(launch_quantize_i8(idx->codes, idx->ld, r0, n, (int8_t*)idx->fplane[FILTER_I8],
+                              idx->fscale, idx->rn2[FILTER_I8], st, idx->esize),
            "vs: int8 filter plane");
   }
   if (idx->plane_on[FILTER_BF16] && idx->l2aug()) {
@@ -1179,9 +1187,9 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(scr.alloc((void**)&qcount, 2 * sizeof(int)), "vs: scratch");
   const float* qinv = mode == MODE_COS ? qaux : nullptr;
   const float* xinv = mode == MODE_COS ? a.xaux : nullptr;
-  VS_HIP(launch_verify_rescore(vmode, nq, KF, need, Dk, Ik, (const float*)idx->codes, idx->norms,
-                               Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags,
-                               st, qinv, xinv, qr2, gc, x.qcut),
+  VS_HIP(launch_verify_rescore(vmode, nq, KF, need, Dk, Ik, idx->codes, idx->norms, Q, qaux,
+                               idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags, st, qinv,
+                               xinv, qr2, gc, x.qcut, idx->esize),
          "vs: verify");
   unsigned long long* dst = device_stats(idx->device);
   if (!dst) return fail(VS_E_HIP, "vs: statistics buffer");
@@ -1190,9 +1198,9 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount, dst + 1, gathered ? nullptr : dst + 0, st),
          "vs: flags");
   if (wide_enabled())
-    VS_HIP(launch_verify_wide(vmode, nq, qlist, qcount, KF, need, (const float*)idx->codes,
-                              idx->norms, Q, qaux, idx->ld, ba, stats, part, L, vp.key, vp.id,
-                              vp.KP, flags, st, qinv, xinv, qr2, Dk, Ik, dst + 4, x.qcut),
+    VS_HIP(launch_verify_wide(vmode, nq, qlist, qcount, KF, need, idx->codes, idx->norms, Q, qaux,
+                              idx->ld, ba, stats, part, L, vp.key, vp.id, vp.KP, flags, st, qinv,
+                              xinv, qr2, Dk, Ik, dst + 4, x.qcut, idx->esize),
            "vs: verify wide");
   VS_HIP(launch_compact_flags(flags, nq, qlist, qcount + 1, last_plane ? dst + 2 : dst + 3,
                               nullptr, st),
@@ -1219,12 +1227,13 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   return run_gemm_rescored(idx, a, need, KF, plane, st, next, qcount + 1);
 }
 
-// The staged engine's last stage: the exact fp32 MFMA GEMM over the queries no
-// filter stage settled (gathered: gl[0 .. *gc) of `a`) keeps KF candidates per
-// query, which are rescored like every other stage's (verify_rescore: fp64
-// sums, one rounding), so every key the staged engine returns is the fp32
-// rounding of the exact score (oracle/flat.py key_window).  The check verify
-// computes is not used here: this is the last stage.
+// The staged engine's last stage: the exact fp32 MFMA GEMM (bf16 rows: the
+// bf16 one) over the queries no filter stage settled (gathered: gl[0 .. *gc) of
+// `a`) keeps KF candidates per query, which are rescored like every other
+// stage's (verify_rescore: fp64 sums, one rounding), so every key the staged
+// engine returns is the fp32 rounding of the exact score (oracle/flat.py
+// key_window); the candidates are proven with the GEMM's own bound and what it
+// cannot prove goes to the exact-key stream (below).
 // Slots of the exact-key stream per launch (its lists: kExactSlots x up to
 // 256 row blocks x KP entries); launches past the device-side count exit.
 constexpr int kExactSlots = 256;
@@ -1236,7 +1245,7 @@ bool exact_stream_on() {
 int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int plane,
                       hipStream_t st, const int* gl, const int* gc) {
   // more than the 64 entries one exact page holds (inner product, k > 32): the
-  // two-page exact engine over the gathered queries (its keys are the fp32
+  // paged exact engine over the gathered queries (its keys are the fp32
   // engine's own, as in a search that never went through the filter)
   if (KF > 64) return run_paged(idx, a, st, gl, gc);
   const int ntotal = (int)idx->ntotal;
@@ -1276,6 +1285,11 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
   VS_HIP(scr.alloc((void**)&flags, (size_t)cap * sizeof(int)), "vs: scratch");
   VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
   const float* Qa = a.self0 >= 0 ? (const float*)idx->row(a.self0) : a.qbuf;
+  uint16_t* qc16 = nullptr;
+  if (idx->esize == 2) {
+    if (a.self0 >= 0 || !a.qb16) return fail(VS_E_INVALID, "vs: bf16 last stage");
+    VS_HIP(scr.alloc((void**)&qc16, (size_t)cap * idx->ld * sizeof(uint16_t)), "vs: scratch");
+  }
   const float* qinv = a.mode == MODE_COS ? ac : nullptr;
   const float* xinv = a.mode == MODE_COS ? a.xaux : nullptr;
   const int emode = a.mode == MODE_L2 && a.l2_direct ? MODE_L2D : a.mode;
@@ -1287,7 +1301,8 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
   // is the exact top-k of the rescored keys.
   BoundArgs ba = make_bound_args(idx->ld, FILTER_BF16);
   ba.rows_exact = 1;
-  const bool stream_ok = exact_stream_on() && exact_stream_nq(idx->ld) > 0 && KP <= 64;
+  const bool stream_ok =
+      exact_stream_on() && idx->esize == 4 && exact_stream_nq(idx->ld) > 0 && KP <= 64;
   unsigned long long* dstats = device_stats(idx->device);
   int *fl = nullptr, *fc = nullptr, *ol = nullptr, *ewc = nullptr;
   Partials ep;
@@ -1322,22 +1337,27 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
     // the window's query rows and aux values, slot by slot, for the rescoring
     VS_HIP(launch_gather_queries(Qa, idx->ld, a.qaux, wl, wc, cap, a.self0, qc, ac, qrow, st),
            "vs: gathered queries");
+    // bf16 rows: the bf16 kernels take bf16 query rows (the staged values are
+    // already bf16-rounded, so the conversion is exact)
+    if (qc16) VS_HIP(launch_f32_to_bf16(qc, idx->ld, qc16, idx->ld, cap, idx->ld, st), "vs: bf16 queries");
     if (skinny) {
-      VS_HIP(launch_skinny_topk(KP, a.mode, a.nq, idx->codes, idx->esize, a.xaux, qc, ac, idx->ld,
-                                ntotal, sp.P, sp, st, wc),
+      VS_HIP(launch_skinny_topk(KP, a.mode, a.nq, idx->codes, idx->esize, a.xaux,
+                                qc16 ? (const void*)qc16 : (const void*)qc, ac, idx->ld, ntotal,
+                                sp.P, sp, st, wc),
              "vs: skinny_topk launch");
     } else {
-      VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux, Qa, a.qaux, idx->ld, idx->esize,
-                              ntotal, cap, nsplit, a.self0, part, st, wl, wc),
+      VS_HIP(launch_gemm_topk(KP, a.mode, idx->codes, a.xaux,
+                              idx->esize == 2 ? a.qb16 : (const void*)Qa, a.qaux, idx->ld,
+                              idx->esize, ntotal, cap, nsplit, a.self0, part, st, wl, wc),
              "vs: gemm_topk launch");
     }
     VS_HIP(launch_merge_partials(MODE_L2, skinny ? sp : part, skinny ? a.nq : cap, KF, 0, 0.0f, Dk,
                                  Ik, KF, st, 0, nullptr, wc),
            "vs: merge");
-    VS_HIP(launch_verify_rescore(emode, cap, KF, need, Dk, Ik, (const float*)idx->codes,
-                                 idx->norms, qc, ac, idx->ld, ba, idx->bstats[plane],
-                                 skinny ? sp : part, KP, vp.key, vp.id, vp.KP, flags, st, qinv,
-                                 xinv, nullptr, wc),
+    VS_HIP(launch_verify_rescore(emode, cap, KF, need, Dk, Ik, idx->codes, idx->norms, qc, ac,
+                                 idx->ld, ba, idx->bstats[plane], skinny ? sp : part, KP, vp.key,
+                                 vp.id, vp.KP, flags, st, qinv, xinv, nullptr, wc, nullptr,
+                                 idx->esize),
            "vs: rescore");
     VS_HIP(launch_merge_partials(emode, vp, cap, a.k, idx->id_base, a.min_score, a.D, a.I, a.k,
                                  st, a.raw, wl, wc),
@@ -1635,7 +1655,8 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
   // fp32 bytes), candidates rescored and proven exactly as for large batches,
   // the few queries it cannot settle through the bf16 plane and the fp32
   // rows (skinny kernels too) — instead of streaming the fp32 rows.
-  if (small_filter_on() && idx->esize == 4 && engine == VS_ENGINE_AUTO && KF > 0 && KF <= 32 &&
+  if (small_filter_on() && (idx->esize == 4 || mode == MODE_IP) && engine == VS_ENGINE_AUTO &&
+      KF > 0 && KF <= 32 &&
       nq <= kSkinnyMaxQ && a.self0 < 0 && ntotal >= kSmallFilterMinRows &&
       (mode == MODE_IP || mode == MODE_L2) && (i8_ok || b16_ok) && small_l2d_ok(mode, a)) {
     if (i8_ok && b16_ok) i8_ok = adaptive_use_i8(idx);
@@ -2335,7 +2356,8 @@ int vs_remove_ids(vs_index* idx, const int64_t* ids, int64_t n, int64_t* nremove
     VS_HIP(hipMemcpyAsync(drm, rm.data(), (size_t)nrem * sizeof(int64_t), hipMemcpyHostToDevice,
                           st),
            "vs_remove_ids: upload");
-    VS_HIP(launch_fill_nan_rows(idx->codes, idx->rowbytes(), idx->norms, idx->esize, drm, nrem, st),
+    VS_HIP(launch_fill_nan_rows(idx->codes, idx->rowbytes(), idx->norms, idx->esize, drm, nrem, st,
+                                idx->plane_on[FILTER_I8] ? idx->fscale : nullptr),
            "vs_remove_ids: tombstones");
     std::vector<int64_t> merged;
     merged.reserve(idx->dead.size() + rm.size());

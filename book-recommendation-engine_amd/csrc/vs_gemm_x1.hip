@@ -144,6 +144,16 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   return t;
 }
 
+// Four elements of a stored row as floats: fp32 rows, or bf16 rows widened
+// (exactly) — the verification of a bf16 index's int8 plane rescores the
+// stored bf16 values.
+__device__ __forceinline__ f32x4 row4(const float* __restrict__ p) { return *(const f32x4*)p; }
+__device__ __forceinline__ f32x4 row4(const uint16_t* __restrict__ p) {
+  const uint2 u = *(const uint2*)p;
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u),
+               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xFFFF0000u)};
+}
+
 __device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 __device__ __forceinline__ i32x4 as_i4(const uint4& u) { return __builtin_bit_cast(i32x4, u); }
 
@@ -1344,6 +1354,15 @@ static int x1_split_den() {
   const char* e = getenv("VS_X1_SPLIT");
   return e ? std::max(0, atoi(e)) : kX1SplitDen;
 }
+// Segmented split passes (env VS_X1_SPLITSEG=1, read at every search; A/B):
+// a split pass of den = 2^m parts (m >= 2) runs its dump part as m launches
+// over parts [1, 2), [2, 4), .. [den / 2, den), a replay after each, so every
+// segment doubles the rows seen and a lane list meets ~8 rows below its floor
+// per segment however small the list launch's share (1 / den) is.
+static bool x1_split_segments(int den) {
+  const char* e = getenv("VS_X1_SPLITSEG");
+  return e && atoi(e) != 0 && den >= 4 && (den & (den - 1)) == 0;
+}
 constexpr int kSplitMinTiles = 16;
 // (default: the bf16 plane's passes only — clustered C3 +1.4 %, C3's int8
 // pass -1 %, profiles/r05u)
@@ -1398,13 +1417,22 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
   // clustered +1.4 % (profiles/r05u).
   const int F = x1_first_den(EL);
   const bool quarter = cutting && !split && nchunk >= 4 && F >= 2 && per_block / (F * nchunk) >= 2;
+  const bool sseg = split && x1_split_segments(den);
+  int lg = 0;
+  while ((1 << lg) < den) ++lg;
   const int nparts = split ? den : quarter ? F * nchunk : nchunk;
-  const int nlaunch = split ? 2 : quarter ? nchunk + 1 : nchunk;
+  const int nlaunch = sseg ? lg + 1 : split ? 2 : quarter ? nchunk + 1 : nchunk;
   const int64_t ldb = a.ld * filter_bytes(EL);
   if (a.qtile0 < 0) return hipErrorInvalidValue;
   for (int c = 0; c < nlaunch; ++c) {
-    const int p0 = split ? (c == 0 ? 0 : 1) : quarter ? (c == 0 ? 0 : c == 1 ? 1 : F * (c - 1)) : c;
-    const int p1 = split ? (c == 0 ? 1 : den) : quarter ? (c == 0 ? 1 : F * c) : c + 1;
+    const int p0 = sseg    ? (c == 0 ? 0 : 1 << (c - 1))
+                   : split   ? (c == 0 ? 0 : 1)
+                   : quarter ? (c == 0 ? 0 : c == 1 ? 1 : F * (c - 1))
+                             : c;
+    const int p1 = sseg    ? (c == 0 ? 1 : 1 << c)
+                   : split   ? (c == 0 ? 1 : den)
+                   : quarter ? (c == 0 ? 1 : F * c)
+                             : c + 1;
     // the timed span of this launch alone (the cut and replay kernels between
     // launches stay outside the spans); the first launch of a pass whose later
     // launches dump is timed apart ("<name>_list")
@@ -1450,7 +1478,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     // by ~8 of the next n) — the cut alone is too wide when 2B spans
     // thousands of rows (C3: ~5k, 63 % of the lists out of 32 slots in one
     // segment, profiles/r04b).
-    if (later_dump && c > 0 && (((c + 1) & c) == 0 || c + 1 == nlaunch)) {
+    if (later_dump && c > 0 && (sseg || ((c + 1) & c) == 0 || c + 1 == nlaunch)) {
       e = launch_x1_replay(a, part, st);
       if (e != hipSuccess) return e;
     }
@@ -1627,7 +1655,8 @@ hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n,
 // residual |x - s code|^2 in fp64 (s * code and x - s * code are exact there),
 // rounded up to float; a non-finite row gets rn2 = +inf, which makes every
 // bound non-finite (every query then goes to the exact engine).
-__global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restrict__ X, int64_t ld,
+template <typename RT>
+__global__ __launch_bounds__(256) void quantize_i8_kernel(const RT* __restrict__ X, int64_t ld,
                                                           int64_t r0, int64_t n,
                                                           int8_t* __restrict__ codes,
                                                           float* __restrict__ scale,
@@ -1635,11 +1664,11 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restric
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
-  const float* xr = X + (r0 + row) * ld;
+  const RT* xr = X + (r0 + row) * ld;
   float m = 0.0f;
   bool bad = false;
   for (int64_t c = lane * 4; c < ld; c += 256) {
-    const f32x4 v = *(const f32x4*)(xr + c);
+    const f32x4 v = row4(xr + c);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bad |= !isfinite(v[i]);
@@ -1651,7 +1680,7 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const float* __restric
   const float s = bad ? 0.0f : m / 127.0f;
   double acc = 0.0;
   for (int64_t c = lane * 4; c < ld; c += 256) {
-    const f32x4 v = *(const f32x4*)(xr + c);
+    const f32x4 v = row4(xr + c);
     uint32_t packed = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2104,12 +2133,16 @@ hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* o
   return hipGetLastError();
 }
 
-hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
-                              float* scale, float* rn2, hipStream_t st) {
+hipError_t launch_quantize_i8(const void* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
+                              float* scale, float* rn2, hipStream_t st, int xesize) {
   if (n <= 0) return hipSuccess;
-  if (ld % 4 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(quantize_i8_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, ld, r0,
-                     n, codes, scale, rn2);
+  if (ld % 4 != 0 || (xesize != 4 && xesize != 2)) return hipErrorInvalidValue;
+  if (xesize == 4)
+    hipLaunchKernelGGL(quantize_i8_kernel<float>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st,
+                       (const float*)X, ld, r0, n, codes, scale, rn2);
+  else
+    hipLaunchKernelGGL(quantize_i8_kernel<uint16_t>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                       st, (const uint16_t*)X, ld, r0, n, codes, scale, rn2);
   return hipGetLastError();
 }
 
@@ -2223,12 +2256,12 @@ __device__ __forceinline__ void query_split_norms(const float* __restrict__ qrow
 // exact dot product of two fp32 rows (fp64 accumulation across the wave);
 // DIFF: the exact sum of (x - q)^2 instead (faiss's sequential L2 formula,
 // MODE_L2D: each difference of two floats is exact in fp64, its square too)
-template <bool DIFF = false>
-__device__ __forceinline__ double wave_dot(const float* __restrict__ x, const float* __restrict__ q,
+template <bool DIFF = false, typename RT = float>
+__device__ __forceinline__ double wave_dot(const RT* __restrict__ x, const float* __restrict__ q,
                                            int64_t ld, int lane) {
   double acc = 0.0;
   for (int64_t c = lane * 4; c < ld; c += 256) {
-    const f32x4 xv = *(const f32x4*)(x + c);
+    const f32x4 xv = row4(x + c);
     const f32x4 qv = *(const f32x4*)(q + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -2260,16 +2293,16 @@ __device__ __forceinline__ void load_qslice(const float* __restrict__ q, int64_t
     qs.v[i] = c < ld ? *(const f32x4*)(q + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }
-template <bool DIFF = false>
-__device__ __forceinline__ void wave_dot2(const float* __restrict__ xa, const float* __restrict__ xb,
+template <bool DIFF = false, typename RT = float>
+__device__ __forceinline__ void wave_dot2(const RT* __restrict__ xa, const RT* __restrict__ xb,
                                           const QSlice& qs, int64_t ld, int lane, double& ra,
                                           double& rb) {
   f32x4 va[kQV], vb[kQV];
 #pragma unroll
   for (int i = 0; i < kQV; ++i) {
     const int64_t c = lane * 4 + 256 * i;
-    va[i] = c < ld ? *(const f32x4*)(xa + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    vb[i] = c < ld ? *(const f32x4*)(xb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    va[i] = c < ld ? row4(xa + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    vb[i] = c < ld ? row4(xb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   double a = 0.0, b = 0.0;
 #pragma unroll
@@ -2311,10 +2344,10 @@ __device__ __forceinline__ float exact_key(float ip, int q, int r, const float* 
 // local rows; X/xn: fp32 rows (stride ld) and squared norms; Q: query rows
 // (stride ld); qn: |q|^2 as staged for L2.  Writes KF exact (key, row) entries
 // sorted, padded to KP, and fail[q].  NE = candidates per lane (KF <= 64 NE).
-template <int MODE, int NE>
+template <int MODE, int NE, typename RT>
 __global__ __launch_bounds__(64) void verify_rescore_kernel(
     int KF, int M, const float* __restrict__ Dk, const int64_t* __restrict__ Ik,
-    const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
+    const RT* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
     const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
@@ -2372,8 +2405,8 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
     for (int j = 0; j < KF; j += 2) {
       const int ra = sid[j], rb = j + 1 < KF ? sid[j + 1] : -1;
       double da, db;
-      wave_dot2<MODE == MODE_L2D>(X + (int64_t)max(ra, 0) * ld, X + (int64_t)max(rb, 0) * ld, qsl, ld,
-                                  lane, da, db);
+      wave_dot2<MODE == MODE_L2D, RT>(X + (int64_t)max(ra, 0) * ld, X + (int64_t)max(rb, 0) * ld,
+                                      qsl, ld, lane, da, db);
       if (lane == 0) {
         ek[j] = ra < 0 ? FLT_MAX : exact_key<MODE>((float)da, q, ra, qn, xn, qinv, xinv);
         if (j + 1 < KF) ek[j + 1] = rb < 0 ? FLT_MAX : exact_key<MODE>((float)db, q, rb, qn, xn, qinv, xinv);
@@ -2386,7 +2419,7 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
         if (lane == 0) ek[j] = FLT_MAX;
         continue;
       }
-      const double acc = wave_dot<MODE == MODE_L2D>(X + (int64_t)r * ld, qrow, ld, lane);
+      const double acc = wave_dot<MODE == MODE_L2D, RT>(X + (int64_t)r * ld, qrow, ld, lane);
       if (lane == 0) ek[j] = exact_key<MODE>((float)acc, q, r, qn, xn, qinv, xinv);
     }
   }
@@ -2424,25 +2457,34 @@ __global__ __launch_bounds__(64) void verify_rescore_kernel(
 }
 
 hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
-                                 const int64_t* Ik, const float* X, const float* xn,
+                                 const int64_t* Ik, const void* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
                                  const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st, const float* qinv,
                                  const float* xinv, const float* qr2i8, const int* qcount,
-                                 const float* qcut) {
+                                 const float* qcut, int xesize) {
   if (KF > kVerifyMaxKF || KP > kVerifyMaxKF || KF > KP || M < 1 || M > KF || ld % 4 != 0 ||
-      L < 1 || L > lists.KP)
+      L < 1 || L > lists.KP || (xesize != 4 && xesize != 2))
     return hipErrorInvalidValue;
   if (nq <= 0) return hipSuccess;
-#define VS_VERIFY(MD, NE)                                                                     \
-  hipLaunchKernelGGL((verify_rescore_kernel<MD, NE>), dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, \
-                     X, xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L,    \
-                     okey, oid, KP, fail, qinv, xinv, qr2i8, qcount, qcut)
-#define VS_VERIFY_NE(MD) \
-  if (KF <= 64)          \
-    VS_VERIFY(MD, 1);    \
-  else                   \
-    VS_VERIFY(MD, 2)
+#define VS_VERIFY_T(MD, NE, RT)                                                                    \
+  hipLaunchKernelGGL((verify_rescore_kernel<MD, NE, RT>), dim3(nq), dim3(64), 0, st, KF, M, Dk, Ik, \
+                     (const RT*)X, xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P,         \
+                     lists.KP, L, okey, oid, KP, fail, qinv, xinv, qr2i8, qcount, qcut)
+#define VS_VERIFY(MD, NE)                  \
+  do {                                     \
+    if (xesize == 4)                       \
+      VS_VERIFY_T(MD, NE, float);          \
+    else                                   \
+      VS_VERIFY_T(MD, NE, uint16_t);       \
+  } while (0)
+#define VS_VERIFY_NE(MD)   \
+  do {                     \
+    if (KF <= 64)          \
+      VS_VERIFY(MD, 1);    \
+    else                   \
+      VS_VERIFY(MD, 2);    \
+  } while (0)
   if (mode == MODE_IP)
     VS_VERIFY_NE(MODE_IP);
   else if (mode == MODE_L2)
@@ -2455,6 +2497,7 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
     return hipErrorInvalidValue;
 #undef VS_VERIFY_NE
 #undef VS_VERIFY
+#undef VS_VERIFY_T
   return hipGetLastError();
 }
 
@@ -2530,10 +2573,10 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // keys in okey/oid) keep their exact keys: an entry lexicographically at or
 // before the KF-th merged one is one of them, and only the others are read
 // from HBM again (C4: ~40 % of the wide set).
-template <int MODE>
+template <int MODE, typename RT>
 __global__ __launch_bounds__(256) void verify_wide_kernel(
     const int* __restrict__ qlist, const int* __restrict__ count, int KF, int M,
-    const float* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
+    const RT* __restrict__ X, const float* __restrict__ xn, const float* __restrict__ Q,
     const float* __restrict__ qn, int64_t ld, BoundArgs ba, const unsigned* __restrict__ stats,
     const float* __restrict__ lkey, const int* __restrict__ lid, int P, int LKP, int L,
     float* __restrict__ okey, int* __restrict__ oid, int KP, int* __restrict__ fail,
@@ -2669,7 +2712,7 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
         for (int j = wv; j < nu; j += 8) {
           const int ra = cid[j], rb = j + 4 < nu ? cid[j + 4] : ra;
           double da, db;
-          wave_dot2<MODE == MODE_L2D>(X + (int64_t)ra * ld, X + (int64_t)rb * ld, qsl, ld, lane, da,
+          wave_dot2<MODE == MODE_L2D, RT>(X + (int64_t)ra * ld, X + (int64_t)rb * ld, qsl, ld, lane, da,
                                       db);
           put(j, ra, da);
           if (j + 4 < nu) put(j + 4, rb, db);
@@ -2677,7 +2720,7 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
       } else {
         for (int j = wv; j < nu; j += 4) {
           const int r = cid[j];
-          put(j, r, wave_dot<MODE == MODE_L2D>(X + (int64_t)r * ld, qrow, ld, lane));
+          put(j, r, wave_dot<MODE == MODE_L2D, RT>(X + (int64_t)r * ld, qrow, ld, lane));
         }
       }
       if (tid < nk) {  // the reused exact keys after the rescored ones
@@ -2717,22 +2760,29 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
 }
 
 hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
-                              int M, const float* X, const float* xn, const float* Q,
+                              int M, const void* X, const float* xn, const float* Q,
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
                               const float* xinv, const float* qr2i8, const float* Dk,
                               const int64_t* Ik, unsigned long long* sizes,
-                              const float* qcut) {
+                              const float* qcut, int xesize) {
   if (KF > KP || KP > kVerifyMaxKF || (Dk && !Ik) || M < 1 || M > KF || ld % 4 != 0 || L < 1 ||
-      L > lists.KP)
+      L > lists.KP || (xesize != 4 && xesize != 2))
     return hipErrorInvalidValue;
   if (nq_max <= 0) return hipSuccess;
   const int grid = std::min(nq_max, 2048);
-#define VS_WIDE(MD)                                                                               \
-  hipLaunchKernelGGL(verify_wide_kernel<MD>, dim3(grid), dim3(256), 0, st, qlist, count, KF, M, X, \
-                     xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P, lists.KP, L, okey,   \
-                     oid, KP, fail, qinv, xinv, qr2i8, Dk, Ik, sizes, qcut)
+#define VS_WIDE_T(MD, RT)                                                                         \
+  hipLaunchKernelGGL((verify_wide_kernel<MD, RT>), dim3(grid), dim3(256), 0, st, qlist, count, KF, \
+                     M, (const RT*)X, xn, Q, qn, ld, ba, stats, lists.key, lists.id, lists.P,     \
+                     lists.KP, L, okey, oid, KP, fail, qinv, xinv, qr2i8, Dk, Ik, sizes, qcut)
+#define VS_WIDE(MD)             \
+  do {                          \
+    if (xesize == 4)            \
+      VS_WIDE_T(MD, float);     \
+    else                        \
+      VS_WIDE_T(MD, uint16_t);  \
+  } while (0)
   if (mode == MODE_IP)
     VS_WIDE(MODE_IP);
   else if (mode == MODE_L2)
@@ -2744,6 +2794,7 @@ hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int*
   else
     return hipErrorInvalidValue;
 #undef VS_WIDE
+#undef VS_WIDE_T
   return hipGetLastError();
 }
 

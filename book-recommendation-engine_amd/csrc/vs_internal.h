@@ -208,8 +208,9 @@ hipError_t launch_resid_norms(const float* X, int64_t ld, int64_t r0, int64_t n,
 // int8 filter plane of fp32 rows [r0, r0+n) (stride ld): codes (int8,
 // tile-major plane rows r0..), scale[r] = max|x_r| / 127 and, when rn2 != nullptr, rn2[r] = |x_r - scale
 // * code_r|^2 rounded up (+inf for a row with a non-finite element).
-hipError_t launch_quantize_i8(const float* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
-                              float* scale, float* rn2, hipStream_t st);
+// X: fp32 rows (xesize 4) or bf16 rows (xesize 2: a bf16 index's int8 plane).
+hipError_t launch_quantize_i8(const void* X, int64_t ld, int64_t r0, int64_t n, int8_t* codes,
+                              float* scale, float* rn2, hipStream_t st, int xesize = 4);
 // L2 as an inner product ("int8 L2"): ranking rows by the faiss
 // L2 key |q|^2 + |x|^2 - 2 q.x is ranking them by q.x + (nref - n_x) / 2 =
 // x'.q' with x' = [x, e_1 .. e_m], sum_j C e_j = (nref - n_x) / 2 (n_x the
@@ -275,12 +276,13 @@ hipError_t launch_mul_arrays(const float* a, const float* b, int64_t n, float* o
 // entries (okey/oid) and fail[q] = 1 where the exact engine must redo query q.
 // qsc: the queries' int8 scales (int8 filter; null for bf16).
 hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* Dk,
-                                 const int64_t* Ik, const float* X, const float* xn,
+                                 const int64_t* Ik, const void* X, const float* xn,
                                  const float* Q, const float* qn, int64_t ld, const BoundArgs& ba,
                                  const unsigned* stats, Partials lists, int L, float* okey,
                                  int* oid, int KP, int* fail, hipStream_t st,
                                  const float* qinv, const float* xinv, const float* qsc,
-                                 const int* qcount = nullptr, const float* qcut = nullptr);
+                                 const int* qcount = nullptr, const float* qcut = nullptr,
+                                 int xesize = 4);
 // Flagged queries (flags[i] != 0) -> ascending qlist[0 .. *count), all on the
 // device; *total += count and *total_n += n when not null.
 hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
@@ -320,13 +322,13 @@ hipError_t scratch_chunk_get(size_t bytes, hipStream_t st, ScratchChunk* out);
 void scratch_chunk_put(const ScratchChunk& c, hipStream_t st);
 void scratch_trim();
 hipError_t launch_verify_wide(int mode, int nq_max, const int* qlist, const int* count, int KF,
-                              int M, const float* X, const float* xn, const float* Q,
+                              int M, const void* X, const float* xn, const float* Q,
                               const float* qn, int64_t ld, const BoundArgs& ba,
                               const unsigned* stats, Partials lists, int L, float* okey, int* oid,
                               int KP, int* fail, hipStream_t st, const float* qinv,
                               const float* xinv, const float* qsc, const float* Dk,
                               const int64_t* Ik, unsigned long long* sizes = nullptr,
-                              const float* qcut = nullptr);
+                              const float* qcut = nullptr, int xesize = 4);
 // Query cuts and dump launches of the filter pass (vs_gemm_x1.hip, "Query
 // cuts"): bkey[q] = the verification's bound B of query q; x1_dump_applies:
 // the pass of this mode and plane has a dump form (launch_gemm_topk_x1 then
@@ -430,8 +432,11 @@ hipError_t launch_iota(int* out, int n, int* count, hipStream_t st);
 // Tombstones: rows[0 .. n) (device) filled with NaN elements and a NaN norm;
 // the labels I[0 .. n) of a search (kernel rows + id_base) mapped to positions
 // among the live rows (dead: the sorted tombstoned rows, ndead of them).
+// scale (optional): the int8 plane's row factors, set to NaN too (the plane's
+// keys of a tombstoned row are NaN and never enter a list).
 hipError_t launch_fill_nan_rows(void* X, int64_t rowbytes, float* norms, int esize,
-                                const int64_t* rows, int64_t n, hipStream_t st);
+                                const int64_t* rows, int64_t n, hipStream_t st,
+                                float* scale = nullptr);
 hipError_t launch_label_map(int64_t* I, int64_t n, const int64_t* dead, int64_t ndead,
                             int64_t id_base, hipStream_t st);
 hipError_t launch_gather_kept(const void* X, const float* norms, int64_t rowbytes, int64_t src0,

@@ -888,20 +888,24 @@ hipError_t launch_iota(int* out, int n, int* count, hipStream_t st) {
 // per row.
 __global__ __launch_bounds__(256) void fill_nan_rows_kernel(char* __restrict__ X, int64_t rowbytes,
                                                             float* __restrict__ norms, int esize,
-                                                            const int64_t* __restrict__ rows) {
+                                                            const int64_t* __restrict__ rows,
+                                                            float* __restrict__ scale) {
   const int64_t r = rows[blockIdx.x];
   uint32_t* p = (uint32_t*)(X + r * rowbytes);
   const uint32_t v = esize == 2 ? 0x7FC07FC0u : 0x7FC00000u;
   for (int64_t i = threadIdx.x; i < rowbytes / 4; i += 256) p[i] = v;
-  if (threadIdx.x == 0) norms[r] = __uint_as_float(0x7FC00000u);
+  if (threadIdx.x == 0) {
+    norms[r] = __uint_as_float(0x7FC00000u);
+    if (scale) scale[r] = __uint_as_float(0x7FC00000u);
+  }
 }
 
 hipError_t launch_fill_nan_rows(void* X, int64_t rowbytes, float* norms, int esize,
-                                const int64_t* rows, int64_t n, hipStream_t st) {
+                                const int64_t* rows, int64_t n, hipStream_t st, float* scale) {
   if (n <= 0) return hipSuccess;
   if (rowbytes % 4 != 0 || n > INT32_MAX) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fill_nan_rows_kernel, dim3((unsigned)n), dim3(256), 0, st, (char*)X, rowbytes,
-                     norms, esize, rows);
+                     norms, esize, rows, scale);
   return hipGetLastError();
 }
 

@@ -173,3 +173,51 @@ def test_bf16_tombstoned_removals(vf, metric, monkeypatch):
     for q, j in zip(*np.nonzero(diff)):
         assert abs(float(Sr[q, j]) - float(S[q, j])) < 1e-5
     assert index.ntotal == xr.shape[0]
+
+
+def test_bf16_int8_plane_small_batches(vf, monkeypatch):
+    """C5's path at reduced size: a bf16 inner-product index of 300,000 rows
+    keeps an int8 plane; batches of up to 32 queries run the small-batch filter
+    pass over it (1 B per element instead of the rows' 2) and the verification
+    rescores the stored bf16 values in fp64, so the answers are the exact
+    roundings (strict window) of the bf16 rows' scores.  Removals tombstone the
+    rows (their plane factors become NaN and never enter a list), appends
+    extend the plane, a large removal packs rows and plane together."""
+    from vsearch import _lib
+
+    monkeypatch.setenv("VS_PACK_DEN", "16")
+    d, n = 128, 300_000
+    rng = np.random.default_rng(21)
+    xb = rng.standard_normal((n, d)).astype(np.float32)
+    index = vf.IndexFlat(d, IP, dtype="bf16")
+    index.add(xb)
+    assert index.filter_planes == ("i8",)
+    xr = flat.round_bf16(xb)
+
+    def check(seed):
+        for nq in (1, 8, 32):
+            xq = _rand(nq, d, seed + nq)
+            rq = flat.round_bf16(xq)
+            _lib.filter_stats(reset=True)
+            D, I = index.search(xq, 10)
+            fq, _ = _lib.filter_stats(reset=True)
+            assert fq == nq, (nq, fq)  # the int8 plane's filter pass ran
+            Dr, Ir = flat.knn_exact(xr, rq, 10, IP)
+            bad = flat.mismatches(D, I, Dr, Ir, IP, xr, rq, strict=True)
+            assert not bad, (nq, bad[:3])
+
+    check(100)
+    for r in range(2):
+        rm = rng.choice(xr.shape[0], 3000, replace=False)  # tombstones (1 %)
+        assert index.remove_ids(rm) == 3000
+        xr, _ = flat.remove_ids(xr, rm)
+        add = _rand(2000, d, 200 + r)
+        index.add(add)
+        xr = np.concatenate([xr, flat.round_bf16(add)])
+        assert index.ntotal == xr.shape[0]
+        check(300 + r)
+    rm = np.arange(0, xr.shape[0], 9, dtype=np.int64)  # past 1/16: packs
+    assert index.remove_ids(rm) == rm.size
+    xr, _ = flat.remove_ids(xr, rm)
+    check(400)
+    np.testing.assert_array_equal(index.reconstruct_n(0, 1000), xr[:1000])

@@ -260,3 +260,20 @@ def test_cosine_selfjoin_dump_form(lib, monkeypatch):
     Sr, Ir = flat.pgvector_cosine_topk(x, 15, q_rows=rows)
     bad = flat.selfjoin_mismatches(S[rows], I[rows], Sr, Ir, x, rows, strict=True)
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("den,seg", [(8, "0"), (16, "1"), (32, "1")])
+def test_split_pass_segments(lib, monkeypatch, den, seg):
+    """Split passes (one launch per workgroup's tiles: 300,000 rows, 37 tiles
+    per split at the default 64-tile launches): a list launch over 1/den of
+    the tiles, then one dump launch, or (VS_X1_SPLITSEG=1) dump launches over
+    doubling part ranges with a replay after each.  Strict on the sample, no
+    list out of slots, nothing handed to the next stage."""
+    monkeypatch.setenv("VS_X1_CHUNK_TILES", "64")
+    monkeypatch.setenv("VS_X1_SPLIT", str(den))
+    monkeypatch.setenv("VS_X1_SPLITSEG", seg)
+    rng = np.random.default_rng(17)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (B, D_)).astype(np.float32)
+    dumps, over, fq, ff = _search_checked(lib, xb, xq, 10, engine="i8v")
+    assert fq == B and dumps > 0 and over == 0 and ff == 0, (dumps, over, ff)

@@ -10,7 +10,7 @@ for spec in "$@"; do
   name=${spec%%:*}; rest=${spec#*:}; envs=${rest%%:*}; args=""
   [ "$rest" != "$envs" ] && args=${rest#*:}
   env $envs timeout -k 10 300 python3 -u bench.py --steps 4 --warmup 1 --no-cpu-baseline \
-    --batch1-steps 0 --wide-k-steps 0 $args > "$OUT/$name.log" 2>&1
+    --batch1-steps 0 --wide-k-steps 0 --any-k 0 --clustered-steps 0 $args > "$OUT/$name.log" 2>&1
   rc=$?
   grep '^{' "$OUT/$name.log" | python3 -c "
 import json,sys
