@@ -480,7 +480,9 @@ struct X1SpanTimer : X1Timing {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
-int kp_for(int64_t k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : 128; }
+int kp_for(int64_t k) {
+  return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : k <= 128 ? 128 : 256;
+}
 
 int engine_from_env() {
   const char* e = getenv("VS_ENGINE");
@@ -1615,7 +1617,7 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
   // (past 64 candidates, inner product only: the last stage for what the
   // filter cannot settle is then the two-page exact engine, inner product's;
   // L2 / cosine with k > 56 keep the exact engine)
-  const int KF = x1_list_len(need) > 64 && mode != MODE_IP ? 0 : x1_list_len(need);
+  const int KF = x1_list_len(need);
   // the planes this search may run through: int8 first, then bf16; a forced
   // *_VERIFY engine runs its plane alone (an L2 index's int8 plane is the
   // augmented one: L2 searches only)
@@ -1626,9 +1628,17 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
                       (idx->l2aug() ? mode == MODE_L2 && idx->aug_m > 0 : true);
   const bool staged = idx->esize == 4 && engine != VS_ENGINE_FP32_MFMA && KF > 0 && ntotal > 0 &&
                       nq > kSkinnyMaxQ && (i8_ok || b16_ok);
+  // Small batches over a large index with a filter plane for the metric (inner
+  // product; L2 when faiss would take its BLAS branch): the staged engine with
+  // skinny passes (below)
+  const bool small_staged = small_filter_on() && (idx->esize == 4 || mode == MODE_IP) &&
+                            engine == VS_ENGINE_AUTO && KF > 0 && nq <= kSkinnyMaxQ &&
+                            a.self0 < 0 && ntotal >= kSmallFilterMinRows &&
+                            (mode == MODE_IP || mode == MODE_L2) && (i8_ok || b16_ok) &&
+                            small_l2d_ok(mode, a);
   // more entries than one exact page holds (inner product k > 32, raw k > 64)
-  // and no filter pass for them: the two-page exact engine
-  if (need > VS_MAX_K && !staged) return run_paged(idx, a, st);
+  // and no filter pass for them: the paged exact engine
+  if (need > VS_MAX_K && !staged && !small_staged) return run_paged(idx, a, st);
   const int KP = kp_for(need);
 
   // Small batches stream the corpus once.  fp32 L2 searches whose CALL has
@@ -1655,10 +1665,7 @@ int run_topk(vs_index* idx, const SearchArgs& a, hipStream_t st, int force_engin
   // fp32 bytes), candidates rescored and proven exactly as for large batches,
   // the few queries it cannot settle through the bf16 plane and the fp32
   // rows (skinny kernels too) — instead of streaming the fp32 rows.
-  if (small_filter_on() && (idx->esize == 4 || mode == MODE_IP) && engine == VS_ENGINE_AUTO &&
-      KF > 0 && KF <= 32 &&
-      nq <= kSkinnyMaxQ && a.self0 < 0 && ntotal >= kSmallFilterMinRows &&
-      (mode == MODE_IP || mode == MODE_L2) && (i8_ok || b16_ok) && small_l2d_ok(mode, a)) {
+  if (small_staged) {
     if (i8_ok && b16_ok) i8_ok = adaptive_use_i8(idx);
     if (i8_ok) return run_filter_verify(idx, a, need, KF, st, FILTER_I8, !b16_ok);
     return run_filter_verify(idx, a, need, KF, st, FILTER_BF16, false);

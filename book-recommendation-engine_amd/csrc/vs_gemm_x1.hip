@@ -1569,7 +1569,8 @@ int x1_list_len(int need) {
   return need + 8 <= 24   ? 24
          : need + 8 <= 32 ? 32
          : need + 8 <= 64 ? 64
-         : need < kVerifyMaxKF ? kVerifyMaxKF  // inner product k = 29 .. 64 (2k - 1 <= 127)
+         : need < 128 ? 128  // inner product k = 29 .. 64 (2k - 1 <= 127)
+         : need < kVerifyMaxKF ? kVerifyMaxKF  // inner product k = 65 .. 128, L2 k <= 255
                                : 0;
 }
 
@@ -2482,8 +2483,10 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
   do {                     \
     if (KF <= 64)          \
       VS_VERIFY(MD, 1);    \
-    else                   \
+    else if (KF <= 128)    \
       VS_VERIFY(MD, 2);    \
+    else                   \
+      VS_VERIFY(MD, 4);    \
   } while (0)
   if (mode == MODE_IP)
     VS_VERIFY_NE(MODE_IP);

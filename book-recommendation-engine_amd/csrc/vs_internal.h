@@ -299,8 +299,9 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // and the rescored ones.
 constexpr int kWideCap = 2048;
 // The most candidates (KF) the verification rescores per query, and the longest
-// exact list (KP) it writes: 128 holds inner product's 2k - 1 for k <= 64.
-constexpr int kVerifyMaxKF = 128;
+// exact list (KP) it writes: 256 holds inner product's 2k - 1 for k <= 128
+// (and k <= 255 for L2 / cosine); past it the paged exact engine answers.
+constexpr int kVerifyMaxKF = 256;
 // The KF (<= kVerifyMaxKF) lexicographically best (key, row) entries of every
 // query's P lane lists of L entries (stride part.KP), ascending, into Dk/Ik
 // [nq][KF] (the approximate merge when KF > 64; launch_merge_partials below).

@@ -230,12 +230,12 @@ __global__ __launch_bounds__(64) void emit_list_kernel(
     const float* __restrict__ pkey, const int* __restrict__ pid, int KP, int k, int mode, int raw,
     int64_t id_base, float min_score, float* __restrict__ D, int64_t* __restrict__ I,
     int64_t ldo, const int* __restrict__ qlist, const int* __restrict__ qcount) {
-  __shared__ float sk[128];
-  __shared__ int si[128];
+  __shared__ float sk[kVerifyMaxKF];
+  __shared__ int si[kVerifyMaxKF];
   const int lane = threadIdx.x;
   const int q = blockIdx.x;
   if (qcount && q >= *qcount) return;  // gathered batch: slots past the count
-  for (int j = lane; j < 128; j += 64) {
+  for (int j = lane; j < kVerifyMaxKF; j += 64) {
     sk[j] = j < KP ? pkey[(int64_t)q * KP + j] : FLT_MAX;
     si[j] = j < KP ? pid[(int64_t)q * KP + j] : -1;
   }
@@ -255,7 +255,7 @@ hipError_t launch_merge_partials(int mode, Partials part, int nq, int k, int64_t
     return hipErrorInvalidValue;
   if (nq == 0) return hipSuccess;
   if (part.KP > 64) {  // one sorted list per query only (the verification's output)
-    if (part.KP > 128 || part.P != 1 || (part.KL != 0 && part.KL != part.KP))
+    if (part.KP > kVerifyMaxKF || part.P != 1 || (part.KL != 0 && part.KL != part.KP))
       return hipErrorInvalidValue;
     hipLaunchKernelGGL(emit_list_kernel, dim3(nq), dim3(64), 0, st, part.key, part.id, part.KP, k,
                        mode, raw, id_base, min_score, D, I, ldo, qlist, qcount);

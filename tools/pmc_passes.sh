@@ -15,7 +15,7 @@ IFS=';' read -ra GROUPS_ <<< "${PMC_GROUPS:-$DEFAULT}"
 i=0
 for g in "${GROUPS_[@]}"; do
   timeout -k 10 -s KILL 300 rocprofv3 --pmc $g --output-format csv -d "$OUT/g$i" -o run \
-    -- python3 bench.py --steps 1 --warmup 0 --batch1-steps 0 --wide-k-steps 0 --no-cpu-baseline "$@" \
+    -- python3 bench.py --steps 1 --warmup 0 --batch1-steps 0 --wide-k-steps 0 --any-k 0 --clustered-steps 0 --no-cpu-baseline "$@" \
     > "$OUT/g$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
   i=$((i+1))
 done
