@@ -730,14 +730,18 @@ def run_knn(args, ctx):
             ok = bool((Ikh >= 0).all() and (Ikh < args.ntotal).all())
             ok &= bool((np.diff(Dkh, axis=1) <= 0).all() if metric == vfaiss.METRIC_INNER_PRODUCT
                        else (np.diff(Dkh, axis=1) >= 0).all())
+            kk = ctx.lib.timer_kernel()
+            staged = is_x1(kk) or kk.startswith("skinny_plane")
             anyk.append({"k": args.any_k, "batch": bk, "steps": steps,
                          "ms_per_search": round(tk / steps * 1e3, 3),
                          "queries_per_s": round(steps * bk / tk, 1),
-                         "kernel": ctx.lib.timer_kernel(),
+                         "kernel": kk,
                          "kernel_ms_per_search": round(kmk / steps, 3),
-                         "engine": "paged exact (vs_api.hip run_paged): ceil(k / 64) pages of "
-                                   "64 lexicographic entries, more where inner product's tie "
-                                   "rule needs them",
+                         "engine": ("staged filter and verify, up to 256 candidates per query "
+                                    "(inner product k <= 128, L2 k <= 255)" if staged else
+                                    "paged exact (vs_api.hip run_paged): ceil(k / 64) pages of "
+                                    "64 lexicographic entries, more where inner product's tie "
+                                    "rule needs them"),
                          "result_sane": ok})
 
     if ctx.rank == 0:
