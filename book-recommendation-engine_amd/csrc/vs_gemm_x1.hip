@@ -2872,6 +2872,8 @@ __global__ __launch_bounds__(256) void select_lists_kernel(const float* __restri
   __shared__ int wsum[4];
   __shared__ unsigned long long sel[kVerifyMaxKF];
   __shared__ int nsel;
+  __shared__ int hist[256];
+  __shared__ int sel_digit, sel_before;
   const int q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (qcount && q >= *qcount) return;  // gathered batch: slots past the count
@@ -2910,16 +2912,59 @@ __global__ __launch_bounds__(256) void select_lists_kernel(const float* __restri
   };
   const int total = count_le(kNone - 1);
   const int M = total < KF ? total : KF;
-  // the smallest y with M entries at or below it (bit by bit from the top)
+  // the M-th smallest image y, by a radix select over its eight bytes from the
+  // top: per byte a 256-bin histogram of the entries that share the bytes
+  // chosen so far, the bin where the running count reaches the rank left
+  // (8 passes over the entries instead of a bitwise search's 64: one query's
+  // select is one workgroup's latency, a batch-1 search waits for all of it)
   unsigned long long y = kNone - 1;
   if (M > 0 && M < total) {
-    unsigned long long x = 0;  // invariant: count_le(x - 1) < M
-    for (int b = 63; b >= 0; --b) {
-      const unsigned long long t = x + (1ull << b);
-      if (t - 1 < x) continue;  // overflow
-      if (count_le(t - 1) < M) x = t;
+    unsigned long long pre = 0;
+    int want = M;  // rank of y among the entries that share pre's chosen bytes
+    for (int sh = 56; sh >= 0; sh -= 8) {
+      hist[tid] = 0;  // 256 threads, 256 bins
+      __syncthreads();
+      auto add = [&](unsigned long long x) {
+        if (x != kNone && (sh == 56 || (x >> (sh + 8)) == (pre >> (sh + 8))))
+          atomicAdd(&hist[(int)((x >> sh) & 0xFF)], 1);
+      };
+      if (regs) {
+#pragma unroll
+        for (int i = 0; i < kR; ++i) add(v[i]);
+      } else {
+        for (int j = tid; j < n; j += 256) add(image(j));
+      }
+      __syncthreads();
+      if (wv == 0) {  // the bin where the running count reaches `want`
+        const int h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                  h3 = hist[4 * lane + 3];
+        const int own = h0 + h1 + h2 + h3;
+        int inc = own;  // inclusive prefix over the lanes
+        for (int o = 1; o < 64; o <<= 1) {
+          const int t = __shfl_up(inc, o);
+          if (lane >= o) inc += t;
+        }
+        const int before = inc - own;
+        if (before < want && want <= inc) {
+          int c = before, d = 4 * lane;
+          const int hh[4] = {h0, h1, h2, h3};
+          for (int e = 0; e < 4; ++e) {
+            if (c + hh[e] >= want) {
+              d = 4 * lane + e;
+              break;
+            }
+            c += hh[e];
+          }
+          sel_digit = d;
+          sel_before = c;
+        }
+      }
+      __syncthreads();
+      pre |= (unsigned long long)sel_digit << sh;
+      want -= sel_before;
+      __syncthreads();  // hist and the broadcast are rewritten by the next byte
     }
-    y = x;  // count_le(y - 1) < M <= count_le(y): y is the M-th smallest image
+    y = pre;  // the entries are distinct: y is the M-th smallest image
   }
   if (tid == 0) nsel = 0;
   __syncthreads();

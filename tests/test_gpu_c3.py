@@ -36,7 +36,8 @@ N, D_, K = 10_000_000, 1536, 10
 SAMPLE = sorted({q for t in range(16) for q in (256 * t, 256 * t + 37, 256 * t + 160,
                                                  256 * t + 255)})
 CL_SAMPLE = SAMPLE[::2] + [4095]  # clustered: 33 queries (m = 256 candidates each)
-KW = (30, 60)  # inner product's wide k (checked on the IP candidate sets, m = 256)
+KW = (30, 60, 100)  # inner product's wide k (checked on the IP candidate sets, m = 256)
+KW_L2 = (200,)  # L2 past one 64-entry page (the staged engine's 256 candidates)
 
 
 @pytest.fixture(scope="module")
@@ -55,14 +56,15 @@ def c3():
         Db, Ib = index.search(xq, K)  # batch 4096 (default engine)
         D1, I1 = index.search(xq[SAMPLE[-1]:SAMPLE[-1] + 1], K)  # batch 1
         wide = {}
-        if metric == flat.METRIC_INNER_PRODUCT:
-            # the service's wide searches (service.py:627 k = 30, :529 k = 60) at
-            # batch 4096: the filter pass with 64 / 128 candidates per query
-            for kw in KW:
-                wide[kw] = index.search(xq, kw)
-            cand = proven_candidates(index, xq[SAMPLE], metric, N, max(KW), m=256)
-        else:
-            cand = proven_candidates(index, xq[SAMPLE], metric, N, K)
+        # wide k at batch 4096 — the service's (service.py:627 k = 30, :529 k = 60:
+        # 64 / 128 candidates per query) and past one page (the agent's k,
+        # mcp_book_server.py:115,142: 256 candidates) — and at batch 1 (the skinny
+        # int8 pass with the same candidate counts)
+        kws = KW if metric == flat.METRIC_INNER_PRODUCT else KW_L2
+        for kw in kws:
+            wide[kw] = index.search(xq, kw)
+            wide[(kw, 1)] = index.search(xq[SAMPLE[-1]:SAMPLE[-1] + 1], kw)
+        cand = proven_candidates(index, xq[SAMPLE], metric, N, max(kws), m=256)
         out[metric] = (Db, Ib, D1, I1, cand, wide)
         del index
     return xq, out
@@ -127,16 +129,20 @@ def test_c3_batch1_against_oracle(c3, metric):
     assert (I1[0] == Ib[SAMPLE[-1]]).all() or metric == flat.METRIC_L2
 
 
-@pytest.mark.parametrize("kw", KW)
-def test_c3_wide_k_inner_product_against_oracle(c3, kw):
-    """k = 30 and k = 60 at batch 4096 (the filter pass with 64 and 128
-    candidates per query, faiss's tie rule over the 2k - 1 best): strict on the
-    64 sampled queries against their proven 256-row candidate sets."""
+@pytest.mark.parametrize("metric,kw", [(flat.METRIC_INNER_PRODUCT, k) for k in KW] +
+                         [(flat.METRIC_L2, k) for k in KW_L2])
+def test_c3_wide_k_against_oracle(c3, metric, kw):
+    """Inner product k = 30, 60 and 100 (the filter pass with 64, 128 and 256
+    candidates per query, faiss's tie rule over the 2k - 1 best) and L2 k = 200
+    at batch 4096, and the same k at batch 1: strict on the sampled queries
+    against their proven 256-row candidate sets."""
     xq, out = c3
-    _, _, _, _, cand, wide = out[flat.METRIC_INNER_PRODUCT]
+    _, _, _, _, cand, wide = out[metric]
     D, I = wide[kw]
     assert I.shape == (4096, kw) and (I >= 0).all() and (I < N).all()
-    assert (np.diff(D, axis=1) <= 0).all()
+    diffs = np.diff(D, axis=1)
+    assert (diffs <= 0).all() if metric == flat.METRIC_INNER_PRODUCT else (diffs >= 0).all()
     for row, q in enumerate(SAMPLE):
-        assert_against_candidates(D[q], I[q], cand[row], flat.METRIC_INNER_PRODUCT, kw, D_,
-                                  strict=True)
+        assert_against_candidates(D[q], I[q], cand[row], metric, kw, D_, strict=True)
+    D1, I1 = wide[(kw, 1)]
+    assert_against_candidates(D1[0], I1[0], cand[len(SAMPLE) - 1], metric, kw, D_, strict=True)
