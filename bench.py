@@ -737,8 +737,8 @@ def run_knn(args, ctx):
                          "queries_per_s": round(steps * bk / tk, 1),
                          "kernel": kk,
                          "kernel_ms_per_search": round(kmk / steps, 3),
-                         "engine": ("staged filter and verify, up to 256 candidates per query "
-                                    "(inner product k <= 128, L2 k <= 255)" if staged else
+                         "engine": ("staged filter and verify, up to 1024 candidates per query "
+                                    "(inner product k <= 512, L2 k <= 1023)" if staged else
                                     "paged exact (vs_api.hip run_paged): ceil(k / 64) pages of "
                                     "64 lexicographic entries, more where inner product's tie "
                                     "rule needs them"),

@@ -481,7 +481,14 @@ struct X1SpanTimer : X1Timing {
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 int kp_for(int64_t k) {
-  return k <= 8 ? 8 : k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : k <= 128 ? 128 : 256;
+  return k <= 8      ? 8
+         : k <= 16   ? 16
+         : k <= 32   ? 32
+         : k <= 64   ? 64
+         : k <= 128  ? 128
+         : k <= 256  ? 256
+         : k <= 512  ? 512
+                     : 1024;
 }
 
 int engine_from_env() {

@@ -1570,7 +1570,9 @@ int x1_list_len(int need) {
          : need + 8 <= 32 ? 32
          : need + 8 <= 64 ? 64
          : need < 128 ? 128  // inner product k = 29 .. 64 (2k - 1 <= 127)
-         : need < kVerifyMaxKF ? kVerifyMaxKF  // inner product k = 65 .. 128, L2 k <= 255
+         : need < 256 ? 256  // inner product k = 65 .. 128, L2 k <= 255
+         : need < 512 ? 512  // inner product k = 129 .. 256
+         : need < kVerifyMaxKF ? kVerifyMaxKF  // inner product k = 257 .. 512, L2 k <= 1023
                                : 0;
 }
 
@@ -2485,8 +2487,12 @@ hipError_t launch_verify_rescore(int mode, int nq, int KF, int M, const float* D
       VS_VERIFY(MD, 1);    \
     else if (KF <= 128)    \
       VS_VERIFY(MD, 2);    \
-    else                   \
+    else if (KF <= 256)    \
       VS_VERIFY(MD, 4);    \
+    else if (KF <= 512)    \
+      VS_VERIFY(MD, 8);    \
+    else                   \
+      VS_VERIFY(MD, 16);   \
   } while (0)
   if (mode == MODE_IP)
     VS_VERIFY_NE(MODE_IP);
@@ -2623,9 +2629,9 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
       bad = 0;
       eMs = FLT_MAX;
     }
-    if (tid < kVerifyMaxKF) {  // the first check's output for this query (KP entries)
-      rk[tid] = tid < KP ? okey[(int64_t)q * KP + tid] : FLT_MAX;
-      ri[tid] = tid < KP ? oid[(int64_t)q * KP + tid] : -1;
+    for (int t = tid; t < kVerifyMaxKF; t += 256) {  // the first check's output (KP entries)
+      rk[t] = t < KP ? okey[(int64_t)q * KP + t] : FLT_MAX;
+      ri[t] = t < KP ? oid[(int64_t)q * KP + t] : -1;
     }
     const float* qrow = Q + (int64_t)q * ld;
     if (wv == 0) {
@@ -2726,10 +2732,10 @@ __global__ __launch_bounds__(256) void verify_wide_kernel(
           put(j, r, wave_dot<MODE == MODE_L2D, RT>(X + (int64_t)r * ld, qrow, ld, lane));
         }
       }
-      if (tid < nk) {  // the reused exact keys after the rescored ones
-        ck[nu + tid] = kk[tid];
-        cid[nu + tid] = ki[tid];
-        if (!isfinite(kk[tid])) bad = 1;
+      for (int t = tid; t < nk; t += 256) {  // the reused exact keys after the rescored ones
+        ck[nu + t] = kk[t];
+        cid[nu + t] = ki[t];
+        if (!isfinite(kk[t])) bad = 1;
       }
       __syncthreads();
       if (!bad) {  // uniform
@@ -2857,11 +2863,11 @@ __device__ __forceinline__ float key_unorder(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
 
-// The KF = 128 best approximate candidates of each query (KF <= 64 goes through
-// merge_lists_kernel, whose register lists would not hold 128): one
+// The KF = 128 or 256 best approximate candidates of each query (KF <= 64 goes
+// through merge_lists_kernel, whose register lists would not hold 128): one
 // 256-thread workgroup per query finds the KF-th smallest 64-bit image
 // (key order << 32 | row; a query's lists hold distinct rows) of its P lists of
-// L entries by a bitwise search, keeps the entries at or below it and ranks
+// L entries by a radix select, keeps the entries at or below it and ranks
 // them.  Writes Dk/Ik [nq][KF] ascending (FLT_MAX / -1 padding).
 __global__ __launch_bounds__(256) void select_lists_kernel(const float* __restrict__ lkey,
                                                            const int* __restrict__ lid, int P,
@@ -2985,16 +2991,16 @@ __global__ __launch_bounds__(256) void select_lists_kernel(const float* __restri
   __syncthreads();
   float* dk = Dk + (int64_t)q * KF;
   int64_t* ik = Ik + (int64_t)q * KF;
-  if (tid < KF) {
-    if (tid < M) {
-      const unsigned long long x = sel[tid];
+  for (int t = tid; t < KF; t += 256) {
+    if (t < M) {
+      const unsigned long long x = sel[t];
       int rank = 0;
       for (int j = 0; j < M; ++j) rank += sel[j] < x ? 1 : 0;
       dk[rank] = key_unorder((uint32_t)(x >> 32));
       ik[rank] = (int64_t)(uint32_t)(x & 0xFFFFFFFFull);
     } else {
-      dk[tid] = FLT_MAX;
-      ik[tid] = -1;
+      dk[t] = FLT_MAX;
+      ik[t] = -1;
     }
   }
 }

@@ -297,11 +297,11 @@ hipError_t launch_compact_flags(const int* flags, int n, int* list, int* count,
 // okey/oid hold on entry the first check's exact keys of Ik (KP <= 64), which
 // are reused instead of read again.  sizes (optional): += the wide-set entries
 // and the rescored ones.
-constexpr int kWideCap = 2048;
+constexpr int kWideCap = 4096;
 // The most candidates (KF) the verification rescores per query, and the longest
-// exact list (KP) it writes: 256 holds inner product's 2k - 1 for k <= 128
-// (and k <= 255 for L2 / cosine); past it the paged exact engine answers.
-constexpr int kVerifyMaxKF = 256;
+// exact list (KP) it writes: 1024 holds inner product's 2k - 1 for k <= 512
+// (and k <= 1023 for L2 / cosine); past it the paged exact engine answers.
+constexpr int kVerifyMaxKF = 1024;
 // The KF (<= kVerifyMaxKF) lexicographically best (key, row) entries of every
 // query's P lane lists of L entries (stride part.KP), ascending, into Dk/Ik
 // [nq][KF] (the approximate merge when KF > 64; launch_merge_partials below).

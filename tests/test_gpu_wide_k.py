@@ -272,19 +272,18 @@ def test_any_k_large_sampled(vf, metric):
 
 @pytest.mark.parametrize("metric", [L2, IP])
 def test_staged_engine_past_64(vf, metric):
-    """k past one page through the staged filter-and-verify engine (up to 256
-    candidates per query: inner product k <= 128, L2 k <= 255): small batches
+    """k past one page through the staged filter-and-verify engine (up to 1024
+    candidates per query: inner product k <= 512, L2 k <= 1023): small batches
     over >= 2^18 rows (the int8 plane's skinny pass) and a large batch (the x1
     pass), STRICT parity on every query (the answers are exact roundings of
-    rescored scores), k = 100 and 200 (L2) / 100 (IP); k = 300 goes past the
-    staged engine to the paged one."""
+    rescored scores); k = 1100 goes past the staged engine to the paged one."""
     from vsearch import _lib
 
     n, d = 300_000, 64
     xb = _rand(n, d, 900)
     index = vf.IndexFlat(d, metric)
     index.add(xb)
-    ks = (100, 200) if metric == L2 else (65, 100)
+    ks = (100, 200, 700) if metric == L2 else (65, 100, 300)
     for nq in (1, 8, 300):
         xq = _rand(nq, d, 901 + nq)
         for k in ks:
@@ -296,5 +295,5 @@ def test_staged_engine_past_64(vf, metric):
             bad = flat.mismatches(D, I, Dr, Ir, metric, xb, xq, strict=True)
             assert not bad, (nq, k, bad[:3])
     xq = _rand(40, d, 999)
-    D, I = index.search(xq, 300)
-    _check(D, I, xb, xq, 300, metric)
+    D, I = index.search(xq, 1100)
+    _check(D, I, xb, xq, 1100, metric)
