@@ -1214,348 +1214,6 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
   }
 }
 
-// ---------------------------------------------------------------------------
-// The int8 inner-product dump launch over 320-row tiles (gemm_dump_s5).
-//
-// What bounds gemm_topk_x1's dump launch is its load segment: a step's four
-// LDS-DMA pieces per wave (each stalls its wave's issue for ~100-185 cycles,
-// MI355X_MICROARCH.md "LDS-DMA piece issue cost") plus twelve fragment reads
-// outlast the partner wave's 16 MFMAs (512 cycles): ~1,445 cycles per step for
-// 1,024 MFMA cycles (MFMA busy 0.71, profiles/r06c3).  This kernel keeps that
-// schedule (two waves per SIMD, load and matrix segments alternating between
-// the partners) and grows the tile along the rows: 320 rows x 256 queries, five
-// 32-row blocks per wave instead of four (160 accumulators of the ~250
-// registers a wave has at two per SIMD).  A matrix segment is 20 MFMAs (640
-// cycles) against a load segment of 4-5 pieces and 14 reads, and a step moves
-// 36 KB for 1.25x the MFMAs of the 32-KB step (10 % fewer bytes per MFMA).
-// (A one-wave-per-SIMD form with a 384 x 256 tile in 384 accumulators ran 9 %
-// slower per dispatch, profiles/r06w1: without a partner every piece's issue
-// stalls the MFMA stream.)
-//
-// Wave w: rows [160 (w & 1), +160) x queries [64 (w >> 1), +64) of the tile = 5
-// x 2 blocks of 32 x 32 (v_mfma_i32_32x32x32_i8); lane l sees query l & 31 of
-// each query block and rows 8 j + 4 (l >> 5) + e of each row block, so a lane
-// list is (query, split, row half w & 1, lane half l >> 5), as in gemm_topk_x1
-// (pl = 4 sp + 2 wr + h): the list launch, the cuts and x1_replay are shared.
-// Which lane list sees a row differs from gemm_topk_x1's (320-row tiles over
-// the 256-row storage tiles), which the verification does not care about: a
-// row is either below its list's floor (dumped, replayed into that list) or at
-// or above it, hence at or above the list's final last entry.
-//
-// A workgroup's database range is gemm_topk_x1's [t0, t1) storage tiles of its
-// split and launch part; it walks it in 320-row tiles u = positions [256 t0 +
-// 320 u, +320) (1.25 storage tiles).  Position g is slot g & 255 of storage
-// tile g >> 8, which holds row ((g >> 8) << 8) + ((g & 255) ^ tile_perm(g >>
-// 8)), gemm_topk_x1's permutation.  Positions past 256 t1 (the last tile of a
-// range that is not a multiple of 320 rows) re-read the range's last 16-row
-// group and are masked out; rows past ntotal likewise.
-//
-// Pieces per step: Q rows 32 w + 16 j (two per wave, as gemm_topk_x1), X
-// groups w + 8 p (p = 0, 1, and 2 for waves 0-3: 20 groups of 16 rows).  Ring
-// of 4 images of 36 KB, three steps in flight: the image a load segment
-// refills was read one barrier earlier by the lagging waves, so every load
-// segment ends with lgkmcnt(0) (its reads are long done by then: the pieces
-// follow them) before its barrier.
-constexpr int kS5Rows = 320;                  // database rows per tile
-constexpr int kS5Img = (kS5Rows + kT) * 64;   // one 64-B step of both operands: 36 KB
-constexpr int kS5Nbuf = 4;
-
-template <int KR>
-__global__ __launch_bounds__(512, 1) void gemm_dump_s5(
-    const char* __restrict__ XH, const char* __restrict__ QH, const float* __restrict__ qs, int nqa,
-    int nksteps, int ntotal, int ntiles, int nsplit, int nqt, int qtile0, int chunk, int chunk_end,
-    int nchunk, int KP, int qg, const float* __restrict__ pkey, const int* __restrict__ pid,
-    const float* __restrict__ xgmax, const float* __restrict__ xgmin, const float* __restrict__ qcut,
-    int* __restrict__ dcount, int* __restrict__ dslot, int dR) {
-  static_assert(kS5Nbuf * kS5Img <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[kS5Nbuf * kS5Img];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5;
-  const int c32 = lane & 31;
-  const int wr = w & 1;
-  const int wq = w >> 1;
-  const bool lag = w >= 4;  // one barrier behind waves 0-3 (their SIMD partners)
-
-  int qt, sp;
-  {  // gemm_topk_x1's XCD blocking (same grid: nqt x nsplit workgroups)
-    const int nblk = gridDim.x;
-    const int b = blockIdx.x;
-    const int qga = qg < 0 ? -qg : qg;
-    const int QG = nqt < qga ? nqt : qga;
-    const int G = nqt / QG;
-    const int S = nblk >> 3;
-    if ((nblk & 7) == 0 && nqt * nsplit == nblk && nqt % QG == 0 && G <= 8 && 8 % G == 0 &&
-        S % QG == 0) {
-      const int xcd = b & 7, slot = b >> 3, DG = S / QG;
-      qt = (xcd % G) * QG + slot % QG;
-      sp = (xcd / G) * DG + slot / QG;
-    } else if (qg > 0 && (nblk & 7) == 0 && nqt * nsplit == nblk && nqt % QG == 0 && G % 8 == 0) {
-      const int xcd = b & 7, slot = b >> 3, per = QG * nsplit;
-      const int gi = slot / per, rem = slot - gi * per;
-      qt = (gi * 8 + xcd) * QG + rem % QG;
-      sp = rem / QG;
-    } else {
-      const int xcd = b & 7, slot = b >> 3, qq = nblk >> 3, rr = nblk & 7;
-      const int lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
-      qt = lb % nqt;
-      sp = lb / nqt;
-    }
-  }
-  const int s0 = (int)((int64_t)sp * ntiles / nsplit);
-  const int s1 = (int)((int64_t)(sp + 1) * ntiles / nsplit);
-  const int t0 = s0 + (int)((int64_t)(s1 - s0) * chunk / nchunk);
-  const int t1 = s0 + (int)((int64_t)(s1 - s0) * chunk_end / nchunk);
-  const int P = nsplit * 4;
-  const int pl = sp * 4 + wr * 2 + h;
-
-  // per query block: the list's integer threshold for the launch and its
-  // running dump count (gemm_topk_x1's set_Tq: floor min(cut, last entry),
-  // the launch's largest / smallest row factor)
-  int Tq[2], dc[2];
-  {
-    float fm = 0.0f, fn = FLT_MAX;
-    for (int g = 16 * t0 + lane; g < 16 * t1; g += 64) {
-      fm = fmaxf(fm, xgmax[g]);
-      fn = fminf(fn, xgmin[g]);
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      fm = fmaxf(fm, __shfl_xor(fm, m));
-      fn = fminf(fn, __shfl_xor(fn, m));
-    }
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int gq = qt * kT + 64 * wq + 32 * qb + c32;
-      const int64_t o = ((int64_t)gq * P + pl) * KP + KR - 1;
-      float tl = qcut[gq];
-      if (pid[o] >= 0) tl = fminf(tl, pkey[o]);
-      const float last = gq < nqa ? tl : -FLT_MAX;
-      const float qsc = gq < nqa ? qs[gq] : 0.0f;
-      const float c = qsc * fm, cn = qsc * fn;
-      Tq[qb] = (c > 0.0f && -last >= 0.0f)                    ? i8_threshold(-last, c)
-               : (cn > 0.0f && cn <= FLT_MAX && -last < 0.0f) ? min(i8_threshold(-last, cn), -1)
-               : (c > 0.0f || -0.0f < last)                   ? INT_MIN
-                                                              : INT_MAX;
-      dc[qb] = dcount[(int64_t)gq * P + pl];
-      asm volatile("" ::"v"(Tq[qb]), "v"(dc[qb]));
-    }
-  }
-
-  const int gbeg = t0 * kT, gend = t1 * kT;  // the range's positions
-  const int nu = (gend - gbeg + kS5Rows - 1) / kS5Rows;
-  // The step loop per wave group (waves 0-3 stage three database pieces per
-  // step, waves 4-7 two): the group is a template tag, so a step carries no
-  // branch on it — every instruction of the load segment counts (a uniform
-  // branch per piece cost 11 % of a dispatch, profiles/r06nt).
-  auto body = [&](auto lag_tag) {
-    constexpr bool LAG = decltype(lag_tag)::value;
-    constexpr int NPX = LAG ? 2 : 3;  // database pieces per step
-    const uint32_t lds0 = (uint32_t)(uintptr_t)VS_LDS(smem);
-    // DMA lane offset inside a 16-row piece: row lane >> 2, 16-B chunk swizzled
-    // by the LDS row (chunk c of LDS row r at c ^ ((r >> 2) & 3))
-    const uint32_t soff = (uint32_t)(lane >> 2) * 64u + (uint32_t)((lane & 3) ^ (lane >> 4)) * 16u;
-
-    // Load cursor (tile lu, K-step lk, image lbuf): the X pieces' sources
-    // (groups w + 8 p of the tile) and the Q step.  It never stops: past the
-    // last tile its X positions lie past the range (re-reads of the range's
-    // last group, clamped) and its Q steps are the query tile's, so the three
-    // steps it runs ahead of the last one stay in bounds.
-    int lu = 0, lk = 0, lbuf = 0;
-    const char* xb[NPX];
-    uint32_t xl[NPX];
-    const char* const qtile = QH + (int64_t)(qtile0 + qt) * nksteps * 16384 + (uint32_t)(32 * w) * 64u;
-    const char* qstep = qtile;
-    auto set_tile = [&](int u) {
-      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-#pragma unroll
-      for (int p = 0; p < NPX; ++p) {
-        int g = gbeg + kS5Rows * u + 16 * (w + 8 * p);
-        if (g >= gend) g = gend - 16;
-        const int T = g >> 8;
-        const int f = tile_perm(T);
-        xb[p] = XH + (int64_t)T * nksteps * 16384 + (uint32_t)((g & 255) ^ (f & 0xF0)) * 64u;
-        xl[p] = (uint32_t)((ln >> 2) ^ (f & 0x0C)) * 64u + (uint32_t)((ln & 3) ^ (ln >> 4)) * 16u;
-      }
-    };
-    set_tile(0);
-    auto advance = [&]() {
-      if (__builtin_expect(++lk == nksteps, 0)) {
-        lk = 0;
-        set_tile(++lu);
-        qstep = qtile;
-      } else {
-#pragma unroll
-        for (int p = 0; p < NPX; ++p) xb[p] += 16384;
-        qstep += 16384;
-      }
-      lbuf = (lbuf + 1) & (kS5Nbuf - 1);
-    };
-    // the step's pieces in one asm statement (M0 saved once, set per piece;
-    // no instruction offsets: an LDS-DMA adds its offset to the LDS address too)
-    auto stage_step = [&]() {
-      const uint32_t lx = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)lbuf * kS5Img + (uint32_t)w * 1024u);
-      const uint32_t lq =
-          __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)lbuf * kS5Img + (uint32_t)(kS5Rows * 64 + 2 * w * 1024));
-      uint32_t keep;
-      if constexpr (NPX == 3) {
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %4\n\t"
-            "s_add_u32 m0, %1, 0x2000\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %6\n\t"
-            "s_add_u32 m0, %1, 0x4000\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %7, %8\n\t"
-            "s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %9, %10\n\t"
-            "s_add_u32 m0, %2, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %9, %11\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(lx), "s"(lq), "v"(xl[0]), "s"(xb[0]), "v"(xl[1]), "s"(xb[1]), "v"(xl[NPX - 1]),
-              "s"(xb[NPX - 1]), "v"(soff), "s"(qstep), "s"(qstep + 1024)
-            : "memory");
-      } else {
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %4\n\t"
-            "s_add_u32 m0, %1, 0x2000\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %6\n\t"
-            "s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %7, %8\n\t"
-            "s_add_u32 m0, %2, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %7, %9\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(lx), "s"(lq), "v"(xl[0]), "s"(xb[0]), "v"(xl[1]), "s"(xb[1]), "v"(soff),
-              "s"(qstep), "s"(qstep + 1024)
-            : "memory");
-      }
-      static_assert(kS5Img % 1024 == 0 && 8 * 1024 == 0x2000, "stage_step's M0 offsets");
-    };
-
-    i32x16 acc[5][2];
-    uint4 fa0[5], fb0[2], fa1[5], fb1[2];
-    const int fsw = (c32 >> 2) & 3;
-    auto rd = [&](int buf, int s2, uint4 (&fa)[5], uint4 (&fb)[2]) {
-      const char* base = smem + buf * kS5Img;
-      const int co = ((2 * s2 + h) ^ fsw) * 16;
-      const char* cX = base + (160 * wr + c32) * 64 + co;
-      const char* cQ = base + kS5Rows * 64 + (64 * wq + c32) * 64 + co;
-      fb[0] = *(const uint4*)cQ;
-      fb[1] = *(const uint4*)(cQ + 32 * 64);
-#pragma unroll
-      for (int rb = 0; rb < 5; ++rb) fa[rb] = *(const uint4*)(cX + rb * 32 * 64);
-    };
-
-    // prologue: steps 0, 1, 2 in flight; this wave's pieces of step 0 retired
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      stage_step();
-      advance();
-    }
-    if constexpr (LAG) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if constexpr (LAG) __builtin_amdgcn_s_barrier();  // one barrier behind
-    int buf = 0;
-
-    auto step = [&](auto first_tag) {
-      constexpr bool first = decltype(first_tag)::value;
-      // load segment: both sub-steps' fragments, the pieces of step s+3, the
-      // wait for this wave's pieces of step s+1 (steps s+2, s+3 stay in flight)
-      // and for its reads (the lagging waves refill next the image read here)
-      __builtin_amdgcn_sched_barrier(0);
-      rd(buf, 0, fa0, fb0);
-      rd(buf, 1, fa1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      stage_step();
-      advance();
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (LAG) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // matrix segment
-#pragma unroll
-      for (int rb = 0; rb < 5; ++rb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          if constexpr (first) {
-            const i32x16 z = {};
-            acc[rb][qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(fa0[rb]), as_i4(fb0[qb]), z, 0, 0, 0);
-          } else {
-            acc[rb][qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(fa0[rb]), as_i4(fb0[qb]),
-                                                                acc[rb][qb], 0, 0, 0);
-          }
-        }
-#pragma unroll
-      for (int rb = 0; rb < 5; ++rb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-          acc[rb][qb] =
-              __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(fa1[rb]), as_i4(fb1[qb]), acc[rb][qb], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      buf = (buf + 1) & (kS5Nbuf - 1);
-    };
-
-    for (int u = 0; u < nu; ++u) {
-      step(std::true_type{});
-      for (int k = 1; k < nksteps; ++k) step(std::false_type{});
-      // the tile's epilogue, beside the partner's matrix segment: blocks with
-      // a sum above the list's threshold, then (rare) their rows
-      uint32_t pass = 0;
-#pragma unroll
-      for (int rb = 0; rb < 5; ++rb)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          int amax = acc[rb][qb][0];
-#pragma unroll
-          for (int r = 1; r < 16; ++r) amax = max(amax, acc[rb][qb][r]);
-          pass |= (uint32_t)(amax > Tq[qb]) << (2 * rb + qb);
-        }
-      if (__ballot(pass != 0) != 0) {  // uniform: rare
-        const int pos0 = gbeg + kS5Rows * u + 160 * wr + 4 * h;
-#pragma unroll
-        for (int rb = 0; rb < 5; ++rb)
-#pragma unroll
-          for (int qb = 0; qb < 2; ++qb) {
-            if (!(pass & (1u << (2 * rb + qb)))) continue;
-            uint32_t cm = 0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cm |= (uint32_t)(acc[rb][qb][r] > Tq[qb]) << r;
-            while (cm) {
-              const int bi = __builtin_ctz(cm);
-              cm &= cm - 1;
-              const int g = pos0 + 32 * rb + 8 * (bi >> 2) + (bi & 3);
-              if (g >= gend) continue;
-              const int T = g >> 8;
-              const int row = (T << 8) + ((g & 255) ^ tile_perm(T));
-              if (row >= ntotal) continue;
-              const int c = dc[qb]++;
-              if (c < dR) {
-                const int gq = qt * kT + 64 * wq + 32 * qb + c32;
-                const int64_t slot = (int64_t)c * ((int64_t)nqt * kT * P) + (int64_t)gq * P + pl;
-                *(i32x2*)(dslot + slot * 2) = i32x2{row, sel16i(acc[rb][qb], bi)};
-              }
-            }
-          }
-      }
-    }
-    if constexpr (!LAG) __builtin_amdgcn_s_barrier();  // the lagging waves' extra one
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain before the workgroup exits
-  };
-  if (nu > 0) {  // uniform
-    if (lag) body(std::true_type{});
-    else body(std::false_type{});
-  }
-  // the list offsets from the lane id again (not kept live across the main
-  // loop: registers)
-  const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int gq = qt * kT + 64 * wq + 32 * qb + (ln & 31);
-    dcount[(int64_t)gq * P + sp * 4 + wr * 2 + (ln >> 5)] = dc[qb];
-  }
-}
-
 // The replay of a segment of dump launches: one thread per lane list (query
 // q, list pl = 4 sp + 2 wr + h).  The list as the previous launches left it,
 // then every row dumped since in dump order (the order the lane met them:
@@ -1710,12 +1368,6 @@ constexpr int kSplitMinTiles = 16;
 // pass -1 %, profiles/r05u)
 // VS_X1_QUARTER=<F>: the list launch covers 1/F of the first chunk (0: off,
 // 1: 1/4 as F = 4)
-// The int8 inner-product dump launches over 320-row tiles (gemm_dump_s5; env
-// VS_X1_S5=0 keeps gemm_topk_x1's dump form, for A/B; read at every search)
-static bool x1_s5_on() {
-  const char* e = getenv("VS_X1_S5");
-  return !e || atoi(e) != 0;
-}
 static int x1_first_den(int el) {
   const char* e = getenv("VS_X1_QUARTER");
   if (!e) return el == FILTER_BF16 ? 4 : 0;
@@ -1786,13 +1438,7 @@ static hipError_t x1_launch(const X1Args& a, Partials part, hipStream_t st, int*
     // launches dump is timed apart ("<name>_list")
     if (a.timing)
       a.timing->begin(st, !(later_dump && nlaunch > 1) || c > 0, (double)(p1 - p0) / nparts);
-    if (later_dump && c > 0 && MODE == MODE_IP && EL == FILTER_I8 && !a.qrow && a.self0 < 0 &&
-        x1_s5_on()) {
-      hipLaunchKernelGGL((gemm_dump_s5<KR>), dim3(nqt * a.nsplit), dim3(512), 0, st,
-                         (const char*)a.XH, (const char*)a.QH, a.qs, a.nqa, (int)(ldb / 64), a.ntotal,
-                         ntiles, a.nsplit, nqt, a.qtile0, p0, p1, nparts, part.KP, qg, part.key,
-                         part.id, a.xgmax, a.xgmin, a.qcut, a.dcount, a.dslot, a.dR);
-    } else if (later_dump && c > 0) {
+    if (later_dump && c > 0) {
       if constexpr (x1_has_dump(MODE, EL))
         hipLaunchKernelGGL((gemm_topk_x1<KR, MODE, true, EL>), dim3(nqt * a.nsplit), dim3(512), 0,
                            st, (const char*)a.XH, a.xs, a.xaux, (const char*)a.QH, a.qs, a.qaux,
