@@ -924,6 +924,19 @@ bool skinny_deep_on() {
   return !e || atoi(e) != 0;
 }
 
+// Workgroups per filter-pass launch the database splits aim at: one round (256,
+// one per CU) for batches of at most 8 query tiles, whose lane lists stay at
+// 128+ per query (C2, 4 query tiles: 256 lists, 405-407k -> 436-441k
+// queries/s, profiles/r06wgs); two rounds (512) above, where one round would
+// cut the lists to 64 per query and saturate some (the 1.25M-row rank of an
+// 8-GPU C3: 11 queries per search to the deep stage, 441k -> 423k).  Env
+// VS_X1_WGS overrides (A/B; read at every search).
+static int x1_wg_target(int nqt) {
+  const char* e = getenv("VS_X1_WGS");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : nqt <= 8 ? 256 : 512;
+}
+
 int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
                       int plane, bool last_plane, bool deep = false, const int* gl = nullptr,
                       const int* gc = nullptr) {
@@ -939,8 +952,8 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const int L = x1_lane_len();
   // enough lists that their 4*nsplit*L entries cover 16*KF candidates (C4's
   // self-join, KF = 64: 128 lists, which lets the int8 stage settle it: 283k ->
-  // 372k students/s, profiles/r02zc), and two workgroups per CU on 256 CUs: 128
-  // lists per query at C3.  More lists put
+  // 372k students/s, profiles/r02zc), and the workgroup target below (two per
+  // CU on 256 CUs at C3: 128 lists per query; one per CU up to 8 query tiles).  More lists put
   // the wide check's floor T (the best last entry of a full list) deeper
   // behind the top-M, which the bound needs on clustered data and on the int8
   // plane (profiles/r02l_ab_split.txt; one workgroup per CU left 0.7 % of the
@@ -951,9 +964,10 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   // however few they are); with 8 KF / L lists 0 and 26 (60.5 vs 78.9 and 85.9
   // vs 94.2 ms per search, profiles/r05q, VS_X1_SPLIT_MULT=2)
   const int lists_per_cand = mode == MODE_IP && KF >= 64 ? 8 : 4;
+  const int wg_target = x1_wg_target(nqt);
   x.nsplit = (int)std::max<int64_t>(
       std::min<int64_t>(ntiles, lists_per_cand * ((KF + L - 1) / L)),
-      std::min<int64_t>(ntiles, (512 + nqt - 1) / nqt));
+      std::min<int64_t>(ntiles, (wg_target + nqt - 1) / nqt));
   // the deep stage (a gathered batch of the few queries an earlier stage could
   // not settle): as many lists as two workgroups per CU give ONE query tile, so
   // the floors sit far behind the top (the a_M + 2B threshold keeps the wide
@@ -1502,7 +1516,15 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
   const bool l2d = a.mode == MODE_L2 && a.l2_direct && idx->esize == 4 && gemv_fits && a.self0 < 0;
   const bool gemv = !gathered && a.self0 < 0 && idx->esize == 4 && gemv_fits &&
                     (l2d || (a.mode == MODE_IP && a.nq <= 2));
-  const int pmode = l2d ? MODE_L2D : a.mode;
+  // The staged engine's last stage (gathered, fp32 rows): the pages are the
+  // exact-key stream's (vs_exact.hip, floored), every key the rescoring's own
+  // (fp64 sums of the exact products, one rounding), so what no filter stage
+  // settled is answered strictly like the rest (inner product k > 32, L2 k >
+  // 56), not with the fp32 GEMM's keys.  Env VS_EXACT_STREAM=0 keeps the GEMM
+  // pages (A/B).
+  const bool xpages =
+      gathered && idx->esize == 4 && a.self0 < 0 && exact_stream_on() && exact_stream_nq(idx->ld) > 0;
+  const int pmode = l2d || (xpages && a.mode == MODE_L2 && a.l2_direct) ? MODE_L2D : a.mode;
   // query windows: GEMV groups of up to 8, else pages of at most ~2 GB
   int64_t W = a.nq;
   if (gemv) {
@@ -1537,6 +1559,13 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
     VS_HIP(scr.alloc((void**)&part.id, (size_t)kGemvMaxQ * part.P * 64 * sizeof(int)),
            "vs: scratch");
     VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
+  } else if (xpages) {
+    part.P = (int)std::min<int64_t>(256, std::max<int64_t>(1, ((int64_t)ntotal + 1023) / 1024));
+    VS_HIP(scr.alloc((void**)&part.key, (size_t)kExactSlots * part.P * 64 * sizeof(float)),
+           "vs: scratch");
+    VS_HIP(scr.alloc((void**)&part.id, (size_t)kExactSlots * part.P * 64 * sizeof(int)),
+           "vs: scratch");
+    VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
   } else {
     const int ntiles = (ntotal + kBN - 1) / kBN;
     nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, 256));
@@ -1564,7 +1593,10 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
     }
     VS_HIP(launch_page_init(nw, gemv ? kGemvMaxQ : nw, gl, gc, member, active, fkey, fid, st),
            "vs: pages");
-    VS_HIP(launch_compact_flags(active, nw, qlist, qcount, nullptr, nullptr, st), "vs: pages");
+    // (exact-key pages: their queries count as the exact stream's, vs_filter_exact_stats)
+    unsigned long long* xst = xpages ? device_stats(idx->device) : nullptr;
+    VS_HIP(launch_compact_flags(active, nw, qlist, qcount, xst ? xst + 8 : nullptr, nullptr, st),
+           "vs: pages");
     for (int64_t p = 0; p < npages; ++p) {
       if (p > 0) {
         VS_HIP(launch_page_step(Dacc, Iacc, KA, (int)p - 1, nw, a.k, rule ? 1 : 0, pmode, active,
@@ -1582,6 +1614,30 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
         VS_HIP(launch_merge_partials(pmode, part, nw, 64, 0, -INFINITY, Dacc + p * 64,
                                      Iacc + p * 64, KA, st, 1, nullptr, wc),
                "vs: merge launch");
+        continue;
+      }
+      if (xpages) {  // the active queries in launches of kExactSlots (past the count: exit)
+        ExactStreamArgs ea;
+        ea.X = (const float*)idx->codes;
+        ea.xn = idx->norms;
+        ea.xinv = a.mode == MODE_COS ? a.xaux : nullptr;
+        ea.ld = idx->ld;
+        ea.ntotal = ntotal;
+        ea.Q = qf;
+        ea.qaux = qaux;
+        ea.slots = qlist;
+        ea.count = qcount;
+        ea.nslot = kExactSlots;
+        ea.fkey = fkey;
+        ea.fid = fid;
+        for (int s0 = 0; s0 < nslot; s0 += kExactSlots) {
+          ea.s0 = s0;
+          VS_HIP(launch_window_count(qcount, s0, kExactSlots, wc, st), "vs: window");
+          VS_HIP(launch_exact_stream(64, pmode, ea, part, st), "vs: exact stream");
+          VS_HIP(launch_merge_partials(pmode, part, kExactSlots, 64, 0, -INFINITY, Dacc + p * 64,
+                                       Iacc + p * 64, KA, st, 1, qlist + s0, wc),
+                 "vs: merge launch");
+        }
         continue;
       }
       for (int w0 = 0; w0 < nslot; w0 += cap) {

@@ -14,6 +14,11 @@
 // the wave reduces by xor-shuffles 32 .. 1: wave_dot's order, so a row's key is
 // bit-identical to the one verify_rescore gives it.
 //
+// With a floor per query (fkey / fid: the paged engine's previous page) it is
+// the exact-key form of a page: the staged engine's last stage past 64
+// candidates (vs_api.hip run_paged, gathered) pages each query's order of exact
+// keys 64 entries at a time.
+//
 // Layout: one workgroup per block of rows (4 waves, each wave 4 rows at a
 // time, lane l reading chunk l of each: 1 KiB per wave instruction, coalesced),
 // persistent over the gathered queries in groups of NQ (their rows staged in
@@ -30,7 +35,7 @@ __global__ __launch_bounds__(256) void exact_stream_topk(
     int rows_per_block, const float* __restrict__ Q, const float* __restrict__ qaux,
     const int* __restrict__ qrow, const float* __restrict__ xinv, const int* __restrict__ slots,
     const int* __restrict__ count, int s0, int nslot, float* __restrict__ pkey,
-    int* __restrict__ pid) {
+    int* __restrict__ pid, const float* __restrict__ fkey, const int* __restrict__ fid) {
   extern __shared__ __attribute__((aligned(16))) float sq[];  // [NQ][ld], then list merge
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -57,9 +62,17 @@ __global__ __launch_bounds__(256) void exact_stream_topk(
     const int sl = jq < n ? slots[s0 + jq] : 0;
     float qa = 0.0f;
     int self = -1;
+    // a page's floor (the paged engine): only entries lexicographically after
+    // the previous page's last one enter; none: (-inf, -1)
+    float fk = -INFINITY;
+    int fi = -1;
     if (lane < NQ && jq < n) {
       if constexpr (MODE == MODE_L2 || MODE == MODE_COS) qa = qaux[sl];
       if (qrow) self = qrow[sl];
+      if (fkey) {
+        fk = fkey[sl];
+        fi = fid[sl];
+      }
     }
     float lk[KP];
     int li[KP];
@@ -115,7 +128,7 @@ __global__ __launch_bounds__(256) void exact_stream_topk(
           } else {
             key = ip;  // the rounded exact sum of (x - q)^2
           }
-          list_insert<KP, int>(lk, li, key, row);
+          if (lex_less(fk, fi, key, row)) list_insert<KP, int>(lk, li, key, row);
         }
       }
     }
@@ -160,7 +173,7 @@ static hipError_t exact_dispatch_mode(int mode, const ExactStreamArgs& a, Partia
 #define VS_EXACT(MD)                                                                            \
   hipLaunchKernelGGL((exact_stream_topk<NQ, KP, MD>), dim3(part.P), dim3(256), lds, st, a.X,     \
                      a.xn, a.ld, a.ntotal, rpb, a.Q, a.qaux, a.qrow, a.xinv, a.slots, a.count,  \
-                     a.s0, a.nslot, part.key, part.id)
+                     a.s0, a.nslot, part.key, part.id, a.fkey, a.fid)
   switch (mode) {
     case MODE_IP:
       VS_EXACT(MODE_IP);

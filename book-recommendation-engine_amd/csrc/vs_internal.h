@@ -375,6 +375,10 @@ struct ExactStreamArgs {
   const int* slots = nullptr;
   const int* count = nullptr;
   int s0 = 0, nslot = 0;
+  // per query (indexed like slots' entries): only entries lexicographically
+  // after (fkey, fid) enter (a page of the paged engine); null: no floor
+  const float* fkey = nullptr;
+  const int* fid = nullptr;
 };
 int exact_stream_nq(int64_t ld);
 hipError_t launch_exact_stream(int KP, int mode, const ExactStreamArgs& a, Partials part,

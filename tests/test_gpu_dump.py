@@ -158,6 +158,33 @@ def test_dense_near_ties_reach_the_exact_stream(lib, engine):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("k", [40, 100])
+def test_dense_near_ties_past_32_exact_pages(lib, k):
+    """The same near-ties at inner product k = 40 / 100 (79 / 199 candidates,
+    past the 64 that one exact page holds): what no filter stage settles runs
+    the paged engine over exact-key pages (vs_exact.hip with a floor per query:
+    every key the rescoring's own) instead of the fp32 GEMM's
+    pages, so the answer is STRICT here too."""
+    from vsearch import faiss as vfaiss
+
+    rng = np.random.default_rng(78)
+    xb = rng.uniform(-1, 1, (N, D_)).astype(np.float32)
+    dup = rng.uniform(-1, 1, D_).astype(np.float32)
+    pos = np.sort(rng.choice(N, 150_000, replace=False))
+    xb[pos] = dup[None, :] * (1.0 + 1e-3 * pos[:, None] / N).astype(np.float32)
+    xq = (dup[None, :] + 0.3 * rng.uniform(-1, 1, (B, D_))).astype(np.float32)
+    index = vfaiss.IndexFlat(D_, IP)
+    index.add(xb)
+    lib.filter_stats(reset=True)
+    D, I = index.search(xq, k)
+    streamed = lib.filter_exact_stats()
+    lib.filter_stats(reset=True)
+    assert streamed > 0
+    Dr, Ir = flat.knn_exact(xb, xq[SAMPLE], k, IP)
+    bad = flat.mismatches(D[SAMPLE], I[SAMPLE], Dr, Ir, IP, xb, xq[SAMPLE], strict=True)
+    assert not bad, bad[:5]
+
+
 def test_dump_launches_queries_pointing_away(lib):
     """Every inner product below 0 (rows in [0, 1), queries in [-1, 0)): the
     lists' floors are above 0, where the largest row factor bounds nothing (a
