@@ -1260,6 +1260,7 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
 // Slots of the exact-key stream per launch (its lists: kExactSlots x up to
 // 256 row blocks x KP entries); launches past the device-side count exit.
 constexpr int kExactSlots = 256;
+constexpr int kXPageSlots = 1024;  // run_paged's exact-key pages
 bool exact_stream_on() {
   const char* e = getenv("VS_EXACT_STREAM");
   return !e || atoi(e) != 0;
@@ -1550,7 +1551,7 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
   // the page kernels' partial lists
   Partials part;
   part.KP = 64;
-  int nsplit = 1, cap = 0;
+  int nsplit = 1, cap = 0, xslots = 0;
   int* wc = nullptr;
   if (gemv) {
     part.P = (int)std::min<int64_t>(2048, std::max<int64_t>(1, (ntotal + 255) / 256));
@@ -1560,10 +1561,15 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
            "vs: scratch");
     VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
   } else if (xpages) {
+    // slots per exact-page launch: the whole gathered batch up to 1,024 (its
+    // lists: 1,024 x 256 row blocks x 64 entries = 134 MB), so a page of a
+    // 4,096-query search is 4 launch triples, not 16 (they run every search,
+    // usually over an empty count)
     part.P = (int)std::min<int64_t>(256, std::max<int64_t>(1, ((int64_t)ntotal + 1023) / 1024));
-    VS_HIP(scr.alloc((void**)&part.key, (size_t)kExactSlots * part.P * 64 * sizeof(float)),
+    xslots = (int)std::min<int64_t>(kXPageSlots, round_up(std::max(a.nq, 1), kBQ));
+    VS_HIP(scr.alloc((void**)&part.key, (size_t)xslots * part.P * 64 * sizeof(float)),
            "vs: scratch");
-    VS_HIP(scr.alloc((void**)&part.id, (size_t)kExactSlots * part.P * 64 * sizeof(int)),
+    VS_HIP(scr.alloc((void**)&part.id, (size_t)xslots * part.P * 64 * sizeof(int)),
            "vs: scratch");
     VS_HIP(scr.alloc((void**)&wc, sizeof(int)), "vs: scratch");
   } else {
@@ -1627,14 +1633,14 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
         ea.qaux = qaux;
         ea.slots = qlist;
         ea.count = qcount;
-        ea.nslot = kExactSlots;
+        ea.nslot = xslots;
         ea.fkey = fkey;
         ea.fid = fid;
-        for (int s0 = 0; s0 < nslot; s0 += kExactSlots) {
+        for (int s0 = 0; s0 < nslot; s0 += xslots) {
           ea.s0 = s0;
-          VS_HIP(launch_window_count(qcount, s0, kExactSlots, wc, st), "vs: window");
+          VS_HIP(launch_window_count(qcount, s0, xslots, wc, st), "vs: window");
           VS_HIP(launch_exact_stream(64, pmode, ea, part, st), "vs: exact stream");
-          VS_HIP(launch_merge_partials(pmode, part, kExactSlots, 64, 0, -INFINITY, Dacc + p * 64,
+          VS_HIP(launch_merge_partials(pmode, part, xslots, 64, 0, -INFINITY, Dacc + p * 64,
                                        Iacc + p * 64, KA, st, 1, qlist + s0, wc),
                  "vs: merge launch");
         }
