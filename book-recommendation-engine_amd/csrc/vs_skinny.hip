@@ -48,6 +48,26 @@ __device__ __forceinline__ void skinny_glds(const void* sbase, uint32_t voff, ui
       : "memory");
 }
 
+// The same with the non-temporal cache policy: the plane passes stream every
+// row piece once, from one CU (MI355X_MICROARCH.md "nt-weights": nt on a stream
+// that ONE CU reads once).  C3 batch 1 over the int8 plane: 2.80 -> 2.58 ms per
+// query, the pass 2.49 -> 2.29 ms = 0.77 -> 0.84 of HBM (profiles/r06snt, two
+// rounds); the query pieces, which every CU reads, keep the default policy.
+template <bool NT>
+__device__ __forceinline__ void skinny_glds_p(const void* sbase, uint32_t voff, uint32_t lds) {
+  if constexpr (!NT) {
+    skinny_glds(sbase, voff, lds);
+  } else {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds)
+        : "memory");
+  }
+}
+
 constexpr int kSkinnyRows = 128;  // database rows per tile (32 per wave)
 
 // slice images in the ring: 4 for one query group (4 x 18 KB per workgroup),
@@ -297,7 +317,7 @@ constexpr int kPlaneQ = 64;
 constexpr int kPlaneNB = 4;
 constexpr int kPlaneImg = 16384 + 4096;
 
-template <int KL, int EL, int NQG>
+template <int KL, int EL, int NQG, bool NT>
 __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     const char* __restrict__ XH, const char* __restrict__ QH, int nksteps, int ntiles, int ntotal,
     const int* __restrict__ qcount, float* __restrict__ pkey, int* __restrict__ pid, int KP,
@@ -342,8 +362,8 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
     const char* qb = QH + (int64_t)st * 16384;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      skinny_glds(xb + (4 * w + i) * 1024, soff,
-                  __builtin_amdgcn_readfirstlane(base + (uint32_t)(4 * w + i) * 1024u));
+      skinny_glds_p<NT>(xb + (4 * w + i) * 1024, soff,
+                        __builtin_amdgcn_readfirstlane(base + (uint32_t)(4 * w + i) * 1024u));
     // query piece w (NQG = 1: every wave the same piece 0, identical bytes to
     // identical LDS addresses, so every wave issues 5 loads per step)
     const int qp = NQG == 1 ? 0 : w;
@@ -468,6 +488,13 @@ __global__ __launch_bounds__(256, 2) void skinny_plane_topk(
   }
 }
 
+// The plane passes' row pieces with the non-temporal policy (default; env
+// VS_SKINNY_NT=0 keeps the default policy, for A/B; read at every search)
+static bool skinny_nt() {
+  const char* e = getenv("VS_SKINNY_NT");
+  return !e || atoi(e) != 0;
+}
+
 hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64_t ld, int ntotal,
                                const int* qcount, const float* qs, const float* xs, Partials part,
                                hipStream_t st, int nq_hint) {
@@ -480,10 +507,18 @@ hipError_t launch_skinny_plane(int filter, const void* XH, const void* QH, int64
   // nq_hint: the host's bound on the count (0: unknown, up to kPlaneQ): the
   // 16-query variant runs for counts <= 16, the 64-query one above; each exits
   // on the other's counts, so both are launched unless the bound decides
-#define VS_SP(EL_, NQG_)                                                                       \
-  hipLaunchKernelGGL((skinny_plane_topk<8, EL_, NQG_>), dim3(part.P), dim3(256), 0, st,         \
-                     (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount, part.key, \
-                     part.id, part.KP, qs, xs)
+  const bool nt = skinny_nt();
+#define VS_SP(EL_, NQG_)                                                                          \
+  do {                                                                                            \
+    if (nt)                                                                                       \
+      hipLaunchKernelGGL((skinny_plane_topk<8, EL_, NQG_, true>), dim3(part.P), dim3(256), 0, st, \
+                         (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount,       \
+                         part.key, part.id, part.KP, qs, xs);                                    \
+    else                                                                                          \
+      hipLaunchKernelGGL((skinny_plane_topk<8, EL_, NQG_, false>), dim3(part.P), dim3(256), 0,   \
+                         st, (const char*)XH, (const char*)QH, nksteps, ntiles, ntotal, qcount,   \
+                         part.key, part.id, part.KP, qs, xs);                                    \
+  } while (0)
   if (filter == FILTER_I8) {
     VS_SP(FILTER_I8, 1);
     if (nq_hint <= 0 || nq_hint > 16) VS_SP(FILTER_I8, 4);
