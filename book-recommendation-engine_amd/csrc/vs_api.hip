@@ -828,6 +828,9 @@ struct SearchArgs {
   float min_score = 0.0f;
   int raw = 0;                   // VS_RAW_ORDER
   bool l2_direct = false;        // faiss's sequential branch (the call's nq < 20)
+  // the call waits for its results anyway (host outputs): a small batch may
+  // read its device-side count after the first stage and skip the empty rest
+  bool host_wait = false;
   float* D = nullptr;
   int64_t* I = nullptr;
 };
@@ -935,6 +938,13 @@ static int x1_wg_target(int nqt) {
   const char* e = getenv("VS_X1_WGS");
   const int v = e ? atoi(e) : 0;
   return v > 0 ? v : nqt <= 8 ? 256 : 512;
+}
+
+// (env VS_SMALL_SKIP=0 keeps the later stages' launches, for A/B; read at
+// every search)
+static bool small_skip_on() {
+  const char* e = getenv("VS_SMALL_SKIP");
+  return !e || atoi(e) != 0;
 }
 
 int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
@@ -1231,6 +1241,23 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(launch_merge_partials(vmode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
                                a.raw, gl, gc),
          "vs: merge");
+  // A small batch whose call waits for its results anyway (host outputs: the
+  // live search_catalog path, mcp_book_server.py:142): one read of the count
+  // still flagged instead of the later stages' ~30 launches over an empty
+  // count (~4.5 us each, ~0.13 ms of a 2.6-ms C3 batch-1 search)
+  if (small && a.host_wait && small_skip_on()) {
+    int left = -1;
+    VS_HIP(hipMemcpyAsync(&left, qcount + 1, sizeof(int), hipMemcpyDeviceToHost, st),
+           "vs: flags");
+    VS_HIP(hipStreamSynchronize(st), "vs: flags");
+    if (left == 0) {
+      if (!last_plane && plane == FILTER_I8) {
+        int rc = adaptive_record(idx, qcount + 1, nq, st);
+        if (rc) return rc;
+      }
+      return VS_OK;
+    }
+  }
   // what is still flagged (usually nothing: every tile exits), as query ids of `a`
   const int* next = qlist;
   if (gathered) {
@@ -2166,6 +2193,7 @@ int vs_search(vs_index* idx, const float* x, int64_t n, int64_t k, float* D, int
       sa.k = (int)k;
       sa.raw = (flags & VS_RAW_ORDER) ? 1 : 0;
       sa.l2_direct = n < kBlasThreshold;  // faiss decides on the whole call's nq
+      sa.host_wait = !out_dev;
       sa.D = Dd + c0 * k;
       sa.I = Id + c0 * k;
       int rc = run_topk(idx, sa, st, VS_ENGINE_AUTO);
