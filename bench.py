@@ -116,6 +116,11 @@ def rocprof_prefix(kname: str):
         return "void vs::gemm_topk_x1<", "el=1"
     if kname == "gemm_topk_x1":
         return "void vs::gemm_topk_x1<", "el=0"
+    # the small-batch plane pass: skinny_plane_topk<KL, EL, NQG, NT>, EL 1 = int8
+    if kname == "skinny_plane_topk_i8":
+        return "void vs::skinny_plane_topk<", "<8, 1,"
+    if kname == "skinny_plane_topk":
+        return "void vs::skinny_plane_topk<", "<8, 0,"
     return "void vs::" + kname + "<", ""
 
 
