@@ -15,5 +15,5 @@ mkdir -p build_$sfx
   2> build_$sfx/vs_gemm_x1.remarks
 python3 ../../tools/check_no_spill.py build_$sfx/vs_gemm_x1.remarks gemm_topk_x1 || [ -n "${ALLOW_SPILL:-}" ]  # stamp builds: bf16 kernels spill (diagnose int8 only)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../vsearch/libvsearch_$sfx.so \
-  build/vs_api.o build/vs_gemm.o build_$sfx/vs_gemm_x1.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
+  build/vs_api.o build/vs_exact.o build/vs_gemm.o build_$sfx/vs_gemm_x1.o build/vs_gemv.o build/vs_skinny.o build/vs_support.o
 echo "built vsearch/libvsearch_$sfx.so"
