@@ -108,15 +108,6 @@ constexpr int kDumpMaxR = 128;
 #ifndef VS_X1_SEGDMA
 #define VS_X1_SEGDMA 0
 #endif
-// Split fragment reads in the segmented schedule of dump launches (default;
-// A/B builds: -DVS_X1_SPLITRD=0): a step's sub-step 0 fragments are read in
-// the previous step's matrix segment, after its sub-step 0 MFMAs (their
-// registers are free then), so a load segment carries 6 reads beside its DMA
-// pieces instead of 12; the lagging waves stage one step further ahead so that
-// the image those reads need is complete (seg_step below).
-#ifndef VS_X1_SPLITRD
-#define VS_X1_SPLITRD 1
-#endif
 // A hybrid launch (mostly dump tiles) takes the dump launches' schedule.
 constexpr int x1_sched(int el, bool dump, bool hyb = false) {
   return el != FILTER_I8 ? 2 : VS_X1_SCHED_I8 ? VS_X1_SCHED_I8 : dump || hyb ? 2 : 1;
@@ -1036,39 +1027,16 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // the cost is the bytes entering the CU, not the LDS path; s_setprio on
     // either half: -0.1 %; profiles/r04n/ab_qreg_prio.txt: not shipped)
     static_assert(NBUF == 5, "segmented schedule: 3 steps in flight over 5 images");
-    // Split reads (dump launches, VS_X1_SPLITRD): a matrix segment of step s
-    // reads image s+1 (sub-step 0), which must hold every wave's pieces of
-    // step s+1 by then.  Waves 0-3 retire theirs in their load segment of step
-    // s (the barrier before), but waves 4-7 run that segment beside it, so they
-    // run one step further ahead: 4 steps staged, their load segment of step s
-    // retires step s+2 (the same vmcnt(8): two younger steps of 4 pieces in
-    // flight for both groups).  Images: a refill by waves 0-3 (step s+3, phase
-    // 2s) lands on step s-2's image, last read in phase 2s-3 (waves 4-7's load
-    // segment of s-2); a refill by waves 4-7 (step s+4, phase 2s+1) on step
-    // s-1's, last read in phase 2s-1 and consumed by their own MFMAs in phase
-    // 2s; every read of image s+1 (phases 2s+1 / 2s+2) follows both groups'
-    // retires of step s+1 (phases 2s and 2s-1).
-    constexpr bool kSplitRd = DUMP && VS_X1_SPLITRD && !VS_X1_SEGDMA;
-    // VS_X1_SPLITRD=2: sub-step 1 as well, read after the matrix segment's last
-    // MFMAs (its registers free then): a load segment is its DMA pieces alone
-    constexpr bool kSplitRd2 = kSplitRd && VS_X1_SPLITRD >= 2;
-    const bool lag = w >= 4;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       stage_step();
       advance_cursor();
     }
-    if (kSplitRd && lag) {  // uniform
-      stage_step();
-      advance_cursor();
-    }
-    // this wave's pieces of step 0 (split reads, waves 4-7: of steps 0 and 1)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of step 0
     __builtin_amdgcn_s_barrier();
+    const bool lag = w >= 4;
     if (lag) __builtin_amdgcn_s_barrier();  // uniform: one barrier behind
     int buf = 0;
-    if constexpr (kSplitRd) rd(0, 0, fa0, fb0);  // step 0's sub-step 0
-    if constexpr (kSplitRd2) rd(0, 1, fa1, fb1);  // and sub-step 1
 #if VS_X1_STAMP
     tA = stamp_now();
 #define VS_X1_MARK(i) (tB = stamp_now(), sg[i] += tB - tA, tA = tB)
@@ -1080,10 +1048,9 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
     // branch on its position in the tile.
     auto seg_step = [&](auto first_tag) {
       constexpr bool first = decltype(first_tag)::value;
-      const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!kSplitRd) rd(buf, 0, fa0, fb0);  // split reads: read a step earlier
-      if constexpr (!kSplitRd2) rd(buf, 1, fa1, fb1);
+      rd(buf, 0, fa0, fb0);
+      rd(buf, 1, fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
 #if !VS_X1_SEGDMA
       stage_step();
@@ -1110,20 +1077,8 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa0, fb0);
       }
-      if constexpr (kSplitRd) {
-        // the next step's sub-step 0 (its image is complete: see the prologue;
-        // past the end a harmless read of a stale image), into the registers
-        // the MFMAs above have read
-        __builtin_amdgcn_sched_barrier(0);
-        rd(nbuf, 0, fa0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) mfma_rb(rb, fa1, fb1);
-      if constexpr (kSplitRd2) {
-        __builtin_amdgcn_sched_barrier(0);
-        rd(nbuf, 1, fa1, fb1);
-      }
 #else
       {
         // step s+3's pieces into the image of step s-2 (read two barriers ago
@@ -1183,7 +1138,7 @@ __global__ __launch_bounds__(512, 1) void gemm_topk_x1(
       __builtin_amdgcn_sched_barrier(0);
       VS_X1_MARK(4);
       VS_X1_MARK(5);
-      buf = nbuf;
+      buf = buf + 1 == NBUF ? 0 : buf + 1;
     };
     auto seg_tiles = [&](int ta, int tb, auto dm_tag) {
       for (int t = ta; t < tb; ++t) {
