@@ -962,9 +962,9 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   const int L = x1_lane_len();
   // enough lists that their 4*nsplit*L entries cover 16*KF candidates (C4's
   // self-join, KF = 64: 128 lists, which lets the int8 stage settle it: 283k ->
-  // 372k students/s, profiles/r02zc), and the workgroup target below (two per
-  // CU on 256 CUs at C3: 128 lists per query; one per CU up to 8 query tiles).  More lists put
-  // the wide check's floor T (the best last entry of a full list) deeper
+  // 372k students/s, profiles/r02zc), and the workgroup target (x1_wg_target:
+  // two per CU on 256 CUs at C3, 128 lists per query; one per CU up to 8 query
+  // tiles).  More lists put the wide check's floor T (the best last entry of a full list) deeper
   // behind the top-M, which the bound needs on clustered data and on the int8
   // plane (profiles/r02l_ab_split.txt; one workgroup per CU left 0.7 % of the
   // C3 queries to the exact engine on int8)
@@ -1649,7 +1649,7 @@ int run_paged(vs_index* idx, const SearchArgs& a, hipStream_t st, const int* gl,
                "vs: merge launch");
         continue;
       }
-      if (xpages) {  // the active queries in launches of kExactSlots (past the count: exit)
+      if (xpages) {  // the active queries in launches of xslots (past the count: exit)
         ExactStreamArgs ea;
         ea.X = (const float*)idx->codes;
         ea.xn = idx->norms;
