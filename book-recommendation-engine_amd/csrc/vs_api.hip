@@ -964,10 +964,10 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   // self-join, KF = 64: 128 lists, which lets the int8 stage settle it: 283k ->
   // 372k students/s, profiles/r02zc), and the workgroup target (x1_wg_target:
   // two per CU on 256 CUs at C3, 128 lists per query; one per CU up to 8 query
-  // tiles).  More lists put the wide check's floor T (the best last entry of a full list) deeper
-  // behind the top-M, which the bound needs on clustered data and on the int8
-  // plane (profiles/r02l_ab_split.txt; one workgroup per CU left 0.7 % of the
-  // C3 queries to the exact engine on int8)
+  // tiles).  More lists put the wide check's floor T (the best last entry of a
+  // full list) deeper behind the top-M, which the bound needs on clustered data
+  // and on the int8 plane (profiles/r02l_ab_split.txt; one workgroup per CU left
+  // 0.7 % of the C3 queries to the exact engine on int8)
   // Inner product past k = 32 (M = 2k - 1 of 59 .. 127, KF = 64 / 128) takes
   // twice as many lists again: at C3 (B = 4096) k = 30 left 13 queries per
   // search and k = 60 815 to the deep bf16 stage (a 10M-row pass of ~20-30 ms
