@@ -891,8 +891,8 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
 //     clustered data to the bf16 plane), and after the last plane to the exact
 //     fp32 engine (a launch whose tiles past the device-side count exit at
 //     once), whose rows overwrite theirs.
-// The host never waits: counts live in device memory.  `gl` / `gc` (stages
-// after the first): the batch is queries gl[0 .. *gc) of `a`.
+// Counts live in device memory; the host reads one only to skip the later
+// stages when none is left (tail_wait_on).  `gl` / `gc` (stages after the first): the batch is queries gl[0 .. *gc) of `a`.
 // dump launches in the filter pass (default; env VS_X1_DUMP=0 runs every
 // launch as a list launch, for A/B)
 static bool dump_enabled() {
@@ -940,11 +940,35 @@ static int x1_wg_target(int nqt) {
   return v > 0 ? v : nqt <= 8 ? 256 : 512;
 }
 
-// (env VS_SMALL_SKIP=0 keeps the later stages' launches, for A/B; read at
-// every search)
-static bool small_skip_on() {
-  const char* e = getenv("VS_SMALL_SKIP");
-  return !e || atoi(e) != 0;
+// Whether a search reads the count of queries a stage leaves flagged (a 4-byte
+// copy to pinned memory and a wait on the stream) and enqueues the later stages
+// only when some remain.  Host-output calls wait for their results anyway;
+// device-output calls wait too: the later stages over an empty count are ~45
+// launches of ~5 us each (0.25 ms of a 2.39-ms C2 search, 0.58 ms of the
+// 1.25M-row rank's 10.5 ms, profiles/r06tl), far more than the wait.  Not on a
+// capturing stream (a graph keeps every launch).  Env VS_TAIL_WAIT=0 keeps
+// every launch (A/B; read at every search).
+static bool tail_wait_on(const SearchArgs& a, hipStream_t st) {
+  const char* e = getenv("VS_TAIL_WAIT");
+  if (e && atoi(e) == 0) return false;
+  if (a.host_wait) return true;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return cs == hipStreamCaptureStatusNone;
+}
+
+// The device-side count *dcount once the stream has reached this point (one
+// pinned int per host thread).
+static int read_count(const int* dcount, hipStream_t st, int* out) {
+  static thread_local int* pin = nullptr;
+  if (!pin) VS_HIP(hipHostMalloc((void**)&pin, sizeof(int), hipHostMallocPortable), "vs: count");
+  VS_HIP(hipMemcpyAsync(pin, dcount, sizeof(int), hipMemcpyDeviceToHost, st), "vs: count");
+  VS_HIP(hipStreamSynchronize(st), "vs: count");
+  *out = *pin;
+  return VS_OK;
 }
 
 int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipStream_t st,
@@ -1241,18 +1265,17 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(launch_merge_partials(vmode, vp, nq, a.k, idx->id_base, a.min_score, a.D, a.I, a.k, st,
                                a.raw, gl, gc),
          "vs: merge");
-  // A small batch whose call waits for its results anyway (host outputs: the
-  // live search_catalog path, mcp_book_server.py:142): one read of the count
-  // still flagged instead of the later stages' ~30 launches over an empty
-  // count (~4.5 us each, ~0.13 ms of a 2.6-ms C3 batch-1 search)
-  if (small && a.host_wait && small_skip_on()) {
+  // The first stage's and the deep stage's leftovers, read when the call may
+  // wait (tail_wait_on): nothing left, no later stage is enqueued (the live
+  // search_catalog path, mcp_book_server.py:142, at batch 1: ~30 launches,
+  // 0.13 ms of a 2.6-ms search; C2 ~45, 0.25 ms)
+  if ((!gathered || deep) && tail_wait_on(a, st)) {
     int left = -1;
-    VS_HIP(hipMemcpyAsync(&left, qcount + 1, sizeof(int), hipMemcpyDeviceToHost, st),
-           "vs: flags");
-    VS_HIP(hipStreamSynchronize(st), "vs: flags");
+    int rc = read_count(qcount + 1, st, &left);
+    if (rc) return rc;
     if (left == 0) {
-      if (!last_plane && plane == FILTER_I8) {
-        int rc = adaptive_record(idx, qcount + 1, nq, st);
+      if (!last_plane && !gathered && plane == FILTER_I8) {
+        rc = adaptive_record(idx, qcount + 1, nq, st);
         if (rc) return rc;
       }
       return VS_OK;
@@ -1356,6 +1379,7 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
       exact_stream_on() && idx->esize == 4 && exact_stream_nq(idx->ld) > 0 && KP <= 64;
   unsigned long long* dstats = device_stats(idx->device);
   int *fl = nullptr, *fc = nullptr, *ol = nullptr, *ewc = nullptr;
+  int xslots = kExactSlots;
   Partials ep;
   if (stream_ok) {
     VS_HIP(scr.alloc((void**)&fl, (size_t)cap * sizeof(int)), "vs: scratch");
@@ -1364,9 +1388,13 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
     VS_HIP(scr.alloc((void**)&ewc, sizeof(int)), "vs: scratch");
     ep.KP = kp_for(need);
     ep.P = (int)std::min<int64_t>(256, std::max<int64_t>(1, ((int64_t)ntotal + 1023) / 1024));
-    VS_HIP(scr.alloc((void**)&ep.key, (size_t)kExactSlots * ep.P * ep.KP * sizeof(float)),
+    // slots per launch: the whole window when its lists fit in ~256 MB (C3:
+    // one launch triple over an empty count instead of 16), else kExactSlots
+    xslots = (int)std::min<int64_t>(
+        cap, std::max<int64_t>(kExactSlots, ((int64_t)256 << 20) / ((int64_t)ep.P * ep.KP * 8)));
+    VS_HIP(scr.alloc((void**)&ep.key, (size_t)xslots * ep.P * ep.KP * sizeof(float)),
            "vs: scratch");
-    VS_HIP(scr.alloc((void**)&ep.id, (size_t)kExactSlots * ep.P * ep.KP * sizeof(int)),
+    VS_HIP(scr.alloc((void**)&ep.id, (size_t)xslots * ep.P * ep.KP * sizeof(int)),
            "vs: scratch");
   }
   // A small batch (its flagged queries are at most its a.nq <= kSkinnyMaxQ):
@@ -1429,12 +1457,12 @@ int run_gemm_rescored(vs_index* idx, const SearchArgs& a, int need, int KF, int 
     ea.qrow = a.self0 >= 0 ? qrow : nullptr;
     ea.slots = fl;
     ea.count = fc;
-    ea.nslot = kExactSlots;
-    for (int s0 = 0; s0 < cap; s0 += kExactSlots) {
+    ea.nslot = xslots;
+    for (int s0 = 0; s0 < cap; s0 += xslots) {
       ea.s0 = s0;
-      VS_HIP(launch_window_count(fc, s0, kExactSlots, ewc, st), "vs: exact stream");
+      VS_HIP(launch_window_count(fc, s0, xslots, ewc, st), "vs: exact stream");
       VS_HIP(launch_exact_stream(ep.KP, emode, ea, ep, st), "vs: exact stream");
-      VS_HIP(launch_merge_partials(emode, ep, kExactSlots, a.k, idx->id_base, a.min_score, a.D,
+      VS_HIP(launch_merge_partials(emode, ep, xslots, a.k, idx->id_base, a.min_score, a.D,
                                    a.I, a.k, st, a.raw, ol + s0, ewc),
              "vs: merge");
     }
