@@ -251,7 +251,10 @@ class IndexFlat(Index):
     def search_device(self, xq_ptr: int, n: int, k: int, D_ptr: int, I_ptr: int,
                       stream: int = 0, raw: bool = False) -> None:
         """Device-resident search: all buffers are device pointers on this index's
-        device; asynchronous on `stream` (a hipStream_t, 0 = default stream)."""
+        device; stream-ordered on `stream` (a hipStream_t, 0 = default stream).
+        Returns once the first filter stage's count of unsettled queries is read
+        (later stages are enqueued only for queries left; VS_TAIL_WAIT=0 keeps
+        the call fully asynchronous)."""
         flags = _lib.IN_DEVICE | _lib.OUT_DEVICE | (_lib.RAW_ORDER if raw else 0)
         _lib.check(self._lib.vs_search(self._h, ctypes.c_void_p(xq_ptr), int(n), int(k),
                                        ctypes.c_void_p(D_ptr), ctypes.c_void_p(I_ptr), flags,

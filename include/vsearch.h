@@ -164,7 +164,10 @@ int vs_set_id_base(vs_index* idx, int64_t id_base);
  * pages where the k-th key's run of equal keys fills a page).  Any k > 0
  * (k > ntotal pads; k > INT_MAX/2: VS_E_INVALID).  L2 calls with n < 20 use faiss's sequential branch (direct sum of
  * squares), n >= 20 the BLAS branch (|q|^2 + |x|^2 - 2 q.x clamped at 0).
- * Asynchronous on `stream` when every buffer is on the device (no host wait).
+ * Stream-ordered on `stream` when every buffer is on the device; the call
+ * returns once its first filter stage's count of unsettled queries is known
+ * (a 4-byte read; later stages are enqueued only for queries left; env
+ * VS_TAIL_WAIT=0 or a capturing stream: fully asynchronous, every launch kept).
  * Caller: FAISS.similarity_search_with_score_by_vector, reached from
  * src/recommendation_api/mcp_book_server.py:142, candidate_builder.py:187,321,
  * service.py:529,627.  D is n*k float32, I is n*k int64. */
