@@ -1224,6 +1224,8 @@ int run_filter_verify(vs_index* idx, const SearchArgs& a, int need, int KF, hipS
   VS_HIP(scr.alloc((void**)&Ik, (size_t)nq * KF * sizeof(int64_t)), "vs: scratch");
   if (KF > 64) {  // 2k - 1 > 64 (inner product, k > 32): the select kernel
     VS_HIP(launch_select_lists(part, L, nq, KF, Dk, Ik, st, gc), "vs: merge");
+  } else if (select_heads_applies(part, L, KF)) {
+    VS_HIP(launch_select_heads(part, nq, KF, Dk, Ik, st, gc), "vs: merge");
   } else {
     Partials mp = part;
     mp.KP = kp_for(KF);

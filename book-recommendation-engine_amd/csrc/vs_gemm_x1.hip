@@ -1334,11 +1334,15 @@ static bool x1_hybrid_on() {
 // (profiles/r04t/ab_chunk.txt).  Env VS_X1_CHUNK_TILES overrides both (read at
 // every search: A/B runs, and tests that need multi-launch passes on small
 // indexes).
+// (round 6: 40-tile launches there, four of them for the 1.25M-row rank —
+// one list launch, three dumps — instead of five 32-tile ones: 460.5k vs
+// 447.6k / 451.6k queries/s, profiles/r06rc)
+constexpr int kX1ShortChunkTiles = 40;
 static int x1_chunk_tiles(int per_block, bool can_dump) {
   const char* e = getenv("VS_X1_CHUNK_TILES");
   const int v = e ? atoi(e) : 0;
   if (v > 0) return v;
-  return can_dump && per_block >= 128 && per_block <= 3 * kX1ChunkTiles ? kX1ChunkTiles / 2
+  return can_dump && per_block >= 128 && per_block <= 3 * kX1ChunkTiles ? kX1ShortChunkTiles
                                                                         : kX1ChunkTiles;
 }
 
@@ -2283,7 +2287,10 @@ __device__ __forceinline__ double wave_dot(const RT* __restrict__ x, const float
 // The same sums for two rows at once against a query whose slice of this lane
 // sits in registers (ld <= 256 kQV): every load of both rows is issued before
 // the first FMA (one memory round trip per pair instead of one per 1 KB), and
-// each row's terms are added in wave_dot's order (identical results).
+// each row's terms are added in wave_dot's order (identical results).  (Four
+// rows per step: the first check 51 vs 54 us at C2, the wide check 194 vs 130
+// us at one wave per SIMD, profiles/r06tl2: both are bound by the rows' HBM
+// gathers, ~3-4 TB/s.)
 constexpr int kQV = 8;
 struct QSlice {
   f32x4 v[kQV];
@@ -3011,6 +3018,111 @@ hipError_t launch_select_lists(Partials part, int L, int nq, int KF, float* Dk, 
   if (nq <= 0) return hipSuccess;
   hipLaunchKernelGGL(select_lists_kernel, dim3(nq), dim3(256), 0, st, part.key, part.id, part.P,
                      part.KP, L, KF, Dk, Ik, qcount);
+  return hipGetLastError();
+}
+
+// The KF <= 64 best approximate candidates of each query from its P sorted
+// lane lists of 8 entries (stride 8), by a bound from the lists' heads instead
+// of merge_lists_kernel's six rounds of 32-entry merges (C2: 35-38 us vs the
+// merge's 94 in two levels, profiles/r06tl2).  The KF-th smallest head U (lexicographic (key, row);
+// a query's lists hold distinct rows) bounds the KF-th smallest entry: the KF
+// lists of the smallest heads hold KF entries <= U.  Only those lists can hold
+// an entry <= U, so at most 8 KF entries (<= 512) are kept and ranked.  Fewer
+// than KF non-empty lists: every entry is kept.  Same output as the merge:
+// Dk/Ik [nq][KF] ascending, (FLT_MAX, -1) padding.
+constexpr int kHeadsMaxP = 512;
+constexpr int kHeadsMaxKF = 64;
+__global__ __launch_bounds__(256) void select_heads_kernel(const float* __restrict__ lkey,
+                                                           const int* __restrict__ lid, int P,
+                                                           int KF, float* __restrict__ Dk,
+                                                           int64_t* __restrict__ Ik,
+                                                           const int* __restrict__ qcount) {
+  __shared__ float hk[kHeadsMaxP];
+  __shared__ int hi[kHeadsMaxP];
+  __shared__ float ck[8 * kHeadsMaxKF];
+  __shared__ int ci[8 * kHeadsMaxKF];
+  __shared__ int cnt, ui;
+  __shared__ float uk;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (qcount && q >= *qcount) return;  // gathered batch: slots past the count
+  const int64_t base = (int64_t)q * P * 8;
+  for (int p = tid; p < P; p += 256) {
+    hk[p] = lkey[base + (int64_t)p * 8];
+    hi[p] = lid[base + (int64_t)p * 8];
+  }
+  if (tid == 0) {
+    cnt = 0;
+    ui = -1;  // no bound: fewer than KF non-empty lists
+    uk = FLT_MAX;
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += 256) {
+    const float k0 = hk[p];
+    const int i0 = hi[p];
+    if (i0 < 0) continue;
+    int r = 0;
+    for (int t = 0; t < P; ++t) r += hi[t] >= 0 && lex_less(hk[t], hi[t], k0, i0) ? 1 : 0;
+    if (r == KF - 1) {
+      uk = k0;
+      ui = i0;
+    }
+  }
+  __syncthreads();
+  const float U = uk;
+  const int Ui = ui;
+  for (int p = tid; p < P; p += 256) {
+    if (Ui >= 0 && lex_less(U, Ui, hk[p], hi[p])) continue;  // head above the bound
+    const f32x4* kp = (const f32x4*)(lkey + base + (int64_t)p * 8);
+    const int4* ip = (const int4*)(lid + base + (int64_t)p * 8);
+    const f32x4 ka = kp[0], kb = kp[1];
+    const int4 ia = ip[0], ib = ip[1];
+    const float kk[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+    const int ii[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (ii[j] < 0 || (Ui >= 0 && lex_less(U, Ui, kk[j], ii[j]))) break;  // sorted: the rest too
+      const int s = atomicAdd(&cnt, 1);
+      if (s < 8 * kHeadsMaxKF) {
+        ck[s] = kk[j];
+        ci[s] = ii[j];
+      }
+    }
+  }
+  __syncthreads();
+  // <= 8 KF: at most KF lists pass the head test when bounded
+  const int n = min(cnt, 8 * kHeadsMaxKF);
+  float* dk = Dk + (int64_t)q * KF;
+  int64_t* ik = Ik + (int64_t)q * KF;
+  for (int j = tid; j < n; j += 256) {
+    const float k0 = ck[j];
+    const int i0 = ci[j];
+    int r = 0;
+    for (int t = 0; t < n; ++t) r += lex_less(ck[t], ci[t], k0, i0) ? 1 : 0;
+    if (r < KF) {
+      dk[r] = k0;
+      ik[r] = i0;
+    }
+  }
+  for (int j = n + tid; j < KF; j += 256) {
+    dk[j] = FLT_MAX;
+    ik[j] = -1;
+  }
+}
+
+bool select_heads_applies(const Partials& part, int L, int KF) {
+  const char* e = getenv("VS_SELECT_HEADS");  // =0: the list merge (A/B; read at every search)
+  if (e && atoi(e) == 0) return false;
+  return L == 8 && part.KP == 8 && KF >= 1 && KF <= kHeadsMaxKF && part.P >= KF &&
+         part.P <= kHeadsMaxP;
+}
+
+hipError_t launch_select_heads(Partials part, int nq, int KF, float* Dk, int64_t* Ik,
+                               hipStream_t st, const int* qcount) {
+  if (!select_heads_applies(part, 8, KF)) return hipErrorInvalidValue;
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(select_heads_kernel, dim3(nq), dim3(256), 0, st, part.key, part.id, part.P,
+                     KF, Dk, Ik, qcount);
   return hipGetLastError();
 }
 

@@ -307,6 +307,11 @@ constexpr int kVerifyMaxKF = 1024;
 // [nq][KF] (the approximate merge when KF > 64; launch_merge_partials below).
 hipError_t launch_select_lists(Partials part, int L, int nq, int KF, float* Dk, int64_t* Ik,
                                hipStream_t st, const int* qcount = nullptr);
+// The same for KF <= 64 from lane lists of L = 8 (stride 8) by a bound from the
+// lists' heads (P >= KF, P <= 512; select_heads_applies), else the list merge.
+bool select_heads_applies(const Partials& part, int L, int KF);
+hipError_t launch_select_heads(Partials part, int nq, int KF, float* Dk, int64_t* Ik,
+                               hipStream_t st, const int* qcount = nullptr);
 
 // Scratch chunks (vs_api.hip): device memory of at least `bytes` whose previous
 // use the taker's stream `st` waits for; put records the chunk's last use on

@@ -830,6 +830,43 @@ def test_staged_engine_hands_clustered_queries_to_bf16(vf):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("metric,k", [(IP, 10), (IP, 30), (flat.METRIC_L2, 10), (flat.METRIC_L2, 20)])
+def test_select_heads_matches_list_merge(vf, metric, k, monkeypatch):
+    """The first stage's candidate selection from the lane lists' heads
+    (select_heads_kernel: the KF-th smallest head bounds the KF-th entry) gives
+    the list merge's candidates: the same (D, I) and the same wide-check
+    counts with VS_SELECT_HEADS=0, on rows with clusters of near-copies (lists
+    whose every entry is below the bound) and exact against the oracle."""
+    from vsearch import _lib
+
+    rng = np.random.default_rng(77)
+    d = 128
+    xb = rng.uniform(-1, 1, (300_000, d)).astype(np.float32)
+    hard = rng.uniform(-1, 1, (16, d)).astype(np.float32)
+    pos = rng.choice(xb.shape[0], (16, 300), replace=False)
+    for j in range(16):
+        xb[pos[j]] = (hard[j] + 0.02 * rng.standard_normal((300, d))).astype(np.float32)
+    xq = rng.uniform(-1, 1, (1024, d)).astype(np.float32)
+    xq[:16] = hard + 0.01 * rng.standard_normal((16, d)).astype(np.float32)
+    index = vf.IndexFlatL2(d) if metric == flat.METRIC_L2 else vf.IndexFlatIP(d)
+    index.add(xb)
+    out = {}
+    for sel in ("1", "0"):
+        monkeypatch.setenv("VS_SELECT_HEADS", sel)
+        _lib.filter_stats(reset=True)
+        D, I = index.search(xq, k)
+        out[sel] = (D, I, _lib.filter_wide_stats())
+        _lib.filter_stats(reset=True)
+    assert np.array_equal(out["1"][1], out["0"][1])
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][2] == out["0"][2]
+    rows = np.concatenate([np.arange(16), np.arange(16, 1024, 97)])
+    Dr, Ir = flat.knn_exact(xb, xq[rows], k, metric)
+    bad = flat.mismatches(out["1"][0][rows], out["1"][1][rows], Dr, Ir, metric, xb, xq[rows],
+                          strict=True)
+    assert not bad, bad[:5]
+
+
 def test_deep_stage_few_queries_skinny(vf, monkeypatch):
     """A few hard queries in a large batch (40 of 4,096, each beside 200
     near-copies of its own direction): the int8 checks hand them on, and the
