@@ -130,3 +130,47 @@ def test_writer_of_one_index_does_not_drain_another():
     assert not flat.mismatches(Da, Ia, Dr, Ir, flat.METRIC_INNER_PRODUCT, xr, xa[:300], strict=True)
     Db, Ib = big.search(xq[:512].cpu().numpy(), k)
     assert (Ib == I[:512].cpu().numpy()).all()
+
+
+def test_tail_wait_keeps_device_results(monkeypatch):
+    """Device-output searches read their first stage's leftover count and
+    enqueue the later stages only when queries remain (vs_api.hip
+    tail_wait_on).  With queries beside 200 near-copies of their own direction
+    (the int8 checks hand them on: the later stages run) and without (nothing
+    left: the search ends after its first stage), the lists equal those of
+    VS_TAIL_WAIT=0 (every launch kept) and of the host-output path."""
+    import torch
+
+    from vsearch import faiss as vfaiss
+
+    rng = np.random.default_rng(5)
+    d = 256
+    xb = rng.uniform(-1, 1, (300_000, d)).astype(np.float32)
+    hard = rng.uniform(-1, 1, (8, d)).astype(np.float32)
+    pos = rng.choice(xb.shape[0], (8, 200), replace=False)
+    for j in range(8):
+        xb[pos[j]] = (hard[j] * (1.0 + 0.02 * rng.uniform(0, 1, (200, 1)))
+                      + 0.01 * rng.standard_normal((200, d))).astype(np.float32)
+    index = vfaiss.IndexFlatIP(d)
+    index.add(xb)
+    st = torch.cuda.Stream()
+    for nq, nh in ((512, 8), (512, 0), (16, 3), (1, 0)):
+        xq = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+        xq[:nh] = hard[:nh] + 0.01 * rng.standard_normal((nh, d)).astype(np.float32)
+        q = torch.from_numpy(xq).cuda()
+        out = {}
+        for tw in ("1", "0"):
+            monkeypatch.setenv("VS_TAIL_WAIT", tw)
+            D = torch.empty(nq, 10, device="cuda")
+            I = torch.empty(nq, 10, dtype=torch.int64, device="cuda")
+            st.wait_stream(torch.cuda.current_stream())  # q's copy
+            with torch.cuda.stream(st):
+                index.search_device(q.data_ptr(), nq, 10, D.data_ptr(), I.data_ptr(),
+                                    stream=st.cuda_stream)
+            st.synchronize()
+            out[tw] = (D.cpu().numpy(), I.cpu().numpy())
+        monkeypatch.delenv("VS_TAIL_WAIT")
+        Dh, Ih = index.search(xq, 10)
+        for tw in ("1", "0"):
+            assert np.array_equal(out[tw][1], Ih), (nq, nh, tw)
+            assert np.array_equal(out[tw][0], Dh), (nq, nh, tw)
