@@ -1253,13 +1253,16 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
   const float cut = qcut[q];
   const float qsc = EL == FILTER_I8 ? qs[q] : 0.0f;
   const int selfrow = self0 >= 0 ? (int)(self0 + q) : -1;
+  static_assert(KR % 4 == 0, "lane lists move as 16-B pieces");
   float lk[KR];
   int li[KR];
-  const int64_t o = i * KP;
+  const int64_t o = i * KP;  // KP: a multiple of 4 (launch_x1_replay)
 #pragma unroll
-  for (int e = 0; e < KR; ++e) {
-    lk[e] = pkey[o + e];
-    li[e] = pid[o + e];
+  for (int e = 0; e < KR; e += 4) {
+    const f32x4 kv = *(const f32x4*)(pkey + o + e);
+    const int4 iv = *(const int4*)(pid + o + e);
+    lk[e] = kv.x, lk[e + 1] = kv.y, lk[e + 2] = kv.z, lk[e + 3] = kv.w;
+    li[e] = iv.x, li[e + 1] = iv.y, li[e + 2] = iv.z, li[e + 3] = iv.w;
   }
   // the list's slots c = 0 .. cnt-1 at dslot[c * nl + i] (slot-major), eight
   // at a time: their loads, then their rows' factors, then the admissions in
@@ -1283,9 +1286,9 @@ __global__ __launch_bounds__(256) void x1_replay_kernel(
     }
   }
 #pragma unroll
-  for (int e = 0; e < KR; ++e) {
-    pkey[o + e] = lk[e];
-    pid[o + e] = li[e];
+  for (int e = 0; e < KR; e += 4) {
+    *(f32x4*)(pkey + o + e) = f32x4{lk[e], lk[e + 1], lk[e + 2], lk[e + 3]};
+    *(int4*)(pid + o + e) = make_int4(li[e], li[e + 1], li[e + 2], li[e + 3]);
   }
 }
 
@@ -1552,7 +1555,7 @@ bool x1_dump_applies(int mode, int filter) {
 hipError_t launch_x1_replay(const X1Args& a, Partials part, hipStream_t st) {
   unsigned long long* stats = a.dstats;
   if (!a.dump || !a.dcount || a.nqa <= 0) return hipSuccess;
-  if (part.KP < x1_lane_len()) return hipErrorInvalidValue;
+  if (part.KP < x1_lane_len() || part.KP % 4 != 0) return hipErrorInvalidValue;
   const int64_t n = (int64_t)a.nqa * part.P;
   const dim3 grid((unsigned)((n + 255) / 256));
   const int64_t nl = (int64_t)a.nq_pad * part.P;  // lists of the pass (the slots' stride)
